@@ -1,0 +1,941 @@
+// ctws_api.cpp — host side of libctws.so: the C-ABI of include/ctws.h.
+//
+// Replaces the block loop of the reference job entry (cluster_tools/watershed/watershed.py:
+// 380-381, `for block_id in block_list: _ws_block(...)`) with batched launches: all blocks of
+// a batch go through one pipeline of gfx950 kernels (grid.y = block), so even a single job
+// fills the 256 CUs.  The caller keeps the dataset I/O and the "processed block" log protocol.
+//
+// Pipeline per batch (kernel files in brackets):
+//   input min/max -> normalize + threshold + EDT x  [k_edt]     (_read_data, _apply_dt)
+//   EDT y [, z] -> dt, dt min/max                    [k_edt]
+//   Gaussian(sigma_seeds) of dt                      [k_gauss]   (_make_seeds)
+//   hmap + Gaussian(sigma_weights)                   [k_gauss]   (_make_hmap)
+//   local maxima, plateaus, seed CC, scan-order ids  [k_cc]
+//   seeded flood                                     [k_flood]   (watershedsNew)
+//   size filter + regrow flood                       [k_post, k_flood] (apply_size_filter)
+//   2-D slice offsets / mask                         [k_post]    (_apply_watershed)
+//   halo crop CC + uint64 offset                     [k_cc]      (_ws_block :326-341)
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/ctws.h"
+#include "ctws_kernels.h"
+
+using namespace ctws;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct Workspace {
+    int64_t cap_vox = 0, cap_words = 0, cap_chunks = 0, cap_slices = 0, cap_tiles = 0, cap_blocks = 0;
+    float *fin = nullptr, *dt = nullptr, *A = nullptr, *Bf = nullptr, *sm = nullptr, *hm = nullptr;
+    uint8_t* cls = nullptr;
+    uint32_t *P = nullptr, *PF = nullptr, *lab = nullptr;
+    uint64_t* key = nullptr;
+    uint64_t* W = nullptr;
+    uint32_t *Wp = nullptr, *csum = nullptr;
+    uint32_t *smin = nullptr, *smax = nullptr, *sb = nullptr, *slmax = nullptr, *soff = nullptr, *surv = nullptr;
+    uint8_t *act0 = nullptr, *act1 = nullptr;
+    BlockDesc* desc = nullptr;
+    BlockStat* stat = nullptr;
+    uint32_t* counter = nullptr;
+    double* taps = nullptr;  // [6][128]
+};
+
+constexpr int kMaxTaps = 127;  // radius <= 63
+
+}  // namespace
+
+struct ctws_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    Workspace ws;
+    uint32_t* h_counter = nullptr;  // pinned
+    double* h_taps = nullptr;       // pinned [6][128]
+    std::vector<std::pair<const char*, float>> timings;
+    std::vector<hipEvent_t> events;
+    // host-pointer staging
+    DevBuf st_in, st_mask, st_init, st_out;
+    // test hooks
+    int stop_after = 0;
+    std::vector<BlockDesc> last_desc;
+    // RCCL
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+namespace {
+
+#define HIPCHK(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            h->err = std::string(#expr) + ": " + hipGetErrorString(e_);                  \
+            return CTWS_EHIP;                                                            \
+        }                                                                                \
+    } while (0)
+
+#define LAUNCHCHK()                                                                      \
+    do {                                                                                 \
+        hipError_t e_ = hipGetLastError();                                               \
+        if (e_ != hipSuccess) {                                                          \
+            h->err = std::string("kernel launch: ") + hipGetErrorString(e_);             \
+            return CTWS_EHIP;                                                            \
+        }                                                                                \
+    } while (0)
+
+template <class T>
+int dev_alloc(ctws_handle* h, T*& p, int64_t n) {
+    if (p) {
+        hipFree(p);
+        p = nullptr;
+    }
+    if (n <= 0) n = 1;
+    hipError_t e = hipMalloc((void**)&p, sizeof(T) * (size_t)n);
+    if (e != hipSuccess) {
+        h->err = std::string("hipMalloc(") + std::to_string(sizeof(T) * (size_t)n) + "): " + hipGetErrorString(e);
+        p = nullptr;
+        return CTWS_ENOMEM;
+    }
+    return CTWS_OK;
+}
+
+int grow(ctws_handle* h, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes) return CTWS_OK;
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipMalloc(&b.p, std::max<size_t>(bytes, 16)) != hipSuccess) {
+        h->err = "hipMalloc staging failed (" + std::to_string(bytes) + " bytes)";
+        return CTWS_ENOMEM;
+    }
+    b.bytes = bytes;
+    return CTWS_OK;
+}
+
+int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks, int64_t slices, int64_t tiles,
+                     int64_t blocks) {
+    Workspace& w = h->ws;
+    int r = CTWS_OK;
+#define ALLOC(field, n) \
+    if ((r = dev_alloc(h, w.field, (n))) != CTWS_OK) return r
+    if (vox > w.cap_vox) {
+        vox = std::max<int64_t>(vox, w.cap_vox + w.cap_vox / 4);
+        ALLOC(fin, vox);
+        ALLOC(dt, vox);
+        ALLOC(A, vox);
+        ALLOC(Bf, vox);
+        ALLOC(sm, vox);
+        ALLOC(hm, vox);
+        ALLOC(cls, vox);
+        ALLOC(P, vox);
+        ALLOC(PF, vox);
+        ALLOC(lab, vox);
+        ALLOC(key, vox);
+        w.cap_vox = vox;
+    }
+    if (words > w.cap_words) {
+        ALLOC(W, words);
+        ALLOC(Wp, words);
+        w.cap_words = words;
+    }
+    if (chunks > w.cap_chunks) {
+        ALLOC(csum, chunks);
+        w.cap_chunks = chunks;
+    }
+    if (slices > w.cap_slices) {
+        ALLOC(smin, slices);
+        ALLOC(smax, slices);
+        ALLOC(sb, slices);
+        ALLOC(slmax, slices);
+        ALLOC(soff, slices);
+        ALLOC(surv, slices);
+        w.cap_slices = slices;
+    }
+    if (tiles > w.cap_tiles) {
+        ALLOC(act0, tiles);
+        ALLOC(act1, tiles);
+        w.cap_tiles = tiles;
+    }
+    if (blocks > w.cap_blocks) {
+        ALLOC(desc, blocks);
+        ALLOC(stat, blocks);
+        w.cap_blocks = blocks;
+    }
+    if (!w.counter) ALLOC(counter, 4);
+    if (!w.taps) ALLOC(taps, 6 * 128);
+#undef ALLOC
+    return CTWS_OK;
+}
+
+// vigra Kernel1D<double>::initGaussian(sigma, 1.0) (restated; taps for offsets -r..r)
+std::vector<double> gaussian_taps(double sigma) {
+    std::vector<double> k;
+    if (sigma > 0.0) {
+        const double sigma2 = -0.5 / sigma / sigma;
+        const double norm = 1.0 / (std::sqrt(2.0 * M_PI) * sigma);
+        int radius = (int)(3.0 * sigma + 0.5);
+        if (radius == 0) radius = 1;
+        for (double x = -(double)radius; x <= (double)radius; ++x) {
+            const double x2 = x * x;
+            k.push_back(norm * std::exp(x2 * sigma2));
+        }
+    } else {
+        k.push_back(1.0);
+    }
+    double sum = 0.0;
+    for (double v : k) sum += v;
+    sum = 1.0 / sum;
+    for (double& v : k) v = v * sum;
+    return k;
+}
+
+struct BlockIO {
+    const void* in;
+    const uint8_t* mask;
+    const uint64_t* init;
+    uint64_t* out;
+};
+
+struct Plan {
+    // validated, derived configuration
+    int nd_ws, dt_2d;
+    int pitch[3];
+    bool seeds_smooth, weights_smooth;
+    double sig_seeds[3], sig_weights[3];
+};
+
+int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
+    p.nd_ws = cfg->apply_ws_2d ? 2 : 3;
+    p.dt_2d = cfg->apply_dt_2d ? 1 : 0;
+    if (cfg->pass_id != 0) {
+        h->err = "two-pass pass 1 (_ws_pass2) is not implemented in this build";
+        return CTWS_EUNSUPPORTED;
+    }
+    for (int k = 0; k < 3; ++k) p.pitch[k] = 1;
+    if (cfg->has_pixel_pitch) {
+        if (p.dt_2d) {
+            h->err = "apply_dt_2d requires pixel_pitch None (watershed.py:151)";
+            return CTWS_EINVAL;
+        }
+        for (int k = 0; k < 3; ++k) {
+            const double v = cfg->pixel_pitch[k];
+            if (v != std::floor(v) || v < 1.0 || v > 1000.0) {
+                h->err = "non-integer pixel_pitch is not supported by the exact integer EDT";
+                return CTWS_EUNSUPPORTED;
+            }
+            p.pitch[k] = (int)v;
+        }
+    }
+    auto sig = [&](const double* s, int is_list, double* out, bool& en) -> int {
+        en = is_list ? true : (s[0] != 0.0);
+        if (is_list && p.nd_ws == 2) {
+            h->err = "per-axis sigma needs a 3-D watershed (volume_utils.py:97-98)";
+            return CTWS_EINVAL;
+        }
+        for (int k = 0; k < 3; ++k) {
+            out[k] = is_list ? s[k] : s[0];
+            if (out[k] < 0.0) {
+                h->err = "negative sigma";
+                return CTWS_EINVAL;
+            }
+            if ((int)(3.0 * out[k] + 0.5) > 63) {
+                h->err = "sigma too large (radius > 63)";
+                return CTWS_EUNSUPPORTED;
+            }
+        }
+        return CTWS_OK;
+    };
+    int r;
+    if ((r = sig(cfg->sigma_seeds, cfg->sigma_seeds_is_list, p.sig_seeds, p.seeds_smooth)) != CTWS_OK) return r;
+    if ((r = sig(cfg->sigma_weights, cfg->sigma_weights_is_list, p.sig_weights, p.weights_smooth)) != CTWS_OK)
+        return r;
+    return CTWS_OK;
+}
+
+int col_width(int L) { return L <= 512 ? 32 : (L <= 1024 ? 16 : 8); }
+
+void record(ctws_handle* h, size_t idx) {
+    while (h->events.size() <= idx) {
+        hipEvent_t e;
+        hipEventCreate(&e);
+        h->events.push_back(e);
+    }
+    hipEventRecord(h->events[idx], h->stream);
+}
+
+// ---- Gaussian passes over the active axes, z -> y -> x --------------------------------------
+int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, const float* src, float* dst,
+              int nb, int maxZ, int maxY, int maxX, HmapParams hp, int taps_slot) {
+    Workspace& w = h->ws;
+    int axes[3], na = 0;
+    for (int a = (pl.nd_ws == 3 ? 0 : 1); a < 3; ++a)
+        if (sig[a] > 0.0) axes[na++] = a;
+    if (na == 0) {
+        if (hmap_src) {
+            dim3 g((unsigned)std::min<int64_t>(((int64_t)maxZ * maxY * maxX + 255) / 256, 4096), nb);
+            k_hmap<<<g, 256, 0, h->stream>>>(w.desc, w.stat, hp, w.fin, w.dt, w.smin, w.smax, dst);
+            LAUNCHCHK();
+        } else if (src != dst) {
+            // identity smoothing: the caller reads `src`
+        }
+        return CTWS_OK;
+    }
+    const float* cur = src;
+    for (int i = 0; i < na; ++i) {
+        const int a = axes[i];
+        auto taps = gaussian_taps(sig[a]);
+        const int r = (int)taps.size() / 2;
+        const int L = a == 0 ? maxZ : (a == 1 ? maxY : maxX);
+        (void)L;
+        double* dtaps = w.taps + (taps_slot * 3 + a) * 128;
+        double* htaps = h->h_taps + (taps_slot * 3 + a) * 128;
+        std::memcpy(htaps, taps.data(), sizeof(double) * taps.size());
+        HIPCHK(hipMemcpyAsync(dtaps, htaps, sizeof(double) * taps.size(), hipMemcpyHostToDevice, h->stream));
+        float* out = (i == na - 1) ? dst : ((i % 2 == 0) ? w.A : w.Bf);
+        GaussParams gp{a, r, (i == 0 && hmap_src) ? 1 : 0};
+        const float* in = (i == 0 && hmap_src) ? w.fin : cur;
+        if (a == 2) {
+            dim3 g((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
+            const size_t lds = 2 * 128 * 4 + 4 * (size_t)maxX * 4;
+            k_gauss_row<<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax, out);
+        } else {
+            const int Lm = a == 0 ? maxZ : maxY;
+            const int other = a == 0 ? maxY : maxZ;
+            const int W = col_width(Lm);
+            dim3 g((unsigned)((int64_t)other * ((maxX + W - 1) / W)), nb);
+            const size_t lds = 2 * 128 * 4 + (size_t)Lm * W * 4;
+            if (W == 32)
+                k_gauss_col<32><<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax,
+                                                            out);
+            else if (W == 16)
+                k_gauss_col<16><<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax,
+                                                            out);
+            else
+                k_gauss_col<8><<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax,
+                                                           out);
+        }
+        LAUNCHCHK();
+        cur = out;
+    }
+    return CTWS_OK;
+}
+
+// ---- flood rounds until no tile is active -----------------------------------------------
+int run_flood(ctws_handle* h, int nd, int nb, int max_tiles, int64_t ntiles, const float* hm, int* rounds_out) {
+    Workspace& w = h->ws;
+    HIPCHK(hipMemsetAsync(w.act0, 1, (size_t)ntiles, h->stream));
+    HIPCHK(hipMemsetAsync(w.act1, 0, (size_t)ntiles, h->stream));
+    uint8_t* cur = w.act0;
+    uint8_t* nxt = w.act1;
+    dim3 g((unsigned)max_tiles, nb);
+    int round = 0;
+    for (; round < 1000000; ++round) {
+        HIPCHK(hipMemsetAsync(w.counter, 0, 4, h->stream));
+        if (nd == 3)
+            k_flood<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
+        else
+            k_flood<2><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
+        LAUNCHCHK();
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        if (*h->h_counter == 0) break;
+        HIPCHK(hipMemsetAsync(cur, 0, (size_t)ntiles, h->stream));
+        std::swap(cur, nxt);
+    }
+    if (rounds_out) *rounds_out = round + 1;
+    return CTWS_OK;
+}
+
+int64_t words_of(int64_t n) { return n / 64 + 1; }
+int64_t chunks_of(int64_t n) { return (words_of(n) + 255) / 256; }
+
+// ---- one batch, all pointers on the device ------------------------------------------------
+int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* blocks, const BlockIO* io, int nb) {
+    Workspace& w = h->ws;
+    std::vector<BlockDesc> desc(nb);
+    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0;
+    int maxZ = 0, maxY = 0, maxX = 0, max_tiles = 0;
+    int64_t maxN = 0, maxNI = 0;
+    const int TZ = pl.nd_ws == 3 ? 4 : 1, TY = pl.nd_ws == 3 ? 8 : 32, TX = 64;
+    const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
+    for (int i = 0; i < nb; ++i) {
+        const ctws_block& b = blocks[i];
+        BlockDesc& d = desc[i];
+        std::memset(&d, 0, sizeof(d));
+        d.Z = (int)b.outer_shape[0];
+        d.Y = (int)b.outer_shape[1];
+        d.X = (int)b.outer_shape[2];
+        d.nd_ws = pl.nd_ws;
+        d.N = (int64_t)d.Z * d.Y * d.X;
+        d.base = T;
+        d.iz0 = (int)b.inner_begin[0];
+        d.iy0 = (int)b.inner_begin[1];
+        d.ix0 = (int)b.inner_begin[2];
+        d.IZ = (int)b.inner_shape[0];
+        d.IY = (int)b.inner_shape[1];
+        d.IX = (int)b.inner_shape[2];
+        d.NI = (int64_t)d.IZ * d.IY * d.IX;
+        d.crop = b.crop_relabel ? 1 : 0;
+        d.ibase = T;  // inner arrays reuse the outer-sized parent array (NI <= N)
+        d.wbase = TW;
+        d.cbase = TC;
+        d.sbase = TS;
+        d.input = io[i].in;
+        d.mask = io[i].mask;
+        d.init = io[i].init;
+        d.out = io[i].out;
+        d.n_channels = b.n_channels;
+        d.dtype = b.input_dtype;
+        if (b.n_channels > 0) {
+            int cb = cfg->channel_begin, ce = cfg->channel_end < 0 ? b.n_channels : cfg->channel_end;
+            if (cb < 0) cb += b.n_channels;
+            if (ce > b.n_channels) ce = b.n_channels;
+            if (cb > ce) cb = ce;
+            d.c0 = cb;
+            d.C = ce - cb;
+            if (d.C <= 0) {
+                h->err = "empty channel range";
+                return CTWS_EINVAL;
+            }
+        } else {
+            d.c0 = 0;
+            d.C = 1;
+        }
+        d.id_offset = (uint64_t)b.block_id * bvol;
+        d.tz = (d.Z + TZ - 1) / TZ;
+        d.ty = (d.Y + TY - 1) / TY;
+        d.tx = (d.X + TX - 1) / TX;
+        d.tbase = (int)TT;
+        d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
+                            (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
+        T += d.N;
+        TI += d.NI;
+        TW += words_of(d.N);
+        TC += chunks_of(d.N);
+        TS += d.Z;
+        TT += (int64_t)d.tz * d.ty * d.tx;
+        maxZ = std::max(maxZ, d.Z);
+        maxY = std::max(maxY, d.Y);
+        maxX = std::max(maxX, d.X);
+        maxN = std::max(maxN, d.N);
+        maxNI = std::max(maxNI, d.NI);
+        max_tiles = std::max(max_tiles, d.tz * d.ty * d.tx);
+        // validation against what the kernels assume
+        if (d.X > 1024 || d.Y > 2048 || d.Z > 2048 || d.N >= (1ll << 31)) {
+            h->err = "outer block too large for the kernels (X <= 1024, Y, Z <= 2048, N < 2^31)";
+            return CTWS_EUNSUPPORTED;
+        }
+        if (d.iz0 < 0 || d.iy0 < 0 || d.ix0 < 0 || d.iz0 + d.IZ > d.Z || d.iy0 + d.IY > d.Y || d.ix0 + d.IX > d.X ||
+            d.IZ <= 0 || d.IY <= 0 || d.IX <= 0) {
+            h->err = "inner block outside the outer block";
+            return CTWS_EINVAL;
+        }
+        if (!d.input || !d.out) {
+            h->err = "null input/output";
+            return CTWS_EINVAL;
+        }
+        // vigra's convolveLine needs line length > kernel radius
+        auto chk_len = [&](const double* sg, bool en) -> bool {
+            if (!en) return true;
+            const int lens[3] = {d.Z, d.Y, d.X};
+            for (int a = (pl.nd_ws == 3 ? 0 : 1); a < 3; ++a) {
+                if (sg[a] <= 0) continue;
+                int r = (int)(3.0 * sg[a] + 0.5);
+                if (r == 0) r = 1;
+                if (lens[a] < r + 1) return false;
+            }
+            return true;
+        };
+        if (!chk_len(pl.sig_seeds, pl.seeds_smooth) || !chk_len(pl.sig_weights, pl.weights_smooth)) {
+            h->err = "convolveLine(): kernel longer than line";
+            return CTWS_EINVAL;
+        }
+        double dmax;
+        if (pl.dt_2d) dmax = (double)d.Y * d.Y + (double)d.X * d.X;
+        else
+            dmax = std::pow((double)pl.pitch[0] * d.Z, 2) + std::pow((double)pl.pitch[1] * d.Y, 2) +
+                   std::pow((double)pl.pitch[2] * d.X, 2);
+        if (dmax >= 16777216.0) {
+            h->err = "dmax >= 2^24: float32 squared distances are no longer exact";
+            return CTWS_EUNSUPPORTED;
+        }
+    }
+    int r;
+    if ((r = ensure_workspace(h, T, TW, TC, TS, TT, nb)) != CTWS_OK) return r;
+    HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
+    h->last_desc = desc;
+    std::vector<BlockStat> st(nb);
+    for (auto& s : st) {
+        std::memset(&s, 0, sizeof(s));
+        s.in_min = 0xFFFFFFFFu;
+        s.dt_min = 0xFFFFFFFFu;
+    }
+    HIPCHK(hipMemcpyAsync(w.stat, st.data(), sizeof(BlockStat) * nb, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w.smin, 0xFFFFFFFFu, (size_t)TS, h->stream));
+    HIPCHK(hipMemsetAsync(w.smax, 0, sizeof(uint32_t) * TS, h->stream));
+    HIPCHK(hipMemsetAsync(w.slmax, 0, sizeof(uint32_t) * TS, h->stream));
+    HIPCHK(hipMemsetAsync(w.surv, 0, sizeof(uint32_t) * TS, h->stream));
+
+    const dim3 vg((unsigned)std::min<int64_t>((maxN + 255) / 256, 4096), nb);
+    const dim3 ig((unsigned)std::min<int64_t>((maxNI + 255) / 256, 4096), nb);
+    const dim3 wg((unsigned)((words_of(maxN) + 255) / 256), nb);
+    size_t ev = 0;
+    h->timings.clear();
+    std::vector<const char*> names;
+    auto mark = [&](const char* name) {
+        record(h, ev++);
+        names.push_back(name);
+    };
+    mark("start");
+
+    // ---- normalize + threshold + EDT ------------------------------------------------------
+    {
+        dim3 g((unsigned)std::min<int64_t>(((int64_t)maxN * 2 + 255) / 256, 4096), nb);
+        k_input_minmax<<<g, 256, 0, h->stream>>>(w.desc, w.stat);
+        LAUNCHCHK();
+        PrepParams pp{(float)cfg->threshold, cfg->invert_inputs, cfg->agglomerate_channels, pl.pitch[2] * pl.pitch[2]};
+        dim3 gx((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
+        k_prep_edt_x<<<gx, 256, 4 * (size_t)maxX * 4, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+        LAUNCHCHK();
+        k_set_active<<<(nb + 255) / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb);
+        LAUNCHCHK();
+    }
+    mark("prep_edt_x");
+    {
+        // y pass (final for a 2-D dt), then z pass (3-D dt)
+        const int Wy = col_width(maxY);
+        EdtColParams ep{1, pl.pitch[1] * pl.pitch[1], pl.dt_2d, pl.dt_2d, 0u};
+        dim3 gy((unsigned)((int64_t)maxZ * ((maxX + Wy - 1) / Wy)), nb);
+        const size_t ldsy = (size_t)maxY * Wy * 4;
+        auto launch_col = [&](int W, dim3 g, size_t lds, EdtColParams p, const uint32_t* gin, uint32_t* gout) {
+            if (W == 32)
+                k_edt_col<32><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax);
+            else if (W == 16)
+                k_edt_col<16><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax);
+            else
+                k_edt_col<8><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax);
+        };
+        launch_col(Wy, gy, ldsy, ep, (uint32_t*)w.A, (uint32_t*)w.Bf);
+        LAUNCHCHK();
+        if (!pl.dt_2d) {
+            const int Wz = col_width(maxZ);
+            dim3 gz((unsigned)((int64_t)maxY * ((maxX + Wz - 1) / Wz)), nb);
+            const size_t ldsz = (size_t)maxZ * Wz * 4;
+            EdtColParams ez{2, pl.pitch[0] * pl.pitch[0], 1, 0, 0u};
+            launch_col(Wz, gz, ldsz, ez, (uint32_t*)w.Bf, nullptr);
+            LAUNCHCHK();
+            if (pl.nd_ws == 2) {
+                dim3 gs((unsigned)maxZ, nb);
+                k_dt_slice_stats<<<gs, 256, 0, h->stream>>>(w.desc, w.stat, w.dt, w.smin, w.smax);
+                LAUNCHCHK();
+            }
+        }
+    }
+    mark("edt_yz");
+
+    // ---- seed map smoothing, hmap -----------------------------------------------------------
+    HmapParams hp{(float)cfg->alpha, (float)(1.0 - cfg->alpha), pl.nd_ws == 2 ? 1 : 0};
+    const float* seedmap = w.dt;
+    if (pl.seeds_smooth) {
+        bool any = false;
+        for (int a = (pl.nd_ws == 3 ? 0 : 1); a < 3; ++a) any |= pl.sig_seeds[a] > 0.0;
+        if (any) {
+            if ((r = run_gauss(h, pl, pl.sig_seeds, false, w.dt, w.sm, nb, maxZ, maxY, maxX, hp, 0)) != CTWS_OK)
+                return r;
+            seedmap = w.sm;
+        }
+    }
+    mark("smooth_seeds");
+    {
+        const double sw[3] = {pl.weights_smooth ? pl.sig_weights[0] : 0.0, pl.weights_smooth ? pl.sig_weights[1] : 0.0,
+                              pl.weights_smooth ? pl.sig_weights[2] : 0.0};
+        if ((r = run_gauss(h, pl, sw, true, w.fin, w.hm, nb, maxZ, maxY, maxX, hp, 1)) != CTWS_OK) return r;
+    }
+    mark("hmap");
+
+    // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
+    k_localmax<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls);
+    LAUNCHCHK();
+    k_plateau_init<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
+    k_plateau_union<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
+    k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
+    k_seed_init<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF);
+    k_seed_union<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF);
+    k_flatten<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF);
+    k_bitmap<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.csum);
+    k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
+    k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
+    k_seed_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.hm, w.lab, w.key);
+    {
+        dim3 gs((unsigned)((maxZ + 255) / 256), nb);
+        k_slice_seed_base<<<gs, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
+    }
+    LAUNCHCHK();
+    mark("seeds");
+    if (h->stop_after == CTWS_STOP_SEEDS) {
+        HIPCHK(hipStreamSynchronize(h->stream));
+        return CTWS_OK;
+    }
+
+    // ---- flood ------------------------------------------------------------------------------
+    int rounds1 = 0, rounds2 = 0;
+    if ((r = run_flood(h, pl.nd_ws, nb, max_tiles, TT, w.hm, &rounds1)) != CTWS_OK) return r;
+    mark("flood");
+    if (h->stop_after == CTWS_STOP_FLOOD) {
+        HIPCHK(hipStreamSynchronize(h->stream));
+        return CTWS_OK;
+    }
+
+    // ---- size filter + regrow ---------------------------------------------------------------
+    if (cfg->size_filter > 0) {
+        uint32_t* counts = (uint32_t*)w.A;
+        k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
+        k_hist<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, counts);
+        FilterParams fp{(uint32_t)cfg->size_filter};
+        k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, nullptr, w.hm, w.lab, w.key, w.surv);
+        LAUNCHCHK();
+        if ((r = run_flood(h, pl.nd_ws, nb, max_tiles, TT, w.hm, &rounds2)) != CTWS_OK) return r;
+    }
+    mark("size_filter");
+
+    // ---- 2-D offsets / mask -> final uint32 ws ---------------------------------------------
+    if (pl.nd_ws == 2) {
+        k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.sb, w.slmax);
+        k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
+    }
+    k_finalize_ws<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, w.soff, w.lab);
+    LAUNCHCHK();
+    mark("finalize");
+    if (h->stop_after == CTWS_STOP_WS) {
+        HIPCHK(hipStreamSynchronize(h->stream));
+        return CTWS_OK;
+    }
+
+    // ---- halo crop CC + uint64 output -------------------------------------------------------
+    bool any_crop = false;
+    for (int i = 0; i < nb; ++i) any_crop |= desc[i].crop != 0;
+    if (any_crop) {
+        const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
+        k_crop_init<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
+        k_crop_union<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
+        k_flatten<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF);
+        k_bitmap<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.csum);
+        k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
+        k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
+        LAUNCHCHK();
+    }
+    mark("crop_cc");
+    k_output<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF, w.W, w.Wp);
+    LAUNCHCHK();
+    mark("output");
+
+    HIPCHK(hipMemcpyAsync(st.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
+    std::vector<uint32_t> surv;
+    if (cfg->size_filter > 0) {
+        surv.resize(TS);
+        HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+    }
+    HIPCHK(hipStreamSynchronize(h->stream));
+    for (size_t i = 1; i < ev; ++i) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, h->events[i - 1], h->events[i]);
+        h->timings.push_back({names[i], ms});
+    }
+    h->timings.push_back({"flood_rounds", (float)rounds1});
+    h->timings.push_back({"regrow_rounds", (float)rounds2});
+    for (int i = 0; i < nb; ++i) {
+        blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : CTWS_BLOCK_EMPTY;
+        blocks[i].max_label = st[i].active ? st[i].max_label : 0;
+        if (st[i].active && cfg->size_filter > 0) {
+            // every segment of a slice/block below size_filter: vigra then seeds the regrow
+            // from the local minima of the hmap (watershedsGraph with labels.any() == false)
+            const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
+            for (int z = 0; z < ns; ++z)
+                if (!surv[desc[i].sbase + z]) {
+                    h->err = "size filter removed every segment of a block/slice (auto-seeded regrow) "
+                             "is not implemented";
+                    return CTWS_EUNSUPPORTED;
+                }
+        }
+    }
+    return CTWS_OK;
+}
+
+int64_t batch_voxels_budget() {
+    const char* e = std::getenv("CTWS_BATCH_VOXELS");
+    if (e) return std::max<int64_t>(1, std::atoll(e));
+    return 512ll << 20;  // ~26 GB of workspace at ~50 B per voxel
+}
+
+int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, bool device_ptrs) {
+    if (!h || !cfg || (!blocks && n > 0) || n < 0) return CTWS_EINVAL;
+    h->err.clear();
+    HIPCHK(hipSetDevice(h->device));
+    Plan pl;
+    int r = make_plan(h, cfg, pl);
+    if (r != CTWS_OK) return r;
+    // blocks whose inner mask is empty are skipped entirely (watershed.py:290-297); the
+    // host-pointer path checks this on the host, the device path on the caller's side
+    std::vector<int> todo;
+    for (int i = 0; i < n; ++i) {
+        ctws_block& b = blocks[i];
+        b.status = CTWS_BLOCK_WRITTEN;
+        b.max_label = 0;
+        if (!device_ptrs && b.mask) {
+            const int64_t* sh = b.outer_shape;
+            bool any = false;
+            for (int64_t z = 0; z < b.inner_shape[0] && !any; ++z)
+                for (int64_t y = 0; y < b.inner_shape[1] && !any; ++y) {
+                    const uint8_t* row = b.mask + ((z + b.inner_begin[0]) * sh[1] + (y + b.inner_begin[1])) * sh[2] +
+                                         b.inner_begin[2];
+                    for (int64_t x = 0; x < b.inner_shape[2]; ++x)
+                        if (row[x]) {
+                            any = true;
+                            break;
+                        }
+                }
+            if (!any) {
+                b.status = CTWS_BLOCK_SKIPPED_MASK;
+                continue;
+            }
+        }
+        todo.push_back(i);
+    }
+    const int64_t budget = batch_voxels_budget();
+    size_t k = 0;
+    while (k < todo.size()) {
+        // batch [k, e)
+        size_t e = k;
+        int64_t vox = 0;
+        while (e < todo.size()) {
+            const ctws_block& b = blocks[todo[e]];
+            const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
+            if (e > k && vox + nv > budget) break;
+            vox += nv;
+            ++e;
+        }
+        const int nb = (int)(e - k);
+        std::vector<ctws_block> bb(nb);
+        std::vector<BlockIO> io(nb);
+        for (int i = 0; i < nb; ++i) bb[i] = blocks[todo[k + i]];
+        if (device_ptrs) {
+            for (int i = 0; i < nb; ++i)
+                io[i] = {bb[i].input, bb[i].mask, bb[i].initial_seeds, bb[i].output};
+            if ((r = run_batch(h, cfg, pl, bb.data(), io.data(), nb)) != CTWS_OK) return r;
+        } else {
+            // stage host buffers through device memory
+            size_t in_bytes = 0, m_bytes = 0, i_bytes = 0, o_bytes = 0;
+            std::vector<size_t> in_off(nb), m_off(nb), i_off(nb), o_off(nb), in_sz(nb);
+            for (int i = 0; i < nb; ++i) {
+                const ctws_block& b = bb[i];
+                const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
+                const size_t es = b.input_dtype == CTWS_U8 ? 1 : (b.input_dtype == CTWS_U16 ? 2 : (b.input_dtype == CTWS_F32 ? 4 : 8));
+                in_sz[i] = (size_t)nv * es * (size_t)std::max(1, b.n_channels);
+                in_off[i] = in_bytes;
+                in_bytes += (in_sz[i] + 255) & ~(size_t)255;
+                m_off[i] = m_bytes;
+                if (b.mask) m_bytes += ((size_t)nv + 255) & ~(size_t)255;
+                i_off[i] = i_bytes;
+                if (b.initial_seeds) i_bytes += (size_t)nv * 8;
+                o_off[i] = o_bytes;
+                o_bytes += (size_t)(b.inner_shape[0] * b.inner_shape[1] * b.inner_shape[2]) * 8;
+            }
+            if ((r = grow(h, h->st_in, in_bytes)) != CTWS_OK) return r;
+            if ((r = grow(h, h->st_mask, m_bytes)) != CTWS_OK) return r;
+            if ((r = grow(h, h->st_init, i_bytes)) != CTWS_OK) return r;
+            if ((r = grow(h, h->st_out, o_bytes)) != CTWS_OK) return r;
+            for (int i = 0; i < nb; ++i) {
+                const ctws_block& b = bb[i];
+                const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
+                char* din = (char*)h->st_in.p + in_off[i];
+                HIPCHK(hipMemcpyAsync(din, b.input, in_sz[i], hipMemcpyHostToDevice, h->stream));
+                io[i].in = din;
+                io[i].mask = nullptr;
+                if (b.mask) {
+                    uint8_t* dm = (uint8_t*)h->st_mask.p + m_off[i];
+                    HIPCHK(hipMemcpyAsync(dm, b.mask, (size_t)nv, hipMemcpyHostToDevice, h->stream));
+                    io[i].mask = dm;
+                }
+                io[i].init = nullptr;
+                if (b.initial_seeds) {
+                    uint64_t* di = (uint64_t*)((char*)h->st_init.p + i_off[i]);
+                    HIPCHK(hipMemcpyAsync(di, b.initial_seeds, (size_t)nv * 8, hipMemcpyHostToDevice, h->stream));
+                    io[i].init = di;
+                }
+                io[i].out = (uint64_t*)((char*)h->st_out.p + o_off[i]);
+            }
+            if ((r = run_batch(h, cfg, pl, bb.data(), io.data(), nb)) != CTWS_OK) return r;
+            for (int i = 0; i < nb; ++i) {
+                const size_t ob = (size_t)(bb[i].inner_shape[0] * bb[i].inner_shape[1] * bb[i].inner_shape[2]) * 8;
+                HIPCHK(hipMemcpyAsync(bb[i].output, io[i].out, ob, hipMemcpyDeviceToHost, h->stream));
+            }
+            HIPCHK(hipStreamSynchronize(h->stream));
+        }
+        for (int i = 0; i < nb; ++i) {
+            blocks[todo[k + i]].status = bb[i].status;
+            blocks[todo[k + i]].max_label = bb[i].max_label;
+        }
+        k = e;
+    }
+    return CTWS_OK;
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+int ctws_abi_version(void) { return CTWS_ABI_VERSION; }
+
+int ctws_open(int device, ctws_handle** out) {
+    if (!out) return CTWS_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return CTWS_EHIP;
+    if (device < 0 || device >= n) return CTWS_EINVAL;
+    ctws_handle* h = new ctws_handle();
+    h->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_counter, 4, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_taps, 6 * 128 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
+        delete h;
+        return CTWS_EHIP;
+    }
+    *out = h;
+    return CTWS_OK;
+}
+
+void ctws_close(ctws_handle* h) {
+    if (!h) return;
+    hipSetDevice(h->device);
+    hipStreamSynchronize(h->stream);
+    Workspace& w = h->ws;
+    void* ptrs[] = {w.fin, w.dt, w.A, w.Bf, w.sm, w.hm, w.cls, w.P, w.PF, w.lab, w.key, w.W, w.Wp, w.csum,
+                    w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.desc, w.stat, w.counter,
+                    w.taps, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    for (auto e : h->events) hipEventDestroy(e);
+    if (h->h_counter) hipHostFree(h->h_counter);
+    if (h->h_taps) hipHostFree(h->h_taps);
+    if (h->comm) ncclCommDestroy(h->comm);
+    hipStreamDestroy(h->stream);
+    delete h;
+}
+
+const char* ctws_last_error(const ctws_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int ctws_ws_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks) {
+    return run_blocks(h, cfg, blocks, n_blocks, false);
+}
+
+int ctws_ws_blocks_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks) {
+    return run_blocks(h, cfg, blocks, n_blocks, true);
+}
+
+int ctws_last_timings(const ctws_handle* h, const char** names, float* ms, int max_entries) {
+    if (!h) return 0;
+    const int n = (int)std::min<size_t>(h->timings.size(), (size_t)std::max(0, max_entries));
+    for (int i = 0; i < n; ++i) {
+        if (names) names[i] = h->timings[i].first;
+        if (ms) ms[i] = h->timings[i].second;
+    }
+    return (int)h->timings.size();
+}
+
+int ctws_debug_set_stop(ctws_handle* h, int stage) {
+    if (!h || stage < 0 || stage > 3) return CTWS_EINVAL;
+    h->stop_after = stage;
+    return CTWS_OK;
+}
+
+int ctws_debug_read(ctws_handle* h, const char* array, int block, void* dst, int64_t nbytes) {
+    if (!h || !array || !dst || block < 0 || block >= (int)h->last_desc.size()) return CTWS_EINVAL;
+    const BlockDesc& d = h->last_desc[block];
+    const Workspace& w = h->ws;
+    const std::string a(array);
+    const void* src = nullptr;
+    size_t es = 4;
+    if (a == "fin") src = w.fin;
+    else if (a == "dt") src = w.dt;
+    else if (a == "seedmap") src = w.sm;
+    else if (a == "hmap") src = w.hm;
+    else if (a == "labels") src = w.lab;
+    else if (a == "cls") { src = w.cls; es = 1; }
+    else return CTWS_EINVAL;
+    if (nbytes != (int64_t)(d.N * es)) {
+        h->err = "ctws_debug_read: nbytes must be N * itemsize";
+        return CTWS_EINVAL;
+    }
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipMemcpy(dst, (const char*)src + d.base * es, (size_t)nbytes, hipMemcpyDeviceToHost));
+    return CTWS_OK;
+}
+
+int ctws_comm_unique_id(ctws_handle* h, void* unique_id_128) {
+    if (!h || !unique_id_128) return CTWS_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) {
+        h->err = "ncclGetUniqueId failed";
+        return CTWS_ECOMM;
+    }
+    std::memcpy(unique_id_128, &id, sizeof(id) < 128 ? sizeof(id) : 128);
+    return CTWS_OK;
+}
+
+int ctws_comm_init(ctws_handle* h, int nranks, int rank, const void* unique_id_128) {
+    if (!h || !unique_id_128 || nranks < 1 || rank < 0 || rank >= nranks) return CTWS_EINVAL;
+    HIPCHK(hipSetDevice(h->device));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id_128, sizeof(id));
+    ncclResult_t rr = ncclCommInitRank(&h->comm, nranks, id, rank);
+    if (rr != ncclSuccess) {
+        h->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(rr);
+        return CTWS_ECOMM;
+    }
+    h->nranks = nranks;
+    h->rank = rank;
+    return CTWS_OK;
+}
+
+int ctws_allgather_counts(ctws_handle* h, const int64_t* local_counts, int64_t n_local, int64_t* all_counts) {
+    if (!h || !local_counts || !all_counts || n_local < 0) return CTWS_EINVAL;
+    if (!h->comm) {
+        std::memcpy(all_counts, local_counts, sizeof(int64_t) * (size_t)n_local);
+        return CTWS_OK;
+    }
+    HIPCHK(hipSetDevice(h->device));
+    int64_t *d_in = nullptr, *d_out = nullptr;
+    HIPCHK(hipMalloc(&d_in, sizeof(int64_t) * std::max<int64_t>(1, n_local)));
+    HIPCHK(hipMalloc(&d_out, sizeof(int64_t) * std::max<int64_t>(1, n_local) * h->nranks));
+    HIPCHK(hipMemcpyAsync(d_in, local_counts, sizeof(int64_t) * n_local, hipMemcpyHostToDevice, h->stream));
+    ncclResult_t rr = ncclAllGather(d_in, d_out, (size_t)n_local, ncclInt64, h->comm, h->stream);
+    if (rr != ncclSuccess) {
+        hipFree(d_in);
+        hipFree(d_out);
+        h->err = std::string("ncclAllGather: ") + ncclGetErrorString(rr);
+        return CTWS_ECOMM;
+    }
+    HIPCHK(hipMemcpyAsync(all_counts, d_out, sizeof(int64_t) * n_local * h->nranks, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    hipFree(d_in);
+    hipFree(d_out);
+    return CTWS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,112 @@
+// ctws_dev.h — device-side data layout and helpers shared by the gfx950 kernels.
+//
+// A *batch* is a set of blocks processed by one pipeline of launches.  Every per-voxel
+// workspace array is the concatenation of the blocks' outer volumes (BlockDesc::base), so
+// one launch covers all blocks of the batch (grid.y = block).  Per-block scalars live in
+// BlockStat, per-slice scalars in arrays indexed by BlockDesc::sbase + z.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ctws {
+
+constexpr uint32_t kInfD2 = 0x3FFFFFFFu;             // "no foreground" squared distance
+constexpr uint64_t kInfKey = 0xFFFFFFFFFFFFFFFFull;  // flood key of an unreached voxel
+constexpr uint32_t kNoParent = 0xFFFFFFFFu;          // union-find: background
+constexpr uint32_t kFixedBit = 0x80000000u;          // flood label: voxel is a seed
+
+struct BlockDesc {
+    int Z, Y, X, nd_ws;     // outer shape; nd_ws = 2 (per-slice ws) or 3
+    int64_t N;              // Z*Y*X
+    int64_t base;           // offset into outer-sized arrays
+    int iz0, iy0, ix0, crop;
+    int IZ, IY, IX, _p0;
+    int64_t NI;             // inner voxels
+    int64_t ibase;          // offset into inner-sized arrays
+    int64_t wbase;          // offset into bitmap-word arrays (words = N/64 + 1)
+    int64_t cbase;          // offset into bitmap-chunk arrays
+    int64_t sbase;          // offset into per-slice arrays (Z entries)
+    const void* input;      // raw outer input (device)
+    const uint8_t* mask;    // outer mask or nullptr
+    const uint64_t* init;   // pass-2 initial seeds or nullptr
+    uint64_t* out;          // inner uint64 output
+    int n_channels, c0, C, dtype;
+    uint64_t id_offset;     // block_id * prod(block_shape)
+    int tz, ty, tx, tbase;  // flood tile grid, offset into per-tile arrays
+    uint32_t maxd;          // 3-D EDT: ceil(dmax) = sum_k (pitch_k n_k)^2
+    uint32_t _p2;
+};
+
+struct BlockStat {
+    uint32_t in_min, in_max;  // ordered-float bits of the raw (float-cast) input
+    uint32_t fg;              // number of voxels above threshold (saturating flag use)
+    uint32_t dt_min, dt_max;  // ordered-float bits of dt over the outer block
+    uint32_t plateau;         // voxels with an equal-valued maxima-neighbour
+    uint32_t n_seeds;         // seed components
+    uint32_t max_label;       // local max label (before the id offset)
+    uint32_t active;          // block takes part in the remaining pipeline
+    uint32_t n_cc;            // crop CC components
+    uint32_t _p[6];
+};
+
+// order-preserving float <-> uint32 mapping (total order for non-NaN floats)
+__device__ __forceinline__ uint32_t ordf(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unordf(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+// union-find on an F-order keyed parent array.  Roots keep the smallest key, so the root
+// of a component is its first voxel in vigra scan order (dim 0 fastest).
+__device__ __forceinline__ uint32_t uf_find(const uint32_t* P, uint32_t a) {
+    // follows parent pointers to the root (roots point to themselves)
+    uint32_t p = P[a];
+    while (p != a) {
+        a = p;
+        p = P[a];
+    }
+    return a;
+}
+__device__ __forceinline__ uint32_t uf_find_compress(uint32_t* P, uint32_t a) {
+    uint32_t r = a;
+    uint32_t p = P[r];
+    while (p != r) {
+        r = p;
+        p = P[r];
+    }
+    // path compression (benign races: every write stores an ancestor)
+    while (true) {
+        uint32_t n = P[a];
+        if (n == r || n == a) break;
+        P[a] = r;
+        a = n;
+    }
+    return r;
+}
+__device__ __forceinline__ void uf_union(uint32_t* P, uint32_t a, uint32_t b) {
+    while (true) {
+        a = uf_find(P, a);
+        b = uf_find(P, b);
+        if (a == b) return;
+        if (a > b) {
+            uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        uint32_t old = atomicCAS(&P[b], b, a);
+        if (old == b) return;
+        b = old;
+    }
+}
+
+// rank of key f among set bits of a per-block bitmap with per-word exclusive prefix
+__device__ __forceinline__ uint32_t bitmap_rank(const uint64_t* W, const uint32_t* Wp, uint32_t f) {
+    uint32_t w = f >> 6;
+    uint64_t m = W[w] & ((1ull << (f & 63)) - 1ull);
+    return Wp[w] + (uint32_t)__popcll(m);
+}
+
+}  // namespace ctws

@@ -1,0 +1,274 @@
+// k_edt.hip — _read_data/normalize, threshold and the exact Euclidean distance transform.
+//
+// Reference: cluster_tools/watershed/watershed.py:267-282 (_read_data), :139-160 (_apply_dt),
+// utils/volume_utils.py:113-120 (normalize); vigra.filters.distanceTransform
+// (separableMultiDistSquared).  For integer pixel pitch and dmax < 2^24 the squared
+// distances are exact integers, so any exact separable EDT reproduces vigra bit for bit:
+//   pass x : 1-D distance to the nearest foreground voxel on the row   (wave-level scans)
+//   pass y : min_y' g(y') + p_y^2 (y - y')^2, LDS-staged columns, bounded search
+//   pass z : same along z, then min(d2, ceil(dmax)) and sqrtf (correctly rounded)
+// HBM traffic per outer voxel: x-pass reads the input (4 B f32 / 1 B u8) and writes the
+// normalized input (4 B) and g^2 (4 B); y and z passes read 4 B and write 4 B each.
+#include "ctws_kernels.h"
+
+namespace ctws {
+
+__device__ __forceinline__ float load_raw(const void* p, int dtype, int64_t i) {
+    switch (dtype) {
+        case 1: return (float)((const uint8_t*)p)[i];
+        case 2: return (float)((const uint16_t*)p)[i];
+        case 3: return ((const float*)p)[i];
+        default: return (float)((const double*)p)[i];
+    }
+}
+
+// ---- per-block min / max of the raw input over the channel range (normalize) -----------
+__global__ void __launch_bounds__(256) k_input_minmax(const BlockDesc* __restrict__ D, BlockStat* S) {
+    const BlockDesc& B = D[blockIdx.y];
+    const int64_t n = (int64_t)B.C * B.N;
+    const int64_t off = (int64_t)B.c0 * B.N;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t o = ordf(load_raw(B.input, B.dtype, off + i));
+        mn = min(mn, o);
+        mx = max(mx, o);
+    }
+    for (int s = 32; s > 0; s >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, s));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, s));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&S[blockIdx.y].in_min, mn);
+        atomicMax(&S[blockIdx.y].in_max, mx);
+    }
+}
+
+// ---- normalized input + threshold + EDT pass along x --------------------------------
+// One wave per row (z, y).  fin = normalize(input) [channel agg, invert, mask -> 1];
+// g2 = p_x^2 * (distance to the nearest voxel with fin > threshold on the row)^2.
+
+__global__ void __launch_bounds__(256) k_prep_edt_x(const BlockDesc* __restrict__ D, BlockStat* S, PrepParams pp,
+                                                    float* __restrict__ fin, uint32_t* __restrict__ g2) {
+    extern __shared__ __attribute__((aligned(16))) int smem_i[];
+    const BlockDesc& B = D[blockIdx.y];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+    if (row >= (int64_t)B.Z * B.Y) return;
+    const int X = B.X;
+    int* sdist = smem_i + wave * X;  // per-wave row buffer: fg flag, then right distance
+    const float mn = unordf(S[blockIdx.y].in_min);
+    const float den = unordf(S[blockIdx.y].in_max) - mn;  // max(x - min) == max - min (monotone rounding)
+    const int64_t rbase = row * X;
+    uint32_t fgcount = 0;
+    for (int x = lane; x < X; x += 64) {
+        const int64_t i = rbase + x;
+        float v;
+        if (B.n_channels == 0) {
+            v = load_raw(B.input, B.dtype, i) - mn;
+            if (den > 0.0f) v = v / den;
+        } else {
+            const int64_t cs = B.N;
+            const int64_t o0 = (int64_t)B.c0 * cs + i;
+            v = load_raw(B.input, B.dtype, o0) - mn;
+            if (den > 0.0f) v = v / den;
+            for (int c = 1; c < B.C; ++c) {
+                float w = load_raw(B.input, B.dtype, o0 + c * cs) - mn;
+                if (den > 0.0f) w = w / den;
+                if (pp.agg == 0) v = v + w;
+                else if (pp.agg == 1) v = fmaxf(v, w);
+                else v = fminf(v, w);
+            }
+            if (pp.agg == 0) v = v / (float)B.C;
+        }
+        if (pp.invert) v = 1.0f - v;
+        if (B.mask && !B.mask[i]) v = 1.0f;
+        fin[B.base + i] = v;
+        const int f = v > pp.threshold;
+        sdist[x] = f;
+        fgcount += f;
+    }
+    // any foreground in the block? (_apply_dt: np.sum(threshd) == 0 -> None)
+    if (__ballot(fgcount != 0) != 0ull && lane == 0) atomicOr(&S[blockIdx.y].fg, 1u);
+    __builtin_amdgcn_wave_barrier();
+    // chunk per lane: [lane*K, lane*K + K)
+    const int K = (X + 63) >> 6;
+    const int x0 = lane * K, x1 = min(X, x0 + K);
+    int last = -1, first = 0x3FFFFFFF;
+    for (int x = x0; x < x1; ++x)
+        if (sdist[x]) {
+            last = x;
+            if (first == 0x3FFFFFFF) first = x;
+        }
+    // exclusive max-scan of `last` from the left, exclusive min-scan of `first` from the right
+    int lp = last, rn = first;
+    for (int s = 1; s < 64; s <<= 1) {
+        int a = __shfl_up(lp, s);
+        if (lane >= s) lp = max(lp, a);
+        int b = __shfl_down(rn, s);
+        if (lane + s < 64) rn = min(rn, b);
+    }
+    int left = __shfl_up(lp, 1);
+    if (lane == 0) left = -1;
+    int right = __shfl_down(rn, 1);
+    if (lane == 63) right = 0x3FFFFFFF;
+    // backward: distance to the nearest fg at or after x
+    int dist[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dist[k] = 0;
+    {
+        int r = right;
+#pragma unroll
+        for (int k = 15; k >= 0; --k) {
+            const int x = x0 + k;
+            if (x < x1) {
+                if (sdist[x]) r = x;
+                dist[k] = r - x;
+            }
+        }
+        int l = left;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int x = x0 + k;
+            if (x < x1) {
+                if (sdist[x]) l = x;
+                const int dl = (l < 0) ? 0x3FFFFFFF : x - l;
+                dist[k] = min(dist[k], dl);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int x = x0 + k;
+        if (x < x1) {
+            const int d = dist[k];
+            sdist[x] = (d >= 0x3FFFFFFF) ? (int)kInfD2 : pp.px2 * d * d;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int x = lane; x < X; x += 64) g2[B.base + rbase + x] = (uint32_t)sdist[x];
+}
+
+// ---- EDT pass along y (stride X) or z (stride Y*X), LDS-staged columns -----------------
+// Tile: the full line (length L) x W consecutive x positions.  Bounded brute force:
+//   best = g[p]; for r = 1.. while p2 r^2 < best: best = min(best, g[p +- r] + p2 r^2)
+// FINAL: clamp to maxDist = ceil(dmax) and write sqrtf(d2) as float, with dt statistics.
+
+template <int W>
+__global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D, BlockStat* S, EdtColParams ep,
+                                                 const uint32_t* __restrict__ gin, uint32_t* __restrict__ gout,
+                                                 float* __restrict__ dt, uint32_t* __restrict__ slice_min,
+                                                 uint32_t* __restrict__ slice_max) {
+    extern __shared__ __attribute__((aligned(16))) int smem_i[];
+    uint32_t* col = (uint32_t*)smem_i;
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int nxc = (B.X + W - 1) / W;
+    const int L = (ep.axis == 1) ? B.Y : B.Z;
+    const int other = (ep.axis == 1) ? B.Z : B.Y;  // the line index that is not x
+    const int t = blockIdx.x;
+    if (t >= other * nxc) return;
+    const int o = t / nxc, xc = t % nxc;
+    const int xb = xc * W;
+    const int64_t lstride = (ep.axis == 1) ? B.X : (int64_t)B.Y * B.X;
+    const int64_t obase = (ep.axis == 1) ? (int64_t)o * B.Y * B.X : (int64_t)o * B.X;
+    const int c = threadIdx.x % W;
+    const int r0 = threadIdx.x / W;
+    constexpr int RS = 256 / W;
+    const bool colok = xb + c < B.X;
+    for (int p = r0; p < L; p += RS)
+        col[p * W + c] = colok ? gin[B.base + obase + p * lstride + xb + c] : kInfD2;
+    __syncthreads();
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    const uint32_t maxd = ep.per_slice ? (uint32_t)(B.Y * B.Y + B.X * B.X) : B.maxd;
+    for (int p = r0; p < L; p += RS) {
+        uint32_t best = col[p * W + c];
+        for (int r = 1;; ++r) {
+            const uint32_t rr = (uint32_t)ep.p2 * (uint32_t)(r * r);
+            if (rr >= best) break;
+            const bool lo = p - r >= 0, hi = p + r < L;
+            if (!lo && !hi) break;
+            if (lo) best = min(best, col[(p - r) * W + c] + rr);
+            if (hi) best = min(best, col[(p + r) * W + c] + rr);
+        }
+        if (!colok) continue;
+        const int64_t gi = B.base + obase + p * lstride + xb + c;
+        if (ep.final_pass) {
+            const uint32_t d2 = min(best, maxd);
+            const float v = __fsqrt_rn((float)d2);
+            dt[gi] = v;
+            const uint32_t ov = ordf(v);
+            mn = min(mn, ov);
+            mx = max(mx, ov);
+        } else {
+            gout[gi] = best;
+        }
+    }
+    if (ep.final_pass) {
+        // workgroup reduce, then per block (3-D ws) and per slice (2-D dt: o is z)
+        __shared__ uint32_t rmn[4], rmx[4];
+        for (int s = 32; s > 0; s >>= 1) {
+            mn = min(mn, (uint32_t)__shfl_xor((int)mn, s));
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, s));
+        }
+        const int wv = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) {
+            rmn[wv] = mn;
+            rmx[wv] = mx;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            mn = min(min(rmn[0], rmn[1]), min(rmn[2], rmn[3]));
+            mx = max(max(rmx[0], rmx[1]), max(rmx[2], rmx[3]));
+            atomicMin(&S[blockIdx.y].dt_min, mn);
+            atomicMax(&S[blockIdx.y].dt_max, mx);
+            if (ep.axis == 1) {
+                atomicMin(&slice_min[B.sbase + o], mn);
+                atomicMax(&slice_max[B.sbase + o], mx);
+            }
+        }
+    }
+}
+
+template __global__ void k_edt_col<32>(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*,
+                                       uint32_t*, uint32_t*);
+template __global__ void k_edt_col<16>(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*,
+                                       uint32_t*, uint32_t*);
+template __global__ void k_edt_col<8>(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*,
+                                      uint32_t*, uint32_t*);
+
+// per-slice min / max of dt (2-D ws on a 3-D dt): one workgroup per slice chunk
+__global__ void __launch_bounds__(256) k_dt_slice_stats(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                        const float* __restrict__ dt, uint32_t* slice_min,
+                                                        uint32_t* slice_max) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int z = blockIdx.x;
+    if (z >= B.Z) return;
+    const int64_t n = (int64_t)B.Y * B.X;
+    const float* p = dt + B.base + (int64_t)z * n;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        uint32_t o = ordf(p[i]);
+        mn = min(mn, o);
+        mx = max(mx, o);
+    }
+    for (int s = 32; s > 0; s >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, s));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, s));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&slice_min[B.sbase + z], mn);
+        atomicMax(&slice_max[B.sbase + z], mx);
+    }
+}
+
+}  // namespace ctws
+
+namespace ctws {
+// a block takes part in the pipeline iff something is above the threshold (_apply_dt)
+__global__ void k_set_active(const BlockDesc* __restrict__ D, BlockStat* S, int n) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < n) S[b].active = S[b].fg != 0u;
+}
+}  // namespace ctws

@@ -1,0 +1,206 @@
+// k_flood.hip — seeded watershed (vigra watershedsNew, region growing) on gfx950.
+//
+// Reference: utils/volume_utils.py:123-139 (vu.watershed, apply_size_filter) calling
+// vigra.analysis.watershedsNew -> seededWatersheds: a min-priority queue, label-on-push,
+// priority(q) = max(h(q), priority(parent)).  Popped priorities are non-decreasing, so every
+// voxel q gets
+//     C(q) = minimax path height from the seeds (the priority it is pushed with), and
+//     label(q) = label of the neighbour popped first, i.e. the neighbour with the smallest C.
+// Equal C values (plateaus) are ordered by the heap in vigra; here the order inside a
+// plateau is the hop distance d from where the plateau level was entered, so the key
+//     K(q) = (C(q), d(q)),   K(q) = f_q(min_p K(p)),
+//     f_q(C, d) = h(q) > C ? (h(q), 0) : (C, d + 1)
+// is strictly increasing along parent edges, and the fixpoint (K, label) with
+// label(q) = label(argmin_p (K(p), label(p))) is unique and independent of the schedule.
+// Seeds are fixed at K = (h, 0).  The parity bar for this stage is VI <= 0.01 / ARand <= 1e-3
+// against the oracle (which reproduces the heap order), not bit-exactness.
+//
+// Schedule: tiles of TZxTYxTX voxels with a 1-voxel halo in LDS relax to the local fixpoint
+// (each thread owns a run of 8 voxels along x and sweeps it forward and backward, so a
+// change crosses the run in one sweep); changed face voxels activate the face-neighbour
+// tiles for the next round; rounds repeat until no tile is active.
+//
+// Keys are uint64 (ordf(C) << 32 | d); labels carry kFixedBit for seeds.
+#include "ctws_kernels.h"
+
+namespace ctws {
+
+template <int ND>
+struct FloodTile;
+template <>
+struct FloodTile<3> {
+    static constexpr int TZ = 4, TY = 8, TX = 64, HZ = TZ + 2;
+};
+template <>
+struct FloodTile<2> {
+    static constexpr int TZ = 1, TY = 32, TX = 64, HZ = 1;
+};
+
+__device__ __forceinline__ void take_min(uint64_t nk, uint32_t nl, uint64_t& bk, uint32_t& bl) {
+    if (nk < bk || (nk == bk && nl < bl)) {
+        bk = nk;
+        bl = nl;
+    }
+}
+
+__device__ __forceinline__ uint64_t f_key(uint32_t hb, uint64_t bk) {
+    const uint32_t c = (uint32_t)(bk >> 32);
+    if (hb > c) return (uint64_t)hb << 32;
+    return bk + 1ull;  // (C, d + 1); d never reaches 2^32
+}
+
+template <int ND>
+__global__ void __launch_bounds__(256) k_flood(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                               const float* __restrict__ h, uint64_t* __restrict__ key,
+                                               uint32_t* __restrict__ lab, const uint8_t* __restrict__ act_cur,
+                                               uint8_t* __restrict__ act_next, uint32_t* __restrict__ counter) {
+    using T = FloodTile<ND>;
+    constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX;
+    constexpr int HZ = T::HZ, HY = TY + 2, HX = TX + 2;
+    constexpr int HN = HZ * HY * HX;
+    constexpr int RUN = 8;
+    __shared__ uint64_t sk[HN];
+    __shared__ uint32_t sl[HN];
+    __shared__ int sface[6];
+
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int ntile = B.tz * B.ty * B.tx;
+    const int t = blockIdx.x;
+    if (t >= ntile) return;
+    if (!act_cur[B.tbase + t]) return;
+    const int txi = t % B.tx, tyi = (t / B.tx) % B.ty, tzi = t / (B.tx * B.ty);
+    const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const int64_t gb = B.base;
+
+    if (threadIdx.x < 6) sface[threadIdx.x] = 0;
+    // ---- load tile + halo
+    for (int c = threadIdx.x; c < HN; c += 256) {
+        const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
+        const int gz = (ND == 3) ? z0 + hz - 1 : z0;
+        const int gy = y0 + hy - 1, gx = x0 + hx - 1;
+        uint64_t k = kInfKey;
+        uint32_t l = 0;
+        if (gz >= 0 && gz < B.Z && gy >= 0 && gy < B.Y && gx >= 0 && gx < B.X) {
+            const int64_t gi = gb + gz * YX + (int64_t)gy * B.X + gx;
+            k = key[gi];
+            l = lab[gi] & ~kFixedBit;
+        }
+        sk[c] = k;
+        sl[c] = l;
+    }
+    // ---- owned run
+    const int run = threadIdx.x % (TX / RUN);
+    const int row = threadIdx.x / (TX / RUN);  // 0 .. TZ*TY-1
+    const int lz = (ND == 3) ? row / TY : 0, ly = row % TY;
+    const int lx0 = run * RUN;
+    const int gz = z0 + lz, gy = y0 + ly;
+    const int hz = (ND == 3) ? lz + 1 : 0, hy = ly + 1;
+    const int hrow = (hz * HY + hy) * HX;
+    uint64_t k[RUN], k0[RUN];
+    uint32_t l[RUN], l0[RUN], hb[RUN];
+    uint32_t fixed = 0, valid = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RUN; ++j) {
+        const int gx = x0 + lx0 + j;
+        const bool in = gz < B.Z && gy < B.Y && gx < B.X;
+        hb[j] = 0;
+        if (in) {
+            const int64_t gi = gb + gz * YX + (int64_t)gy * B.X + gx;
+            hb[j] = ordf(h[gi]);
+            if (lab[gi] & kFixedBit) fixed |= 1u << j;
+            valid |= 1u << j;
+        }
+        k[j] = k0[j] = sk[hrow + lx0 + j + 1];
+        l[j] = l0[j] = sl[hrow + lx0 + j + 1];
+    }
+    const uint32_t upd = valid & ~fixed;
+
+    // ---- local relaxation to the fixpoint
+    for (int it = 0; it < 4096; ++it) {
+        bool ch = false;
+        auto relax = [&](int j) {
+            const int c = hrow + lx0 + j + 1;
+            uint64_t bk = kInfKey;
+            uint32_t bl = 0xFFFFFFFFu;
+            // x-neighbours: own registers inside the run, LDS at the run ends
+            if (j > 0) take_min(k[j - 1], l[j - 1], bk, bl);
+            else take_min(sk[c - 1], sl[c - 1], bk, bl);
+            if (j < RUN - 1) take_min(k[j + 1], l[j + 1], bk, bl);
+            else take_min(sk[c + 1], sl[c + 1], bk, bl);
+            take_min(sk[c - HX], sl[c - HX], bk, bl);
+            take_min(sk[c + HX], sl[c + HX], bk, bl);
+            if (ND == 3) {
+                take_min(sk[c - HX * HY], sl[c - HX * HY], bk, bl);
+                take_min(sk[c + HX * HY], sl[c + HX * HY], bk, bl);
+            }
+            if (bk == kInfKey) return;
+            const uint64_t nk = f_key(hb[j], bk);
+            if (nk != k[j] || bl != l[j]) {
+                k[j] = nk;
+                l[j] = bl;
+                ch = true;
+            }
+        };
+#pragma unroll
+        for (int j = 0; j < RUN; ++j)
+            if (upd & (1u << j)) relax(j);
+#pragma unroll
+        for (int j = RUN - 1; j >= 0; --j)
+            if (upd & (1u << j)) relax(j);
+        __syncthreads();
+        if (ch) {
+#pragma unroll
+            for (int j = 0; j < RUN; ++j) {
+                sk[hrow + lx0 + j + 1] = k[j];
+                sl[hrow + lx0 + j + 1] = l[j];
+            }
+        }
+        if (!__syncthreads_or(ch)) break;
+    }
+
+    // ---- write back, activate face neighbours whose halo changed
+#pragma unroll
+    for (int j = 0; j < RUN; ++j) {
+        if (!(upd & (1u << j))) continue;
+        if (k[j] == k0[j] && l[j] == l0[j]) continue;
+        const int gx = x0 + lx0 + j;
+        const int64_t gi = gb + gz * YX + (int64_t)gy * B.X + gx;
+        key[gi] = k[j];
+        lab[gi] = l[j];
+        const int lx = lx0 + j;
+        if (ND == 3) {
+            if (lz == 0) sface[0] = 1;
+            if (lz == TZ - 1) sface[1] = 1;
+        }
+        if (ly == 0) sface[2] = 1;
+        if (ly == TY - 1) sface[3] = 1;
+        if (lx == 0) sface[4] = 1;
+        if (lx == TX - 1) sface[5] = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int n = 0;
+        auto act = [&](int zz, int yy, int xx) {
+            if (zz < 0 || zz >= B.tz || yy < 0 || yy >= B.ty || xx < 0 || xx >= B.tx) return;
+            act_next[B.tbase + (zz * B.ty + yy) * B.tx + xx] = 1;
+            ++n;
+        };
+        if (sface[0]) act(tzi - 1, tyi, txi);
+        if (sface[1]) act(tzi + 1, tyi, txi);
+        if (sface[2]) act(tzi, tyi - 1, txi);
+        if (sface[3]) act(tzi, tyi + 1, txi);
+        if (sface[4]) act(tzi, tyi, txi - 1);
+        if (sface[5]) act(tzi, tyi, txi + 1);
+        if (n) atomicAdd(counter, (uint32_t)n);
+    }
+}
+
+template __global__ void k_flood<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint32_t*,
+                                    const uint8_t*, uint8_t*, uint32_t*);
+template __global__ void k_flood<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint32_t*,
+                                    const uint8_t*, uint8_t*, uint32_t*);
+
+}  // namespace ctws

@@ -1,0 +1,137 @@
+// k_post.hip — size filter, per-slice offsets and masking of the watershed labels.
+//
+// Reference: utils/volume_utils.py:131-139 (apply_size_filter: np.unique counts, ids with
+// count < size_filter are zeroed, then a watershedsNew regrow seeded by the survivors),
+// watershed.py:211-249 (_apply_watershed: 2-D per-slice offsets `offset += max_id`, mask
+// zeroing), two_pass_watershed.py:160-161,199-202 (`exclude` ids, mismatched id space).
+//
+// Labels during the pipeline are unique within the block: in 2-D ws mode the seeds of
+// slice z are numbered after those of slices < z (global rank in the slice-major key
+// space), so one histogram serves all slices; `slice_seed_base[z]` converts back to the
+// reference's per-slice numbering.
+#include "ctws_kernels.h"
+
+namespace ctws {
+
+#define BLOCK_LOOP(i, B)                                                                      \
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (B).N;              \
+         i += (int64_t)gridDim.x * blockDim.x)
+
+// seeds numbered before slice z: rank of key z*Y*X in the seed-root bitmap (2-D ws)
+__global__ void __launch_bounds__(256) k_slice_seed_base(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                         const uint64_t* __restrict__ W,
+                                                         const uint32_t* __restrict__ Wp, uint32_t* sb) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int z = blockIdx.x * blockDim.x + threadIdx.x;
+    if (z >= B.Z) return;
+    const uint32_t f = (uint32_t)((int64_t)z * B.Y * B.X);
+    sb[B.sbase + z] = (B.nd_ws == 2) ? bitmap_rank(W + B.wbase, Wp + B.wbase, f) : 0u;
+}
+
+__global__ void __launch_bounds__(256) k_hist_zero(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                   uint32_t* __restrict__ counts) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t n = (int64_t)S[blockIdx.y].n_seeds + 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        counts[B.base + i] = 0;
+}
+
+// label counts over the whole outer block (3-D) / slice (2-D: labels are slice-unique)
+__global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                              const uint32_t* __restrict__ lab, uint32_t* __restrict__ counts) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    uint32_t* c = counts + B.base;
+    const int lane = threadIdx.x & 63;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < B.N; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool ok = i < B.N;
+        const uint32_t l = ok ? (lab[B.base + i] & ~kFixedBit) : 0xFFFFFFFFu;
+        // wave-uniform label (the common case inside a segment): one atomic per wave
+        const uint32_t l0 = __shfl(l, 0);
+        const uint64_t same = __ballot(ok && l == l0);
+        const uint64_t act = __ballot(ok);
+        if (same == act) {
+            if (lane == 0 && act) atomicAdd(&c[l0], (uint32_t)__popcll(act));
+        } else if (ok) {
+            atomicAdd(&c[l], 1u);
+        }
+    }
+}
+
+// zero small segments; survivors become the regrow seeds (fixed, key (h, 0))
+__global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     FilterParams fp, const uint32_t* __restrict__ counts,
+                                                     const uint8_t* __restrict__ excl, const float* __restrict__ h,
+                                                     uint32_t* __restrict__ lab, uint64_t* __restrict__ key,
+                                                     uint32_t* __restrict__ survivors) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    BLOCK_LOOP(i, B) {
+        const uint32_t l = lab[B.base + i] & ~kFixedBit;
+        bool keep = l != 0 && (counts[B.base + l] >= fp.size_filter || (excl && excl[B.base + l]));
+        if (keep) {
+            lab[B.base + i] = l | kFixedBit;
+            key[B.base + i] = (uint64_t)ordf(h[B.base + i]) << 32;
+            const int z = (B.nd_ws == 2) ? (int)(i / YX) : 0;
+            if (!survivors[B.sbase + z]) survivors[B.sbase + z] = 1;
+        } else {
+            lab[B.base + i] = 0;
+            key[B.base + i] = kInfKey;
+        }
+    }
+}
+
+// per-slice max_id (2-D ws): max per-slice label over in-mask voxels (all voxels without a
+// mask).  Equals watershedsNew's maxRegionLabel of the (regrow) flood when unmasked.
+__global__ void __launch_bounds__(256) k_slice_max(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                   const uint32_t* __restrict__ lab, const uint32_t* __restrict__ sb,
+                                                   uint32_t* __restrict__ smax) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active || B.nd_ws != 2) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    BLOCK_LOOP(i, B) {
+        if (B.mask && !B.mask[i]) continue;
+        const int z = (int)(i / YX);
+        const uint32_t l = lab[B.base + i] & ~kFixedBit;
+        if (l) atomicMax(&smax[B.sbase + z], l - sb[B.sbase + z]);
+    }
+}
+
+// exclusive scan over slices of max_id (uint32 arithmetic, as `wsz += offset` on uint32)
+__global__ void k_slice_offsets(const BlockDesc* __restrict__ D, const BlockStat* S, const uint32_t* __restrict__ smax,
+                                uint32_t* __restrict__ soff) {
+    const BlockDesc& B = D[blockIdx.x];
+    if (threadIdx.x != 0 || !S[blockIdx.x].active || B.nd_ws != 2) return;
+    uint32_t off = 0;
+    for (int z = 0; z < B.Z; ++z) {
+        soff[B.sbase + z] = off;
+        off += smax[B.sbase + z];
+    }
+}
+
+// final uint32 ws of the outer block: 3-D: label, masked -> 0 (watershed.py:245-248);
+// 2-D: per-slice label + slice offset, masked -> 0 (:220-237)
+__global__ void __launch_bounds__(256) k_finalize_ws(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     const uint32_t* __restrict__ sb, const uint32_t* __restrict__ soff,
+                                                     uint32_t* __restrict__ lab) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    BLOCK_LOOP(i, B) {
+        uint32_t l = lab[B.base + i] & ~kFixedBit;
+        const bool inm = !B.mask || B.mask[i];
+        if (B.nd_ws == 2) {
+            const int z = (int)(i / YX);
+            l = inm ? (l - sb[B.sbase + z]) + soff[B.sbase + z] : 0u;
+        } else if (!inm) {
+            l = 0;
+        }
+        lab[B.base + i] = l;
+    }
+}
+
+}  // namespace ctws

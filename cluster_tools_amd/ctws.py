@@ -1,0 +1,206 @@
+"""ctypes binding of libctws.so (include/ctws.h) — the MI355X watershed kernels.
+
+This is the product path: there is no CPU fallback.  If the HIP library is missing or no
+GPU is visible, every call raises.  Build the library with ``python __graft_entry__.py`` or
+``make -C cluster_tools_amd/csrc``.
+"""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+from ._abi import CtwsBlock, make_cfg, dtype_code, CTWS_OK
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libctws.so')
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libctws.so (raises OSError if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise OSError("libctws.so not found at %s: build it with `make -C %s/csrc`"
+                              % (LIB_PATH, _HERE))
+            L = C.CDLL(LIB_PATH)
+            L.ctws_abi_version.restype = C.c_int
+            L.ctws_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+            L.ctws_close.argtypes = [C.c_void_p]
+            L.ctws_close.restype = None
+            L.ctws_last_error.argtypes = [C.c_void_p]
+            L.ctws_last_error.restype = C.c_char_p
+            for fn in ('ctws_ws_blocks', 'ctws_ws_blocks_device'):
+                getattr(L, fn).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+            L.ctws_last_timings.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+            L.ctws_comm_unique_id.argtypes = [C.c_void_p, C.c_void_p]
+            L.ctws_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+            L.ctws_allgather_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+            L.ctws_debug_set_stop.argtypes = [C.c_void_p, C.c_int]
+            L.ctws_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_int64]
+            _lib = L
+        return _lib
+
+
+EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
+                    'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_comm_unique_id', 'ctws_comm_init',
+                    'ctws_allgather_counts', 'ctws_debug_set_stop', 'ctws_debug_read')
+
+
+class CtwsError(RuntimeError):
+    pass
+
+
+class Handle:
+    """One library handle = one GPU, one HIP stream, one device workspace."""
+
+    def __init__(self, device=0):
+        self._h = C.c_void_p()
+        ret = lib().ctws_open(int(device), C.byref(self._h))
+        if ret != CTWS_OK:
+            raise CtwsError("ctws_open(device=%i) failed with %i (no HIP device?)" % (device, ret))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().ctws_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *args):
+        self.close()
+
+    def _check(self, ret, what):
+        if ret != CTWS_OK:
+            msg = lib().ctws_last_error(self._h)
+            raise CtwsError("%s failed (%i): %s" % (what, ret, msg.decode() if msg else ''))
+
+    def timings(self):
+        n = lib().ctws_last_timings(self._h, None, None, 0)
+        names = (C.c_char_p * n)()
+        ms = (C.c_float * n)()
+        lib().ctws_last_timings(self._h, names, ms, n)
+        return {names[i].decode(): float(ms[i]) for i in range(n)}
+
+    # ---- test hooks ----------------------------------------------------------------------
+    def debug_set_stop(self, stage):
+        self._check(lib().ctws_debug_set_stop(self._h, int(stage)), 'ctws_debug_set_stop')
+
+    def debug_read(self, array, block, shape):
+        dt = {'fin': np.float32, 'dt': np.float32, 'seedmap': np.float32, 'hmap': np.float32,
+              'labels': np.uint32, 'cls': np.uint8}[array]
+        out = np.empty(shape, dtype=dt)
+        self._check(lib().ctws_debug_read(self._h, array.encode(), int(block), out.ctypes.data, out.nbytes),
+                    'ctws_debug_read')
+        return out
+
+    # ---- host (numpy) blocks ------------------------------------------------------------
+    def ws_blocks(self, config, block_shape, blocks, pass_id=0):
+        """Run `_ws_block` on numpy blocks (see oracle.ws_blocks for the dict layout).
+
+        Returns [{'output': inner uint64, 'status': int, 'max_label': int}, ...].
+        """
+        cfg = make_cfg(config, block_shape, pass_id)
+        n = len(blocks)
+        arr = (CtwsBlock * n)()
+        keep, results = [], []
+        for i, b in enumerate(blocks):
+            inp = np.ascontiguousarray(b['input'])
+            keep.append(inp)
+            c = arr[i]
+            c.input = inp.ctypes.data
+            c.input_dtype = dtype_code(inp.dtype)
+            if inp.ndim == 4:
+                c.n_channels = inp.shape[0]
+                c.outer_shape[:] = inp.shape[1:]
+            else:
+                c.n_channels = 0
+                c.outer_shape[:] = inp.shape
+            oshape = tuple(c.outer_shape)
+            if b.get('mask') is not None:
+                m = np.ascontiguousarray(b['mask'], dtype=np.uint8)
+                keep.append(m)
+                c.mask = m.ctypes.data
+            c.inner_begin[:] = list(b.get('inner_begin', (0, 0, 0)))
+            ishape = tuple(b.get('inner_shape', oshape))
+            c.inner_shape[:] = list(ishape)
+            c.crop_relabel = int(bool(b.get('crop_relabel', False)))
+            c.block_id = int(b.get('block_id', 0))
+            if b.get('initial_seeds') is not None:
+                s = np.ascontiguousarray(b['initial_seeds'], dtype=np.uint64)
+                keep.append(s)
+                c.initial_seeds = s.ctypes.data
+            out = b.get('out')
+            if out is None:
+                out = np.zeros(ishape, dtype=np.uint64)
+            assert out.dtype == np.uint64 and out.flags.c_contiguous and out.shape == ishape
+            keep.append(out)
+            c.output = out.ctypes.data
+            results.append({'output': out})
+        self._check(lib().ctws_ws_blocks(self._h, C.byref(cfg), arr, n), 'ctws_ws_blocks')
+        for i, r in enumerate(results):
+            r['status'] = int(arr[i].status)
+            r['max_label'] = int(arr[i].max_label)
+        return results
+
+    # ---- device (torch) blocks ----------------------------------------------------------
+    def ws_blocks_device(self, config, block_shape, blocks, pass_id=0):
+        """Same with torch tensors resident on this GPU: blocks[i] has 'input' (outer tensor),
+        'output' (inner uint64/int64 tensor), optional 'mask' (uint8 tensor), 'inner_begin',
+        'crop_relabel', 'block_id'.  Returns [(status, max_label)]."""
+        cfg = make_cfg(config, block_shape, pass_id)
+        n = len(blocks)
+        arr = (CtwsBlock * n)()
+        codes = {'torch.uint8': 1, 'torch.uint16': 2, 'torch.float32': 3, 'torch.float64': 4}
+        for i, b in enumerate(blocks):
+            inp = b['input']
+            assert inp.is_contiguous() and inp.is_cuda
+            c = arr[i]
+            c.input = inp.data_ptr()
+            c.input_dtype = codes[str(inp.dtype)]
+            if inp.dim() == 4:
+                c.n_channels = inp.shape[0]
+                c.outer_shape[:] = list(inp.shape[1:])
+            else:
+                c.n_channels = 0
+                c.outer_shape[:] = list(inp.shape)
+            if b.get('mask') is not None:
+                c.mask = b['mask'].data_ptr()
+            out = b['output']
+            assert out.is_contiguous() and out.element_size() == 8
+            c.inner_begin[:] = list(b.get('inner_begin', (0, 0, 0)))
+            c.inner_shape[:] = list(out.shape)
+            c.crop_relabel = int(bool(b.get('crop_relabel', False)))
+            c.block_id = int(b.get('block_id', 0))
+            c.output = out.data_ptr()
+        self._check(lib().ctws_ws_blocks_device(self._h, C.byref(cfg), arr, n), 'ctws_ws_blocks_device')
+        return [(int(arr[i].status), int(arr[i].max_label)) for i in range(n)]
+
+    # ---- multi-GPU label-count exchange (RCCL) ------------------------------------------
+    def comm_unique_id(self):
+        buf = (C.c_char * 128)()
+        self._check(lib().ctws_comm_unique_id(self._h, buf), 'ctws_comm_unique_id')
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, unique_id):
+        buf = (C.c_char * 128).from_buffer_copy(unique_id)
+        self._check(lib().ctws_comm_init(self._h, int(nranks), int(rank), buf), 'ctws_comm_init')
+
+    def allgather_counts(self, counts, nranks):
+        counts = np.ascontiguousarray(counts, dtype=np.int64)
+        out = np.zeros(len(counts) * nranks, dtype=np.int64)
+        self._check(lib().ctws_allgather_counts(self._h, counts.ctypes.data, len(counts), out.ctypes.data),
+                    'ctws_allgather_counts', 'ctws_debug_set_stop', 'ctws_debug_read')
+        return out

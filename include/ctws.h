@@ -1,0 +1,176 @@
+/*
+ * ctws.h — C-ABI of libctws.so, the MI355X (gfx950) blockwise DT-watershed.
+ *
+ * This is the drop-in boundary for the hot path of cluster_tools' watershed task.
+ * Every entry point is plain C: pointers, sizes, POD structs.  No torch / HIP types.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo):
+ *
+ *   ctws_ws_blocks / ctws_ws_blocks_device
+ *       the per-job block loop `for block_id in block_list: _ws_block(...)`
+ *       cluster_tools/watershed/watershed.py:380-381, i.e. `_ws_block` (:285-341) with
+ *       `_read_data` (:267-282), `_apply_dt` (:139-160), `_make_seeds` (:179-207),
+ *       `_make_hmap` (:163-169), `_apply_watershed` (:211-249) and the halo crop /
+ *       labelVolumeWithBackground / id offset (:326-341);
+ *       and, with cfg.pass_id == 1, `_ws_pass2`
+ *       cluster_tools/watershed/two_pass_watershed.py:210-255 (+ :122-207).
+ *       The caller does the dataset I/O (ds_in[input_bb], ds_out[output_bb] = ...) and the
+ *       "processed block" log lines, exactly as the reference job entry does.
+ *
+ *   ctws_open / ctws_close / ctws_last_error
+ *       process-level setup; the reference has none (vigra is stateless).  One handle per
+ *       (process, GPU), as LocalTask runs one process per job (cluster_tasks.py:507-529).
+ *
+ *   ctws_comm_init / ctws_allgather_counts
+ *       the per-block label-count exchange that assigns compact global id offsets
+ *       (RelabelWorkflow FindUniques -> FindLabeling, relabel/find_labeling.py:104-116,
+ *       and the offsets scan of thresholded_components/merge_offsets.py:111-119), done
+ *       over RCCL instead of .npy/.json files on a shared filesystem.
+ *
+ * Conventions
+ *   - all arrays are C-contiguous numpy-order arrays (axis 0 = z slowest, axis 2 = x fastest)
+ *   - the caller owns every buffer it passes; no pointer is retained after return
+ *   - return value 0 = ok, negative = error; the message is in ctws_last_error(h)
+ *   - calls on one handle are serialized (not re-entrant); use one handle per thread
+ */
+#ifndef CTWS_H
+#define CTWS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CTWS_ABI_VERSION 1
+
+/* error codes */
+#define CTWS_OK            0
+#define CTWS_EINVAL       -1  /* bad argument                                    */
+#define CTWS_EHIP         -2  /* HIP runtime error                               */
+#define CTWS_ENOMEM       -3  /* device allocation failed                        */
+#define CTWS_ECOMM        -4  /* RCCL error                                      */
+#define CTWS_EUNSUPPORTED -5  /* configuration the kernels do not implement      */
+
+/* input dtypes (ds_in dtype; the reference casts to float32 in normalize) */
+#define CTWS_U8  1
+#define CTWS_U16 2
+#define CTWS_F32 3
+#define CTWS_F64 4
+
+/* agglomerate_channels */
+#define CTWS_AGG_MEAN 0
+#define CTWS_AGG_MAX  1
+#define CTWS_AGG_MIN  2
+
+/* per-block status written by ctws_ws_blocks */
+#define CTWS_BLOCK_WRITTEN      0  /* output holds the block's uint64 labels           */
+#define CTWS_BLOCK_SKIPPED_MASK 1  /* inner mask empty: nothing written (:295-297)     */
+#define CTWS_BLOCK_EMPTY        2  /* nothing above threshold: constant offset written */
+#define CTWS_BLOCK_EMPTY_PASS2  3  /* pass 2, nothing above threshold: nothing written */
+
+/*
+ * Task configuration.  Mirrors the watershed task config keys
+ * (watershed.py:50-60, two_pass_watershed.py:39-49) with the inline defaults the job
+ * code applies (config.get(k, default)).
+ */
+typedef struct ctws_cfg {
+    double  threshold;               /* 'threshold' (compared in float32)                  */
+    double  alpha;                   /* 'alpha'                                            */
+    double  sigma_seeds[3];          /* 'sigma_seeds': scalar in [0] or per-axis list      */
+    int32_t sigma_seeds_is_list;     /*   1 if the config held a list/tuple                */
+    double  sigma_weights[3];        /* 'sigma_weights'                                    */
+    int32_t sigma_weights_is_list;
+    int32_t size_filter;             /* 'size_filter'                                      */
+    int32_t apply_dt_2d;             /* 'apply_dt_2d'                                      */
+    int32_t apply_ws_2d;             /* 'apply_ws_2d'                                      */
+    int32_t has_pixel_pitch;         /* 'pixel_pitch' is not None                          */
+    double  pixel_pitch[3];
+    int32_t invert_inputs;           /* 'invert_inputs'                                    */
+    int32_t channel_begin;           /* 'channel_begin'                                    */
+    int32_t channel_end;             /* 'channel_end', < 0 means None                      */
+    int32_t agglomerate_channels;    /* CTWS_AGG_*                                         */
+    int32_t non_maximum_suppression; /* must be 0: nifty NMS is not available (:20-23)     */
+    int32_t pass_id;                 /* 0 = _ws_block, 1 = _ws_pass2                       */
+    int64_t block_shape[3];          /* global block shape: offset = id * prod(shape)      */
+} ctws_cfg;
+
+/*
+ * One block.  `input` holds the OUTER block (block + halo, clipped to the volume) as
+ * ds_in[input_bb] would return it; `output` receives ws[inner_bb] as uint64.
+ */
+typedef struct ctws_block {
+    const void*     input;           /* [C][Z][Y][X] (n_channels > 0) or [Z][Y][X]         */
+    int32_t         input_dtype;     /* CTWS_U8 / U16 / F32 / F64                          */
+    int32_t         n_channels;      /* 0 for a 3-D dataset                                */
+    int64_t         outer_shape[3];  /* Z, Y, X of the outer block                         */
+    const uint8_t*  mask;            /* outer-shaped, nonzero = in mask; NULL = no mask    */
+    int64_t         inner_begin[3];  /* inner block, local to the outer block              */
+    int64_t         inner_shape[3];
+    int32_t         crop_relabel;    /* 1 iff output_bb != input_bb (:327)                 */
+    int32_t         _pad0;
+    int64_t         block_id;        /* id offset = block_id * prod(cfg.block_shape)       */
+    const uint64_t* initial_seeds;   /* pass 2: ds_out[input_bb], outer-shaped; else NULL  */
+    uint64_t*       output;          /* inner-shaped uint64                                */
+    uint64_t        max_label;       /* out: largest local label before the id offset      */
+    int32_t         status;          /* out: CTWS_BLOCK_*                                  */
+    int32_t         _pad1;
+} ctws_block;
+
+typedef struct ctws_handle ctws_handle;
+
+/* version of this header the library was built against */
+int ctws_abi_version(void);
+
+/* open the library on HIP device `device` (index within HIP_VISIBLE_DEVICES) */
+int ctws_open(int device, ctws_handle** out);
+void ctws_close(ctws_handle* h);
+const char* ctws_last_error(const ctws_handle* h);
+
+/*
+ * Run the watershed of `n_blocks` blocks.  input/mask/initial_seeds/output are HOST
+ * pointers; the library stages them through pinned buffers and HBM.
+ */
+int ctws_ws_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks);
+
+/*
+ * Same, but input/mask/initial_seeds/output are DEVICE pointers on the handle's GPU
+ * (e.g. torch tensors' data_ptr()).  Work is enqueued on the handle's stream and the
+ * call returns after the stream has drained.
+ */
+int ctws_ws_blocks_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks);
+
+/*
+ * Stage timings of the last ctws_ws_blocks* call, measured with HIP events on the
+ * handle's stream (milliseconds).  names[i] is a static string.  Returns the count.
+ */
+int ctws_last_timings(const ctws_handle* h, const char** names, float* ms, int max_entries);
+
+/*
+ * Multi-GPU: join an RCCL communicator (unique_id = 128 bytes from ctws_comm_unique_id on
+ * rank 0, distributed by the caller), then all-gather one int64 count per block so every
+ * rank can compute the exclusive scan of label counts (compact global id offsets).
+ */
+int ctws_comm_unique_id(ctws_handle* h, void* unique_id_128);
+int ctws_comm_init(ctws_handle* h, int nranks, int rank, const void* unique_id_128);
+int ctws_allgather_counts(ctws_handle* h, const int64_t* local_counts, int64_t n_local,
+                          int64_t* all_counts /* nranks * n_local */);
+
+/*
+ * Test hooks (used by the parity tests, not by the task code): stop the pipeline after a
+ * stage and read back one block's outer-shaped workspace array of the last batch.
+ *   arrays: "fin" (float32 normalized input), "dt" (float32), "seedmap" (float32 smoothed
+ *           dt), "hmap" (float32), "labels" (uint32; bit 31 = seed), "cls" (uint8)
+ */
+#define CTWS_STOP_NONE  0
+#define CTWS_STOP_SEEDS 1  /* after seed labelling (labels = seeds)            */
+#define CTWS_STOP_FLOOD 2  /* after the first flood (labels = watershed)        */
+#define CTWS_STOP_WS    3  /* after the size filter + 2-D offsets + masking     */
+int ctws_debug_set_stop(ctws_handle* h, int stage);
+int ctws_debug_read(ctws_handle* h, const char* array, int block, void* dst, int64_t nbytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CTWS_H */
