@@ -68,6 +68,7 @@ struct ctws_handle {
     double* h_taps = nullptr;       // pinned [6][128]
     std::vector<std::pair<const char*, float>> timings;
     std::vector<hipEvent_t> events;
+    hipEvent_t fev[2] = {nullptr, nullptr};
     // host-pointer staging
     DevBuf st_in, st_mask, st_init, st_out;
     // test hooks
@@ -336,8 +337,14 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
 }
 
 // ---- flood rounds until no tile is active -----------------------------------------------
-int run_flood(ctws_handle* h, int nd, int nb, int max_tiles, int64_t ntiles, const float* hm, int* rounds_out) {
+int run_flood(ctws_handle* h, int nd, int nb, int max_tiles, int64_t ntiles, const float* hm, int* rounds_out,
+              float* kernel_ms) {
     Workspace& w = h->ws;
+    if (!h->fev[0]) {
+        hipEventCreate(&h->fev[0]);
+        hipEventCreate(&h->fev[1]);
+    }
+    float kms = 0.f;
     HIPCHK(hipMemsetAsync(w.act0, 1, (size_t)ntiles, h->stream));
     HIPCHK(hipMemsetAsync(w.act1, 0, (size_t)ntiles, h->stream));
     uint8_t* cur = w.act0;
@@ -346,18 +353,24 @@ int run_flood(ctws_handle* h, int nd, int nb, int max_tiles, int64_t ntiles, con
     int round = 0;
     for (; round < 1000000; ++round) {
         HIPCHK(hipMemsetAsync(w.counter, 0, 4, h->stream));
+        hipEventRecord(h->fev[0], h->stream);
         if (nd == 3)
             k_flood<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         else
             k_flood<2><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         LAUNCHCHK();
+        hipEventRecord(h->fev[1], h->stream);
         HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, h->fev[0], h->fev[1]);
+        kms += ms;
         if (*h->h_counter == 0) break;
         HIPCHK(hipMemsetAsync(cur, 0, (size_t)ntiles, h->stream));
         std::swap(cur, nxt);
     }
     if (rounds_out) *rounds_out = round + 1;
+    if (kernel_ms) *kernel_ms = kms;
     return CTWS_OK;
 }
 
@@ -505,7 +518,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- normalize + threshold + EDT ------------------------------------------------------
     {
-        dim3 g((unsigned)std::min<int64_t>(((int64_t)maxN * 2 + 255) / 256, 4096), nb);
+        dim3 g((unsigned)std::min<int64_t>((maxN + 65535) / 65536, 256), nb);
         k_input_minmax<<<g, 256, 0, h->stream>>>(w.desc, w.stat);
         LAUNCHCHK();
         PrepParams pp{(float)cfg->threshold, cfg->invert_inputs, cfg->agglomerate_channels, pl.pitch[2] * pl.pitch[2]};
@@ -594,7 +607,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- flood ------------------------------------------------------------------------------
     int rounds1 = 0, rounds2 = 0;
-    if ((r = run_flood(h, pl.nd_ws, nb, max_tiles, TT, w.hm, &rounds1)) != CTWS_OK) return r;
+    float fk1 = 0.f, fk2 = 0.f;
+    if ((r = run_flood(h, pl.nd_ws, nb, max_tiles, TT, w.hm, &rounds1, &fk1)) != CTWS_OK) return r;
     mark("flood");
     if (h->stop_after == CTWS_STOP_FLOOD) {
         HIPCHK(hipStreamSynchronize(h->stream));
@@ -605,11 +619,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     if (cfg->size_filter > 0) {
         uint32_t* counts = (uint32_t*)w.A;
         k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
-        k_hist<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, counts);
+        dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 1024), nb);
+        k_hist<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, counts);
         FilterParams fp{(uint32_t)cfg->size_filter};
         k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, nullptr, w.hm, w.lab, w.key, w.surv);
         LAUNCHCHK();
-        if ((r = run_flood(h, pl.nd_ws, nb, max_tiles, TT, w.hm, &rounds2)) != CTWS_OK) return r;
+        if ((r = run_flood(h, pl.nd_ws, nb, max_tiles, TT, w.hm, &rounds2, &fk2)) != CTWS_OK) return r;
     }
     mark("size_filter");
 
@@ -658,6 +673,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
     h->timings.push_back({"flood_rounds", (float)rounds1});
     h->timings.push_back({"regrow_rounds", (float)rounds2});
+    h->timings.push_back({"flood_kernel_ms", fk1});
+    h->timings.push_back({"size_filter_kernel_ms", fk2});
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : CTWS_BLOCK_EMPTY;
         blocks[i].max_label = st[i].active ? st[i].max_label : 0;
@@ -831,6 +848,8 @@ void ctws_close(ctws_handle* h) {
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);
+    for (auto e : h->fev)
+        if (e) hipEventDestroy(e);
     if (h->h_counter) hipHostFree(h->h_counter);
     if (h->h_taps) hipHostFree(h->h_taps);
     if (h->comm) ncclCommDestroy(h->comm);

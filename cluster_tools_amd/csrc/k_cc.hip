@@ -189,25 +189,25 @@ __global__ void __launch_bounds__(256) k_bitmap(const BlockDesc* __restrict__ D,
                                                 const uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg,
                                                 uint32_t* __restrict__ csum) {
     const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
+    if (!S[blockIdx.y].active || (inner && !B.crop)) return;
     const int64_t n = inner ? B.NI : B.N;
     const int64_t nw = n / 64 + 1;
-    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if ((int64_t)blockIdx.x * 256 >= nw) return;
     const uint32_t* PF = PFg + (inner ? B.ibase : B.base);
-    uint64_t bits = 0;
-    if (w < nw) {
-        const int64_t f0 = w * 64;
-        for (int b = 0; b < 64; ++b) {
-            const int64_t f = f0 + b;
-            if (f < n && PF[f] == (uint32_t)f) bits |= 1ull << b;
-        }
-        Wg[B.wbase + w] = bits;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // each wave builds 64 words; one word = ballot over 64 consecutive keys (coalesced)
+    uint32_t c = 0;
+    for (int j = 0; j < 64; ++j) {
+        const int64_t w = (int64_t)blockIdx.x * 256 + wv * 64 + j;
+        if (w >= nw) break;
+        const int64_t f = w * 64 + lane;
+        const bool root = f < n && PF[f] == (uint32_t)f;
+        const uint64_t bits = __ballot(root);
+        if (lane == 0) Wg[B.wbase + w] = bits;
+        c += (uint32_t)__popcll(bits);
     }
-    uint32_t c = (uint32_t)__popcll(bits);
-    for (int s = 32; s > 0; s >>= 1) c += __shfl_xor((int)c, s);
     __shared__ uint32_t red[4];
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    if (lane == 0) red[wv] = c;
     __syncthreads();
     if (threadIdx.x == 0) csum[B.cbase + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256) k_bitmap(const BlockDesc* __restrict__ D,
 __global__ void __launch_bounds__(256) k_chunk_scan(const BlockDesc* __restrict__ D, BlockStat* S, int inner,
                                                     uint32_t* __restrict__ csum, int which_counter) {
     const BlockDesc& B = D[blockIdx.x];
-    if (!S[blockIdx.x].active) return;
+    if (!S[blockIdx.x].active || (inner && !B.crop)) return;
     const int64_t n = inner ? B.NI : B.N;
     const int64_t nw = n / 64 + 1;
     const int64_t nc = (nw + 255) / 256;
@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(256) k_word_prefix(const BlockDesc* __restrict
                                                      const uint64_t* __restrict__ Wg, const uint32_t* __restrict__ csum,
                                                      uint32_t* __restrict__ Wp) {
     const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
+    if (!S[blockIdx.y].active || (inner && !B.crop)) return;
     const int64_t n = inner ? B.NI : B.N;
     const int64_t nw = n / 64 + 1;
     if ((int64_t)blockIdx.x * 256 >= nw) return;

@@ -37,9 +37,15 @@ __global__ void __launch_bounds__(256) k_input_minmax(const BlockDesc* __restric
         mn = min(mn, (uint32_t)__shfl_xor((int)mn, s));
         mx = max(mx, (uint32_t)__shfl_xor((int)mx, s));
     }
+    __shared__ uint32_t rmn[4], rmx[4];
     if ((threadIdx.x & 63) == 0) {
-        atomicMin(&S[blockIdx.y].in_min, mn);
-        atomicMax(&S[blockIdx.y].in_max, mx);
+        rmn[threadIdx.x >> 6] = mn;
+        rmx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicMin(&S[blockIdx.y].in_min, min(min(rmn[0], rmn[1]), min(rmn[2], rmn[3])));
+        atomicMax(&S[blockIdx.y].in_max, max(max(rmx[0], rmx[1]), max(rmx[2], rmx[3])));
     }
 }
 
@@ -122,7 +128,7 @@ __global__ void __launch_bounds__(256) k_prep_edt_x(const BlockDesc* __restrict_
             const int x = x0 + k;
             if (x < x1) {
                 if (sdist[x]) r = x;
-                dist[k] = r - x;
+                dist[k] = (r >= 0x3FFFFFFF) ? 0x3FFFFFFF : r - x;
             }
         }
         int l = left;
@@ -147,6 +153,24 @@ __global__ void __launch_bounds__(256) k_prep_edt_x(const BlockDesc* __restrict_
     }
     __builtin_amdgcn_wave_barrier();
     for (int x = lane; x < X; x += 64) g2[B.base + rbase + x] = (uint32_t)sdist[x];
+}
+
+// Correctly rounded sqrtf of an integer n < 2^24 (vigra: sqrt on the float32 dest).  The
+// hardware v_sqrt_f32 is not correctly rounded, so round a double sqrt to float and fix it
+// with exact arithmetic: the float r is correct iff mid(r-,r)^2 < n < mid(r,r+)^2 (midpoints
+// have <= 25 significant bits, so their squares are exact in double; no ties for n < 2^24).
+__device__ __forceinline__ float sqrt_rn_int(uint32_t n) {
+    float r = (float)__dsqrt_rn((double)n);
+    const double dn = (double)n;
+    const float up = __uint_as_float(__float_as_uint(r) + 1u);
+    const double mhi = 0.5 * ((double)r + (double)up);
+    if (mhi * mhi < dn) return up;
+    if (r > 0.0f) {
+        const float lo = __uint_as_float(__float_as_uint(r) - 1u);
+        const double mlo = 0.5 * ((double)r + (double)lo);
+        if (mlo * mlo > dn) return lo;
+    }
+    return r;
 }
 
 // ---- EDT pass along y (stride X) or z (stride Y*X), LDS-staged columns -----------------
@@ -195,7 +219,7 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
         const int64_t gi = B.base + obase + p * lstride + xb + c;
         if (ep.final_pass) {
             const uint32_t d2 = min(best, maxd);
-            const float v = __fsqrt_rn((float)d2);
+            const float v = sqrt_rn_int(d2);
             dt[gi] = v;
             const uint32_t ov = ordf(v);
             mn = min(mn, ov);

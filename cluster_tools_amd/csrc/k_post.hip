@@ -38,27 +38,45 @@ __global__ void __launch_bounds__(256) k_hist_zero(const BlockDesc* __restrict__
         counts[B.base + i] = 0;
 }
 
-// label counts over the whole outer block (3-D) / slice (2-D: labels are slice-unique)
+// label counts over the whole outer block (3-D) / slice (2-D: labels are slice-unique).
+// Each workgroup counts a contiguous range in an LDS histogram (labels <= n_seeds fit in
+// 16K bins) and flushes its non-zero bins with one global atomic each.
+constexpr int kHistBins = 16384;
 __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, const BlockStat* S,
                                               const uint32_t* __restrict__ lab, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t sh[kHistBins];
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     uint32_t* c = counts + B.base;
+    const int64_t nb = (int64_t)S[blockIdx.y].n_seeds + 1;
+    const bool use_lds = nb <= kHistBins;
+    if (use_lds)
+        for (int j = threadIdx.x; j < nb; j += 256) sh[j] = 0;
+    __syncthreads();
+    const int64_t chunk = ((B.N + gridDim.x - 1) / gridDim.x + 255) & ~(int64_t)255;
+    const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(B.N, i0 + chunk);
     const int lane = threadIdx.x & 63;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < B.N; i0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = i0 + threadIdx.x;
-        const bool ok = i < B.N;
+    for (int64_t ib = i0; ib < i1; ib += 256) {
+        const int64_t i = ib + threadIdx.x;
+        const bool ok = i < i1;
         const uint32_t l = ok ? (lab[B.base + i] & ~kFixedBit) : 0xFFFFFFFFu;
-        // wave-uniform label (the common case inside a segment): one atomic per wave
         const uint32_t l0 = __shfl(l, 0);
         const uint64_t same = __ballot(ok && l == l0);
         const uint64_t act = __ballot(ok);
         if (same == act) {
-            if (lane == 0 && act) atomicAdd(&c[l0], (uint32_t)__popcll(act));
+            if (lane == 0 && act) {
+                if (use_lds) atomicAdd(&sh[l0], (uint32_t)__popcll(act));
+                else atomicAdd(&c[l0], (uint32_t)__popcll(act));
+            }
         } else if (ok) {
-            atomicAdd(&c[l], 1u);
+            if (use_lds) atomicAdd(&sh[l], 1u);
+            else atomicAdd(&c[l], 1u);
         }
     }
+    if (!use_lds) return;
+    __syncthreads();
+    for (int j = threadIdx.x; j < nb; j += 256)
+        if (sh[j]) atomicAdd(&c[j], sh[j]);
 }
 
 // zero small segments; survivors become the regrow seeds (fixed, key (h, 0))
@@ -93,11 +111,23 @@ __global__ void __launch_bounds__(256) k_slice_max(const BlockDesc* __restrict__
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || B.nd_ws != 2) return;
     const int64_t YX = (int64_t)B.Y * B.X;
-    BLOCK_LOOP(i, B) {
-        if (B.mask && !B.mask[i]) continue;
-        const int z = (int)(i / YX);
-        const uint32_t l = lab[B.base + i] & ~kFixedBit;
-        if (l) atomicMax(&smax[B.sbase + z], l - sb[B.sbase + z]);
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < B.N; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = i0 + threadIdx.x;
+        uint32_t v = 0;
+        int z = -1;
+        if (i < B.N) {
+            z = (int)(i / YX);
+            const uint32_t l = lab[B.base + i] & ~kFixedBit;
+            if (l && (!B.mask || B.mask[i])) v = l - sb[B.sbase + z];
+        }
+        // one atomic per wave when the wave lies in one slice (the common case)
+        const int z0 = __shfl(z, 0);
+        if (__all(z == z0 || z < 0)) {
+            for (int s = 32; s > 0; s >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, s));
+            if ((threadIdx.x & 63) == 0 && v && z0 >= 0) atomicMax(&smax[B.sbase + z0], v);
+        } else if (v) {
+            atomicMax(&smax[B.sbase + z], v);
+        }
     }
 }
 

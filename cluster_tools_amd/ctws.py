@@ -20,10 +20,19 @@ _lock = threading.Lock()
 
 
 def lib():
-    """Load libctws.so (raises OSError if it was not built)."""
+    """Load libctws.so (raises OSError if it was not built).
+
+    If torch is importable it is imported first: its bundled libamdhip64 then satisfies
+    libctws.so's HIP dependency, so the process has ONE HIP runtime and device pointers,
+    streams and contexts are shared with torch.
+    """
     global _lib
     with _lock:
         if _lib is None:
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             if not os.path.exists(LIB_PATH):
                 raise OSError("libctws.so not found at %s: build it with `make -C %s/csrc`"
                               % (LIB_PATH, _HERE))
@@ -160,9 +169,12 @@ class Handle:
         """Same with torch tensors resident on this GPU: blocks[i] has 'input' (outer tensor),
         'output' (inner uint64/int64 tensor), optional 'mask' (uint8 tensor), 'inner_begin',
         'crop_relabel', 'block_id'.  Returns [(status, max_label)]."""
+        import torch
         cfg = make_cfg(config, block_shape, pass_id)
         n = len(blocks)
         arr = (CtwsBlock * n)()
+        # the library runs on its own stream: make torch's pending writes visible first
+        torch.cuda.synchronize()
         codes = {'torch.uint8': 1, 'torch.uint16': 2, 'torch.float32': 3, 'torch.float64': 4}
         for i, b in enumerate(blocks):
             inp = b['input']

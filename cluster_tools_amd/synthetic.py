@@ -82,3 +82,65 @@ def ellipsoid_mask(shape):
     zz, yy, xx = (((np.arange(s, dtype=np.float64) + 0.5) / s - 0.5) / 0.5 for s in shape)
     r = zz[:, None, None] ** 2 + yy[None, :, None] ** 2 + xx[None, None, :] ** 2
     return (r <= 1.0).astype(np.uint8)
+
+
+def boundary_map_torch(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='float32', device='cuda', z_chunk=32):
+    """Same map as `boundary_map`, generated with torch (float64 arithmetic) on `device`."""
+    import torch
+    shape = tuple(int(s) for s in shape)
+    pz, py, px = (float(p) for p in pitch)
+    ncz, ncy, ncx = (int(np.ceil(s / p)) + 2 for s, p in zip(shape, (pz, py, px)))
+    cz, cy, cx = np.meshgrid(np.arange(ncz), np.arange(ncy), np.arange(ncx), indexing='ij')
+    cell = ((cz * ncy + cy) * ncx + cx).astype(np.uint64)
+    pts = []
+    for k, (c, p) in enumerate(((cz, pz), (cy, py), (cx, px))):
+        j = _u01(seed, cell * np.uint64(3) + np.uint64(k))
+        pts.append(torch.from_numpy(((c - 1) + 0.1 + 0.8 * j) * p).to(device))
+    ptz, pty, ptx = pts
+    Z, Y, X = shape
+    out = torch.empty(shape, dtype=getattr(torch, dtype), device=device)
+    yy = torch.arange(Y, dtype=torch.float64, device=device)[:, None].expand(Y, X)
+    xx = torch.arange(X, dtype=torch.float64, device=device)[None, :].expand(Y, X)
+    icy = torch.div(yy, py, rounding_mode='floor').long() + 1
+    icx = torch.div(xx, px, rounding_mode='floor').long() + 1
+    # per-voxel noise hash: splitmix64 in int64 arithmetic (wrapping)
+    s0 = int(splitmix64(np.uint64(seed + 7919)))
+    M = (1 << 64) - 1
+
+    def to_i64(v):
+        v &= M
+        return v - (1 << 64) if v >= (1 << 63) else v
+
+    def smix(x):
+        x = x + to_i64(0x9E3779B97F4A7C15)
+        x = (x ^ ((x >> 30) & ((1 << 34) - 1))) * to_i64(0xBF58476D1CE4E5B9)
+        x = (x ^ ((x >> 27) & ((1 << 37) - 1))) * to_i64(0x94D049BB133111EB)
+        return x ^ ((x >> 31) & ((1 << 33) - 1))
+
+    for z0 in range(0, Z, z_chunk):
+        z1 = min(Z, z0 + z_chunk)
+        zz = torch.arange(z0, z1, dtype=torch.float64, device=device)[:, None, None]
+        icz = torch.div(zz, pz, rounding_mode='floor').long() + 1
+        d1 = torch.full((z1 - z0, Y, X), float('inf'), dtype=torch.float64, device=device)
+        d2 = torch.full_like(d1, float('inf'))
+        for oz in (-1, 0, 1):
+            for oy in (-1, 0, 1):
+                for ox in (-1, 0, 1):
+                    kz = (icz + oz).expand(z1 - z0, Y, X)
+                    ky = (icy + oy)[None].expand(z1 - z0, Y, X)
+                    kx = (icx + ox)[None].expand(z1 - z0, Y, X)
+                    d = torch.sqrt((ptz[kz, ky, kx] - zz) ** 2 + (pty[kz, ky, kx] - yy[None]) ** 2 +
+                                   (ptx[kz, ky, kx] - xx[None]) ** 2)
+                    closer = d < d1
+                    d2 = torch.where(closer, d1, torch.minimum(d2, d))
+                    d1 = torch.where(closer, d, d1)
+        b = torch.clamp(1.0 - (d2 - d1) / 2.5, 0.0, 1.0)
+        vidx = torch.arange(z0 * Y * X, z1 * Y * X, dtype=torch.int64, device=device).view(z1 - z0, Y, X)
+        h = smix(vidx ^ to_i64(s0))
+        u = ((h >> 40) & ((1 << 24) - 1)).to(torch.float64) * (1.0 / (1 << 24))
+        b = torch.clamp(b + noise * (2.0 * u - 1.0), 0.0, 1.0)
+        if dtype == 'uint8':
+            out[z0:z1] = torch.round(255.0 * b).to(torch.uint8)
+        else:
+            out[z0:z1] = b.to(out.dtype)
+    return out

@@ -433,6 +433,63 @@ struct PQCompare {
     }
 };
 
+// ---------------------------------------------------------------------------------------
+// Model of the GPU flood (cluster_tools_amd/csrc/k_flood.hip): the same label-on-push
+// region growing, but the priority is the total order key K = (C, d) then the label, with
+// C the minimax height (float bits, order-preserving) and d the hop distance inside an
+// equal-C plateau.  vigra breaks equal-C ties by heap position instead; this model is what
+// the GPU must reproduce bit for bit, and VI(model, vigra) is the tie-break gap.
+// ---------------------------------------------------------------------------------------
+int g_flood_model = 0;
+
+inline uint32_t ordf(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+struct ModelEntry {
+    uint64_t key;
+    uint32_t label;
+    int64_t node;
+};
+struct ModelCompare {
+    bool operator()(const ModelEntry& a, const ModelEntry& b) const {
+        if (a.key != b.key) return a.key > b.key;
+        return a.label > b.label;
+    }
+};
+
+uint32_t watersheds_model(const float* h, const Dims& d, uint32_t* labels) {
+    auto nb = direct_nbrs(d.nd);
+    std::priority_queue<ModelEntry, std::vector<ModelEntry>, ModelCompare> pq;
+    uint32_t maxRegionLabel = 0;
+    for (int64_t i = 0; i < d.size; ++i)
+        if (labels[i]) {
+            maxRegionLabel = std::max(maxRegionLabel, labels[i]);
+            pq.push({(uint64_t)ordf(h[i]) << 32, labels[i], i});
+        }
+    int64_t c[3];
+    while (!pq.empty()) {
+        const ModelEntry e = pq.top();
+        pq.pop();
+        coords(d, e.node, c);
+        for (auto& nbv : nb) {
+            int64_t t = c[nbv.dim] + nbv.sign;
+            if (t < 0 || t >= d.n[nbv.dim]) continue;
+            int64_t j = e.node + nbv.sign * d.st[nbv.dim];
+            if (labels[j] == 0) {
+                labels[j] = e.label;
+                const uint32_t hb = ordf(h[j]);
+                const uint32_t cc = (uint32_t)(e.key >> 32);
+                const uint64_t k = hb > cc ? ((uint64_t)hb << 32) : e.key + 1ull;
+                pq.push({k, e.label, j});
+            }
+        }
+    }
+    return maxRegionLabel;
+}
+
 uint32_t watersheds_new(const float* h, const Dims& d, uint32_t* labels) {
     bool any = false;
     for (int64_t i = 0; i < d.size && !any; ++i) any = labels[i] != 0;
@@ -442,6 +499,7 @@ uint32_t watersheds_new(const float* h, const Dims& d, uint32_t* labels) {
         local_minima_strict(h, d, mn.data());
         label_with_background<uint8_t>(mn.data(), d, (uint8_t)0, labels);
     }
+    if (g_flood_model) return watersheds_model(h, d, labels);
     auto nb = direct_nbrs(d.nd);
     std::priority_queue<std::pair<int64_t, float>, std::vector<std::pair<int64_t, float>>, PQCompare> pq;
     uint32_t maxRegionLabel = 0;
@@ -797,6 +855,9 @@ thread_local std::string g_err;
 extern "C" {
 
 const char* orc_last_error() { return g_err.c_str(); }
+
+// 0: vigra's heap order (the reference); 1: the GPU flood's (C, d, label) order (model)
+void orc_set_flood_model(int on) { g_flood_model = on; }
 
 // stage-level entry points (for cross-checks against scipy / scikit-image)
 int orc_distance_transform(const uint8_t* fg, int nd, const int64_t* shape, const double* pitch,

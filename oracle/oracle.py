@@ -59,6 +59,16 @@ def _check(ret):
     return ret
 
 
+class flood_model:
+    """Context manager: run the oracle's floods with the GPU's tie-break model."""
+
+    def __enter__(self):
+        lib().orc_set_flood_model(1)
+
+    def __exit__(self, *a):
+        lib().orc_set_flood_model(0)
+
+
 def distance_transform(fg, pixel_pitch=None):
     """vigra.filters.distanceTransform(fg) (background=True); fg != 0 has distance 0."""
     fg = np.ascontiguousarray(fg != 0, dtype=np.uint8)

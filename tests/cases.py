@@ -1,0 +1,50 @@
+"""Shared parity cases: task configs x synthetic blocks (SURVEY.md §8(c) fixture list)."""
+import numpy as np
+
+from cluster_tools_amd.synthetic import boundary_map, ellipsoid_mask
+
+SHAPE = (32, 96, 96)
+BLOCK_SHAPE = (64, 256, 256)
+
+D3 = dict(apply_dt_2d=False, apply_ws_2d=False)
+
+
+def _x(seed=1, shape=SHAPE, dtype='float32'):
+    return boundary_map(shape, seed=seed, dtype=dtype)
+
+
+def make_cases():
+    x = _x()
+    m = ellipsoid_mask(SHAPE)
+    x4 = np.stack([_x(seed=s) for s in (4, 5, 6)])
+    inner = ((0, 16, 16), (32, 64, 64))
+    inner3 = ((2, 16, 16), (28, 64, 64))
+    # plateau-heavy input: quantized boundary map
+    xq = (np.round(_x(seed=7) * 4) / 4).astype(np.float32)
+    # a slice without any boundary (EDT = sqrt(dmax) there)
+    xe = _x(seed=8).copy()
+    xe[5] = 0.0
+    return {
+        '3d_default': (dict(D3), dict(input=x)),
+        '2d_default': ({}, dict(input=x)),
+        '2d_test_cfg_halo': (dict(threshold=.25, sigma_weights=0., halo=[0, 32, 32]),
+                             dict(input=x, inner_begin=inner[0], inner_shape=inner[1], crop_relabel=True)),
+        '3d_aniso_halo': (dict(D3, sigma_seeds=(.5, 2., 2.), sigma_weights=(.5, 2., 2.), halo=[2, 32, 32]),
+                          dict(input=x, inner_begin=inner3[0], inner_shape=inner3[1], crop_relabel=True)),
+        '3d_pitch': (dict(D3, pixel_pitch=(10, 1, 1)), dict(input=x)),
+        '3d_mask': (dict(D3), dict(input=x, mask=m)),
+        '2d_mask': ({}, dict(input=x, mask=m)),
+        '3d_mask_halo': (dict(D3), dict(input=x, mask=m, inner_begin=inner3[0], inner_shape=inner3[1],
+                                        crop_relabel=True)),
+        '4d_mean': (dict(D3), dict(input=x4)),
+        '4d_max_chan': (dict(D3, agglomerate_channels='max', channel_begin=1), dict(input=x4)),
+        '2d_4d_min': (dict(agglomerate_channels='min'), dict(input=x4)),
+        '3d_invert': (dict(D3, invert_inputs=True, threshold=.3), dict(input=x)),
+        '3d_u8': (dict(D3), dict(input=_x(seed=9, dtype='uint8'))),
+        '3d_f64': (dict(D3), dict(input=x.astype(np.float64))),
+        '3d_plateaus': (dict(D3, sigma_seeds=0., sigma_weights=0.), dict(input=xq)),
+        '2d_plateaus': (dict(sigma_seeds=0.), dict(input=xq)),
+        '2d_empty_slice': ({}, dict(input=xe)),
+        '3d_no_sizefilter': (dict(D3, size_filter=0), dict(input=x)),
+        '3d_sigma0_alpha1': (dict(D3, sigma_seeds=0, alpha=1.0), dict(input=x)),
+    }
