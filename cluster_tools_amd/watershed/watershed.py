@@ -1,0 +1,209 @@
+#! /usr/bin/env python
+"""Watershed task: drop-in for cluster_tools/watershed/watershed.py.
+
+Task surface (same classes, parameters, task_name, config keys and defaults as
+watershed.py:34-128): WatershedBase / WatershedLocal / WatershedSlurm / WatershedLSF.
+Job entry `watershed(job_id, config_path)` (watershed.py:344-384): the per-block loop of
+`_ws_block` (:285-341) becomes batched calls into libctws.so (the gfx950 kernels); this module
+keeps the dataset I/O, the outer/inner bounding boxes (_get_bbs, :252-264) and the
+"processed block"/"processed job" log protocol.  Input reads of the next batch and output
+writes of the previous one overlap the GPU work of the current batch.
+"""
+import json
+import os
+import sys
+from concurrent import futures
+
+import numpy as np
+
+from cluster_tools_amd import luigi_compat as luigi
+import cluster_tools_amd.utils.volume_utils as vu
+import cluster_tools_amd.utils.function_utils as fu
+from cluster_tools_amd.utils.blocking import Blocking
+from cluster_tools_amd.cluster_tasks import SlurmTask, LocalTask, LSFTask
+
+
+class WatershedBase(luigi.Task):
+    """Watershed base class."""
+
+    task_name = 'watershed'
+    src_file = os.path.abspath(__file__)
+
+    input_path = luigi.Parameter()
+    input_key = luigi.Parameter()
+    output_path = luigi.Parameter()
+    output_key = luigi.Parameter()
+    mask_path = luigi.Parameter(default='')
+    mask_key = luigi.Parameter(default='')
+
+    @staticmethod
+    def default_task_config():
+        config = LocalTask.default_task_config()
+        config.update({'threshold': .5,
+                       'apply_dt_2d': True, 'pixel_pitch': None,
+                       'apply_ws_2d': True, 'sigma_seeds': 2., 'size_filter': 25,
+                       'sigma_weights': 2., 'halo': [0, 0, 0],
+                       'channel_begin': 0, 'channel_end': None,
+                       'agglomerate_channels': 'mean', 'alpha': 0.8,
+                       'invert_inputs': False, 'non_maximum_suppression': False})
+        return config
+
+    def clean_up_for_retry(self, block_list, prefix=None):
+        super().clean_up_for_retry(block_list)
+
+    def run_impl(self):
+        shebang, block_shape, roi_begin, roi_end, block_list_path = self.global_config_values(True)
+        self.init(shebang)
+        shape = vu.get_shape(self.input_path, self.input_key)
+        if len(shape) == 4:
+            shape = shape[1:]
+        ws_config = self.get_task_config()
+        chunks = tuple(bs // 2 for bs in block_shape)
+        with vu.file_reader(self.output_path) as f:
+            f.require_dataset(self.output_key, shape=shape, chunks=chunks, compression='gzip', dtype='uint64')
+        ws_config.update({'input_path': self.input_path, 'input_key': self.input_key,
+                          'output_path': self.output_path, 'output_key': self.output_key,
+                          'block_shape': block_shape})
+        if self.mask_path != '':
+            assert self.mask_key != ''
+            ws_config.update({'mask_path': self.mask_path, 'mask_key': self.mask_key})
+        if self.n_retries == 0:
+            block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end,
+                                             block_list_path=block_list_path)
+        else:
+            block_list = self.block_list
+            self.clean_up_for_retry(block_list)
+        self._write_log('scheduling %i blocks to be processed' % len(block_list))
+        n_jobs = min(len(block_list), self.max_jobs)
+        self.prepare_jobs(n_jobs, block_list, ws_config)
+        self.submit_jobs(n_jobs)
+        self.wait_for_jobs()
+        self.check_jobs(n_jobs)
+
+
+class WatershedLocal(WatershedBase, LocalTask):
+    """Watershed on the local machine (one GPU handle per job process)."""
+
+
+class WatershedSlurm(WatershedBase, SlurmTask):
+    """Watershed on a slurm cluster."""
+
+
+class WatershedLSF(WatershedBase, LSFTask):
+    """Watershed on an lsf cluster."""
+
+
+#
+# Implementation
+#
+
+def _get_bbs(blocking, block_id, config):
+    """(input_bb, inner_bb, output_bb) as watershed.py:252-264."""
+    halo = list(config.get('halo', [0, 0, 0]))
+    if sum(halo) > 0:
+        block = blocking.getBlockWithHalo(block_id, halo)
+        input_bb = vu.block_to_bb(block.outerBlock)
+        output_bb = vu.block_to_bb(block.innerBlock)
+        inner_bb = vu.block_to_bb(block.innerBlockLocal)
+    else:
+        block = blocking.getBlock(block_id)
+        input_bb = output_bb = vu.block_to_bb(block)
+        inner_bb = tuple(slice(0, b.stop - b.start) for b in input_bb)
+    return input_bb, inner_bb, output_bb
+
+
+def _read_block(blocking, block_id, ds_in, ds_out, mask, config, pass_id):
+    """Everything `_ws_block` reads for one block (watershed.py:287-303), as a libctws block."""
+    input_bb, inner_bb, output_bb = _get_bbs(blocking, block_id, config)
+    b = {'block_id': block_id, 'output_bb': output_bb, 'crop_relabel': output_bb != input_bb,
+         'inner_begin': [s.start for s in inner_bb], 'inner_shape': [s.stop - s.start for s in inner_bb]}
+    if mask is not None:
+        in_mask = np.asarray(mask[input_bb]).astype('bool')
+        if in_mask[inner_bb].sum() == 0:
+            b['skip'] = True  # watershed.py:295-297: nothing to do, nothing written
+            return b
+        b['mask'] = in_mask.view('uint8')
+    if ds_in.ndim == 4:
+        cb, ce = config.get('channel_begin', 0), config.get('channel_end', None)
+        b['input'] = ds_in[(slice(cb, ce),) + input_bb]
+    else:
+        b['input'] = ds_in[input_bb]
+    if pass_id == 1:
+        b['initial_seeds'] = ds_out[input_bb]
+    return b
+
+
+def _device():
+    return int(os.environ.get('CTWS_DEVICE', os.environ.get('LOCAL_RANK', '0')))
+
+
+def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, batch_blocks=None):
+    """Run `_ws_block` (pass 0) or `_ws_pass2` (pass 1) for `block_list` on the GPU."""
+    from cluster_tools_amd import ctws
+    block_shape = list(config['block_shape'])
+    lib_config = dict(config)
+    if ds_in.ndim == 4:
+        # the host already sliced the channel range
+        lib_config['channel_begin'], lib_config['channel_end'] = 0, None
+    if config.get('non_maximum_suppression', True if pass_id == 1 else False):
+        fu.log("non-maximum suppression was activated, but is not available")
+    batch_blocks = batch_blocks or int(config.get('gpu_batch_blocks', 16))
+    batches = [block_list[i:i + batch_blocks] for i in range(0, len(block_list), batch_blocks)]
+    n_io = max(1, int(config.get('threads_per_job', 1)))
+    ds_in.n_threads = ds_out.n_threads = max(n_io, 4)
+
+    def read_batch(ids):
+        return [_read_block(blocking, bid, ds_in, ds_out, mask, config, pass_id) for bid in ids]
+
+    def write_batch(blocks, results):
+        for b, r in zip(blocks, results):
+            if r is not None and r['status'] in (0, 2):   # written / empty block: constant offset
+                ds_out[b['output_bb']] = r['output']
+            fu.log_block_success(b['block_id'])
+
+    with ctws.Handle(_device()) as h, futures.ThreadPoolExecutor(2) as io:
+        nxt = io.submit(read_batch, batches[0]) if batches else None
+        pending_write = None
+        for bi in range(len(batches)):
+            blocks = nxt.result()
+            nxt = io.submit(read_batch, batches[bi + 1]) if bi + 1 < len(batches) else None
+            for b in blocks:
+                fu.log("start processing block %i" % b['block_id'])
+            todo = [b for b in blocks if not b.get('skip')]
+            res = h.ws_blocks(lib_config, block_shape, todo, pass_id=pass_id) if todo else []
+            by_id = {b['block_id']: r for b, r in zip(todo, res)}
+            if pending_write is not None:
+                pending_write.result()
+            pending_write = io.submit(write_batch, blocks, [by_id.get(b['block_id']) for b in blocks])
+        if pending_write is not None:
+            pending_write.result()
+
+
+def watershed(job_id, config_path):
+    fu.log("start processing job %i" % job_id)
+    fu.log("reading config from %s" % config_path)
+    with open(config_path) as f:
+        config = json.load(f)
+    input_path, input_key = config['input_path'], config['input_key']
+    shape = list(vu.get_shape(input_path, input_key))
+    if len(shape) == 4:
+        shape = shape[1:]
+    block_shape = list(config['block_shape'])
+    block_list = config['block_list']
+    output_path, output_key = config['output_path'], config['output_key']
+    blocking = Blocking([0, 0, 0], shape, block_shape)
+    with vu.file_reader(input_path, 'r') as f_in, vu.file_reader(output_path) as f_out:
+        ds_in = f_in[input_key]
+        assert ds_in.ndim in (3, 4)
+        ds_out = f_out[output_key]
+        assert ds_out.ndim == 3
+        mask = vu.load_mask(config['mask_path'], config['mask_key'], shape) if 'mask_path' in config else None
+        run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0)
+    fu.log_job_success(job_id)
+
+
+if __name__ == '__main__':
+    path = sys.argv[1]
+    assert os.path.exists(path), path
+    job_id = int(os.path.split(path)[1].split('.')[0].split('_')[-1])
+    watershed(job_id, path)

@@ -1,0 +1,48 @@
+"""WatershedWorkflow: drop-in for cluster_tools/watershed/watershed_workflow.py:10-69.
+
+Watershed{Local,Slurm,LSF} (or TwoPassWatershed* with two_pass=True), then RelabelWorkflow
+(FindUniques -> FindLabeling -> Write in place, assignment table at
+output_path/'relabel_watershed').  The optional post-watershed agglomeration of the reference
+(agglomeration=True, nifty RAG + clustering) is out of scope for this build and raises.
+"""
+from cluster_tools_amd import luigi_compat as luigi
+from cluster_tools_amd.cluster_tasks import WorkflowBase
+from cluster_tools_amd.watershed import watershed as watershed_tasks
+from cluster_tools_amd.watershed import two_pass_watershed as two_pass_tasks
+from cluster_tools_amd.relabel import RelabelWorkflow
+
+
+class WatershedWorkflow(WorkflowBase):
+    input_path = luigi.Parameter()
+    input_key = luigi.Parameter()
+    output_path = luigi.Parameter()
+    output_key = luigi.Parameter()
+    mask_path = luigi.Parameter(default='')
+    mask_key = luigi.Parameter(default='')
+    two_pass = luigi.BoolParameter(default=False)
+    agglomeration = luigi.BoolParameter(default=False)
+
+    def requires(self):
+        if self.agglomeration:
+            raise NotImplementedError("agglomeration=True (nifty RAG + agglomerative clustering) is not "
+                                      "part of this build")
+        if self.two_pass:
+            ws_task = getattr(two_pass_tasks, self._get_task_name('TwoPassWatershed'))
+        else:
+            ws_task = getattr(watershed_tasks, self._get_task_name('Watershed'))
+        dep = ws_task(tmp_folder=self.tmp_folder, max_jobs=self.max_jobs, config_dir=self.config_dir,
+                      input_path=self.input_path, input_key=self.input_key,
+                      output_path=self.output_path, output_key=self.output_key,
+                      mask_path=self.mask_path, mask_key=self.mask_key)
+        return RelabelWorkflow(tmp_folder=self.tmp_folder, max_jobs=self.max_jobs, config_dir=self.config_dir,
+                               target=self.target, input_path=self.output_path, input_key=self.output_key,
+                               assignment_path=self.output_path, assignment_key='relabel_watershed',
+                               dependency=dep)
+
+    @staticmethod
+    def get_config():
+        configs = WorkflowBase.get_config()
+        configs.update({'watershed': watershed_tasks.WatershedLocal.default_task_config(),
+                        'two_pass_watershed': two_pass_tasks.TwoPassWatershedLocal.default_task_config(),
+                        **RelabelWorkflow.get_config()})
+        return configs

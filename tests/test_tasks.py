@@ -1,0 +1,174 @@
+"""CPU tests of the drop-in task surface: blocking, checkerboard, n5/zarr I/O, job configs,
+the log protocol and retry (mirroring the reference's test/utils and test/retry tests)."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from cluster_tools_amd import luigi_compat as luigi
+from cluster_tools_amd.utils.blocking import Blocking
+from cluster_tools_amd.utils import volume_utils as vu
+from cluster_tools_amd.utils.function_utils import tail
+from cluster_tools_amd.utils import parse_utils as pu
+
+
+def test_blocking_c_order_and_halo():
+    b = Blocking([0, 0, 0], [100, 100, 60], [64, 32, 32])
+    assert b.blocksPerAxis == [2, 4, 2] and b.numberOfBlocks == 16
+    assert b.getBlock(1).begin == [0, 0, 32] and b.getBlock(1).end == [64, 32, 60]
+    assert b.getBlock(2).begin == [0, 32, 0]
+    bh = b.getBlockWithHalo(3, [8, 8, 8])
+    assert bh.outerBlock.begin == [0, 24, 24] and bh.outerBlock.end == [72, 72, 60]
+    assert bh.innerBlockLocal.begin == [0, 8, 8] and bh.innerBlockLocal.end == [64, 40, 36]
+    assert b.getNeighborId(0, 0, False) == 8 and b.getNeighborId(0, 2, True) == -1
+    assert b.coordinatesToBlockId([70, 40, 40]) == 11
+    assert list(b.getBlockIdsOverlappingBoundingBox([0, 0, 0], [10, 40, 10])) == [0, 2]
+
+
+def _checkerboard_recursive(blocking):
+    """The reference's recursive DFS (utils/volume_utils.py:142-164), for comparison."""
+    blocks_a, blocks_b, all_blocks = [0], [], [0]
+
+    def recurse(current, insert_list):
+        other = blocks_a if insert_list is blocks_b else blocks_b
+        for dim in range(3):
+            ngb = blocking.getNeighborId(current, dim, False)
+            if ngb != -1 and ngb not in all_blocks:
+                insert_list.append(ngb)
+                all_blocks.append(ngb)
+                recurse(ngb, other)
+    recurse(0, blocks_b)
+    return blocks_a, blocks_b
+
+
+@pytest.mark.parametrize('grid', [(2, 2, 2), (4, 2, 2), (2, 6, 4), (5, 4, 3)])
+def test_checkerboard_matches_recursive_reference(grid):
+    b = Blocking([0, 0, 0], [g * 10 for g in grid], [10, 10, 10])
+    ref = _checkerboard_recursive(b)
+    a, bb = vu.make_checkerboard_block_lists(b)
+    assert (a, bb) == ref
+    for lst, parity in ((a, 0), (bb, 1)):
+        assert all(sum(b.blockCoordinates(x)) % 2 == parity for x in lst)
+
+
+def test_checkerboard_odd_block_count_asserts():
+    b = Blocking([0, 0, 0], [30, 30, 30], [10, 10, 10])
+    with pytest.raises(AssertionError):
+        vu.make_checkerboard_block_lists(b)
+
+
+def test_checkerboard_large_grid_no_recursion_limit():
+    b = Blocking([0, 0, 0], [32 * 64, 8 * 256, 8 * 256], [64, 256, 256])  # config 5: 2048 blocks
+    a, bb = vu.make_checkerboard_block_lists(b)
+    assert len(a) == len(bb) == 1024
+
+
+@pytest.mark.parametrize('ext', ['n5', 'zr'])
+def test_file_reader_roundtrip(tmp_path, ext):
+    path = str(tmp_path / ('data.' + ext))
+    x = np.random.RandomState(0).randint(0, 1 << 40, size=(37, 41, 23)).astype('uint64')
+    with vu.file_reader(path) as f:
+        ds = f.require_dataset('a/b', shape=x.shape, chunks=(8, 16, 8), compression='gzip', dtype='uint64')
+        ds[:] = x
+        ds[3:11, 5:40, 2:9] = 7
+    x[3:11, 5:40, 2:9] = 7
+    with vu.file_reader(path, 'r') as f:
+        assert np.array_equal(f['a/b'][:], x)
+        assert np.array_equal(f['a/b'][5:30, 1, :], x[5:30, 1, :])
+    assert vu.get_shape(path, 'a/b') == x.shape
+
+
+def test_n5_layout_is_standard(tmp_path):
+    """attributes.json in F order and big-endian chunks with the n5 header."""
+    import gzip
+    path = str(tmp_path / 'd.n5')
+    with vu.file_reader(path) as f:
+        ds = f.create_dataset('x', shape=(3, 4, 5), chunks=(3, 4, 5), dtype='uint16', compression='gzip')
+        ds[:] = np.arange(60, dtype='uint16').reshape(3, 4, 5)
+    meta = json.load(open(os.path.join(path, 'x', 'attributes.json')))
+    assert meta['dimensions'] == [5, 4, 3] and meta['dataType'] == 'uint16'
+    raw = open(os.path.join(path, 'x', '0', '0', '0'), 'rb').read()
+    assert list(np.frombuffer(raw[:4], '>u2')) == [0, 3] and list(np.frombuffer(raw[4:16], '>u4')) == [5, 4, 3]
+    data = np.frombuffer(gzip.decompress(raw[16:]), '>u2')
+    assert np.array_equal(data, np.arange(60))
+
+
+def test_tail(tmp_path):
+    p = tmp_path / 'out.txt'
+    p.write_text('abcd\n1234\n5678\nwxyz\n')
+    assert tail(str(p), 3) == ['1234', '5678', 'wxyz']
+
+
+def test_log_protocol_parsing(tmp_path):
+    p = tmp_path / 'w_0.log'
+    p.write_text('2020-01-01 10:00:00.000: start\n2020-01-01 10:00:01.000: processed block 3\n'
+                 '2020-01-01 10:00:05.500: processed block 7\n2020-01-01 10:00:06.000: processed job 0\n')
+    assert pu.parse_job(str(p), 0) and not pu.parse_job(str(p), 1)
+    assert pu.parse_blocks(str(p)) == [3, 7]
+    assert pu.parse_runtime(str(p)) == 6.0
+    q = tmp_path / 'w_1.log'
+    q.write_text('2020-01-01 10:00:00.000: processed block 1\n')
+    assert not pu.parse_job(str(q), 1)
+    assert pu.parse_blocks_task(str(tmp_path / 'w_'), 2, [0]) == [1]
+
+
+def _configs(tmp_path, block_shape, **gc):
+    cfg_dir = tmp_path / 'configs'
+    cfg_dir.mkdir()
+    from cluster_tools_amd.cluster_tasks import BaseClusterTask
+    g = BaseClusterTask.default_global_config()
+    g.update({'shebang': '#! ' + sys.executable, 'block_shape': list(block_shape)}, **gc)
+    (cfg_dir / 'global.config').write_text(json.dumps(g))
+    return str(cfg_dir)
+
+
+def test_retry_reruns_failed_blocks(tmp_path):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from failing_task import FailingTaskLocal
+    cfg = _configs(tmp_path, (10, 32, 32), max_num_retries=1)
+    out = str(tmp_path / 'out.n5')
+    task = FailingTaskLocal(output_path=out, output_key='data', shape=[40, 64, 64], config_dir=cfg,
+                            tmp_folder=str(tmp_path / 'tmp'), max_jobs=4)
+    assert luigi.build([task], local_scheduler=True)
+    with vu.file_reader(out, 'r') as f:
+        assert (f['data'][:] == 1).all()
+    cfgs = sorted(os.listdir(str(tmp_path / 'tmp')))
+    assert 'failing_task_job_0.config' in cfgs
+    blocks = json.load(open(str(tmp_path / 'tmp' / 'failing_task_job_1.config')))['block_list']
+    assert all(b % 4 == 1 for b in blocks)   # the retry re-ran exactly the failed blocks
+    assert os.path.exists(str(tmp_path / 'tmp' / 'failing_task.log'))
+
+
+def test_no_retry_without_budget_renames_log(tmp_path):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from failing_task import FailingTaskLocal
+    cfg = _configs(tmp_path, (10, 32, 32), max_num_retries=0)
+    task = FailingTaskLocal(output_path=str(tmp_path / 'o.n5'), output_key='data', shape=[40, 64, 64],
+                            config_dir=cfg, tmp_folder=str(tmp_path / 'tmp'), max_jobs=4)
+    assert not luigi.build([task], local_scheduler=True)
+    assert os.path.exists(str(tmp_path / 'tmp' / 'failing_task_failed.log'))
+
+
+def test_watershed_task_writes_job_configs_and_fails_loudly_without_gpu(tmp_path):
+    """Without a GPU the job processes die before 'processed job': the task raises, the
+    workflow returns False and the task log is renamed (no silent CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from cluster_tools_amd.synthetic import boundary_map
+    from cluster_tools_amd.watershed import WatershedWorkflow
+    cfg = _configs(tmp_path, (16, 32, 32))
+    inp = str(tmp_path / 'in.n5')
+    with vu.file_reader(inp) as f:
+        f.create_dataset('raw', data=boundary_map((32, 64, 64), seed=2), chunks=(16, 32, 32))
+    wf = WatershedWorkflow(input_path=inp, input_key='raw', output_path=str(tmp_path / 'ws.n5'), output_key='ws',
+                           config_dir=cfg, tmp_folder=str(tmp_path / 'tmp'), target='local', max_jobs=2)
+    assert not luigi.build([wf], local_scheduler=True)
+    tmp = tmp_path / 'tmp'
+    job0 = json.load(open(str(tmp / 'watershed_job_0.config')))
+    assert job0['block_list'] == [0, 2, 4, 6] and job0['threshold'] == .5 and job0['block_shape'] == [16, 32, 32]
+    assert os.path.exists(str(tmp / 'watershed_failed.log'))
+    assert os.path.exists(str(tmp / 'watershed.py'))
+    assert open(str(tmp / 'watershed.py')).readline().strip() == '#! ' + sys.executable

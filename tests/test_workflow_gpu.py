@@ -1,0 +1,112 @@
+"""End-to-end WatershedWorkflow (target='local') on the GPU, with the reference's test configs
+(test/watershed/test_watershed.py:86-136) on a synthetic n5 volume.  Checks the reference's
+`_check_result` invariants (:53-70) and compares the watershed stage with the oracle run
+block by block (same blocking, halos and offsets)."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from cluster_tools_amd import luigi_compat as luigi
+from cluster_tools_amd.utils import volume_utils as vu
+from cluster_tools_amd.utils.blocking import Blocking
+from cluster_tools_amd.synthetic import boundary_map, ellipsoid_mask
+from cluster_tools_amd.metrics import vi_scores
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SHAPE = (40, 128, 128)
+BLOCK_SHAPE = [10, 64, 64]
+
+CONFIGS = {
+    'ws_2d': dict(apply_dt_2d=True, apply_ws_2d=True, threshold=0.25, sigma_weights=0., halo=[0, 16, 16]),
+    'ws_3d': dict(apply_dt_2d=False, apply_ws_2d=False, sigma_seeds=(.5, 2., 2.), sigma_weights=(.5, 2., 2.),
+                  halo=[2, 16, 16]),
+    'ws_pixel_pitch': dict(apply_dt_2d=False, apply_ws_2d=False, pixel_pitch=(10, 1, 1)),
+}
+
+
+def _setup(tmp_path, name, with_mask):
+    from cluster_tools_amd.watershed.watershed import WatershedLocal
+    cfg_dir = tmp_path / 'configs'
+    cfg_dir.mkdir()
+    g = WatershedLocal.default_global_config()
+    g['shebang'] = '#! ' + sys.executable
+    g['block_shape'] = BLOCK_SHAPE
+    (cfg_dir / 'global.config').write_text(json.dumps(g))
+    c = WatershedLocal.default_task_config()
+    c.update(CONFIGS[name])
+    (cfg_dir / 'watershed.config').write_text(json.dumps(c))
+    inp = str(tmp_path / 'data.n5')
+    x = boundary_map(SHAPE, seed=3)
+    with vu.file_reader(inp) as f:
+        f.create_dataset('boundaries', data=x, chunks=(10, 64, 64))
+        if with_mask:
+            f.create_dataset('mask', data=ellipsoid_mask(SHAPE), chunks=(10, 64, 64))
+    return str(cfg_dir), inp, x, c
+
+
+def _oracle_volume(x, c, mask):
+    """The reference's per-block `_ws_block` over the volume, via the oracle."""
+    blocking = Blocking([0, 0, 0], list(SHAPE), BLOCK_SHAPE)
+    out = np.zeros(SHAPE, np.uint64)
+    halo = c.get('halo', [0, 0, 0])
+    for bid in range(blocking.numberOfBlocks):
+        if sum(halo) > 0:
+            bh = blocking.getBlockWithHalo(bid, halo)
+            ib, ob, il = vu.block_to_bb(bh.outerBlock), vu.block_to_bb(bh.innerBlock), vu.block_to_bb(bh.innerBlockLocal)
+        else:
+            ib = ob = vu.block_to_bb(blocking.getBlock(bid))
+            il = tuple(slice(0, s.stop - s.start) for s in ib)
+        b = dict(input=x[ib], block_id=bid, inner_begin=[s.start for s in il],
+                 inner_shape=[s.stop - s.start for s in il], crop_relabel=ob != ib)
+        if mask is not None:
+            b['mask'] = mask[ib]
+        r = O.ws_blocks(c, BLOCK_SHAPE, [b])[0]
+        if r['status'] in (0, 2):
+            out[ob] = r['output']
+    return out
+
+
+def _check_result(res, with_mask):
+    """test_watershed.py:53-70."""
+    assert res.shape == SHAPE
+    assert not np.allclose(res, 0)
+    assert (0 in res) == with_mask
+    ids0 = np.unique(res)
+    cc, _ = O.label_with_background(res.astype('uint32'))
+    n_cc = len(np.unique(cc))
+    assert len(ids0) == n_cc, "disconnected segments"
+
+
+@pytest.mark.parametrize('name', sorted(CONFIGS))
+@pytest.mark.parametrize('with_mask', [False, True])
+def test_watershed_workflow(tmp_path, name, with_mask):
+    from cluster_tools_amd.watershed import WatershedWorkflow
+    from cluster_tools_amd.watershed.watershed import WatershedLocal
+    cfg_dir, inp, x, c = _setup(tmp_path, name, with_mask)
+    out = str(tmp_path / 'ws.n5')
+    mask_kw = dict(mask_path=inp, mask_key='mask') if with_mask else {}
+    # 1. the watershed task alone: compare with the oracle block by block
+    ws = WatershedLocal(input_path=inp, input_key='boundaries', output_path=out, output_key='ws_raw',
+                        config_dir=cfg_dir, tmp_folder=str(tmp_path / 'tmp_ws'), max_jobs=2, **mask_kw)
+    assert luigi.build([ws], local_scheduler=True)
+    with vu.file_reader(out, 'r') as f:
+        raw = f['ws_raw'][:]
+    ref = _oracle_volume(x, c, ellipsoid_mask(SHAPE) if with_mask else None)
+    vis, vim = vi_scores(raw, ref, [0] if with_mask else None)
+    assert vis + vim <= 0.01, (vis, vim)
+    # 2. the whole workflow (watershed + relabel)
+    wf = WatershedWorkflow(input_path=inp, input_key='boundaries', output_path=out, output_key='ws',
+                           config_dir=cfg_dir, tmp_folder=str(tmp_path / 'tmp'), target='local', max_jobs=2,
+                           **mask_kw)
+    assert luigi.build([wf], local_scheduler=True)
+    with vu.file_reader(out, 'r') as f:
+        res = f['ws'][:]
+        assert f['ws'].attrs['maxId'] == int(res.max())
+        table = f['relabel_watershed'][:]
+    _check_result(res.astype('uint64'), with_mask)
+    assert len(np.unique(res)) == len(table)
