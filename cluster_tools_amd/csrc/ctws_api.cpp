@@ -337,8 +337,8 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
 }
 
 // ---- flood rounds until no tile is active -----------------------------------------------
-int run_flood(ctws_handle* h, int nd, int nb, int max_tiles, int64_t ntiles, const float* hm, int* rounds_out,
-              float* kernel_ms) {
+int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_t ntiles, const float* hm,
+              int* rounds_out, float* kernel_ms) {
     Workspace& w = h->ws;
     if (!h->fev[0]) {
         hipEventCreate(&h->fev[0]);
@@ -354,7 +354,11 @@ int run_flood(ctws_handle* h, int nd, int nb, int max_tiles, int64_t ntiles, con
     for (; round < 1000000; ++round) {
         HIPCHK(hipMemsetAsync(w.counter, 0, 4, h->stream));
         hipEventRecord(h->fev[0], h->stream);
-        if (nd == 3)
+        if (packed && nd == 3)
+            k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
+        else if (packed)
+            k_flood_packed<2><<<g, 128, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
+        else if (nd == 3)
             k_flood<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         else
             k_flood<2><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
@@ -384,7 +388,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0;
     int maxZ = 0, maxY = 0, maxX = 0, max_tiles = 0;
     int64_t maxN = 0, maxNI = 0;
-    const int TZ = pl.nd_ws == 3 ? 4 : 1, TY = pl.nd_ws == 3 ? 8 : 32, TX = 64;
     const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
     for (int i = 0; i < nb; ++i) {
         const ctws_block& b = blocks[i];
@@ -430,10 +433,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             d.C = 1;
         }
         d.id_offset = (uint64_t)b.block_id * bvol;
-        d.tz = (d.Z + TZ - 1) / TZ;
-        d.ty = (d.Y + TY - 1) / TY;
-        d.tx = (d.X + TX - 1) / TX;
-        d.tbase = (int)TT;
         d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
                             (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
         T += d.N;
@@ -441,13 +440,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         TW += words_of(d.N);
         TC += chunks_of(d.N);
         TS += d.Z;
-        TT += (int64_t)d.tz * d.ty * d.tx;
         maxZ = std::max(maxZ, d.Z);
         maxY = std::max(maxY, d.Y);
         maxX = std::max(maxX, d.X);
         maxN = std::max(maxN, d.N);
         maxNI = std::max(maxNI, d.NI);
-        max_tiles = std::max(max_tiles, d.tz * d.ty * d.tx);
         // validation against what the kernels assume
         if (d.X > 1024 || d.Y > 2048 || d.Z > 2048 || d.N >= (1ll << 31)) {
             h->err = "outer block too large for the kernels (X <= 1024, Y, Z <= 2048, N < 2^31)";
@@ -488,8 +485,29 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             return CTWS_EUNSUPPORTED;
         }
     }
+    // flood tile grids: the largest (wide kernel) bounds the per-tile arrays
+    auto set_tiles = [&](bool packed) {
+        const int TZ = pl.nd_ws == 3 ? (packed ? 16 : 4) : (packed ? 4 : 1);
+        const int TY = pl.nd_ws == 3 ? (packed ? 16 : 8) : 32;
+        const int TX = packed ? (pl.nd_ws == 3 ? 16 : 32) : 64;
+        TT = 0;
+        max_tiles = 0;
+        for (auto& d : desc) {
+            d.tz = (d.Z + TZ - 1) / TZ;
+            d.ty = (d.Y + TY - 1) / TY;
+            d.tx = (d.X + TX - 1) / TX;
+            d.tbase = (int)TT;
+            TT += (int64_t)d.tz * d.ty * d.tx;
+            max_tiles = std::max(max_tiles, d.tz * d.ty * d.tx);
+        }
+    };
+    set_tiles(true);
+    const int64_t TT_packed = TT;
+    set_tiles(false);
+    const int64_t TT_wide = TT;
+    set_tiles(true);
     int r;
-    if ((r = ensure_workspace(h, T, TW, TC, TS, TT, nb)) != CTWS_OK) return r;
+    if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb)) != CTWS_OK) return r;
     HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
     h->last_desc = desc;
     std::vector<BlockStat> st(nb);
@@ -593,7 +611,21 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     k_bitmap<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.csum);
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
-    k_seed_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.hm, w.lab, w.key);
+    // packed flood keys need labels < 2^20 in every block of the batch
+    bool packed = true;
+    {
+        std::vector<BlockStat> s2(nb);
+        HIPCHK(hipMemcpyAsync(s2.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        for (auto& s : s2)
+            if (s.n_seeds >= (1u << 20) - 1u) packed = false;
+        if (!packed) {
+            set_tiles(false);
+            HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
+            h->last_desc = desc;
+        }
+    }
+    k_seed_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.hm, w.lab, w.key, packed ? 1 : 0);
     {
         dim3 gs((unsigned)((maxZ + 255) / 256), nb);
         k_slice_seed_base<<<gs, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
@@ -608,7 +640,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     // ---- flood ------------------------------------------------------------------------------
     int rounds1 = 0, rounds2 = 0;
     float fk1 = 0.f, fk2 = 0.f;
-    if ((r = run_flood(h, pl.nd_ws, nb, max_tiles, TT, w.hm, &rounds1, &fk1)) != CTWS_OK) return r;
+    if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, &rounds1, &fk1)) != CTWS_OK) return r;
+    if (packed) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     mark("flood");
     if (h->stop_after == CTWS_STOP_FLOOD) {
         HIPCHK(hipStreamSynchronize(h->stream));
@@ -622,9 +655,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 1024), nb);
         k_hist<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, counts);
         FilterParams fp{(uint32_t)cfg->size_filter};
-        k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, nullptr, w.hm, w.lab, w.key, w.surv);
+        k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, nullptr, w.hm, w.lab, w.key, w.surv,
+                                                 packed ? 1 : 0);
         LAUNCHCHK();
-        if ((r = run_flood(h, pl.nd_ws, nb, max_tiles, TT, w.hm, &rounds2, &fk2)) != CTWS_OK) return r;
+        if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, &rounds2, &fk2)) != CTWS_OK) return r;
+        if (packed) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     }
     mark("size_filter");
 
@@ -674,6 +709,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     h->timings.push_back({"flood_rounds", (float)rounds1});
     h->timings.push_back({"regrow_rounds", (float)rounds2});
     h->timings.push_back({"flood_kernel_ms", fk1});
+    h->timings.push_back({"flood_packed", packed ? 1.f : 0.f});
     h->timings.push_back({"size_filter_kernel_ms", fk2});
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : CTWS_BLOCK_EMPTY;

@@ -61,7 +61,7 @@ __global__ void k_bitmap(const BlockDesc*, const BlockStat*, int, const uint32_t
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
 __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uint64_t*, const uint32_t*, uint32_t*);
 __global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
-                             const float*, uint32_t*, uint64_t*);
+                             const float*, uint32_t*, uint64_t*, int);
 __global__ void k_crop_init(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_crop_union(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*, const uint64_t*,
@@ -72,12 +72,17 @@ template <int ND>
 __global__ void k_flood(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint32_t*, const uint8_t*,
                         uint8_t*, uint32_t*);
 
+template <int ND>
+__global__ void k_flood_packed(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint32_t*,
+                               const uint8_t*, uint8_t*, uint32_t*);
+__global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
+
 // k_post.hip
 __global__ void k_slice_seed_base(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
 __global__ void k_hist_zero(const BlockDesc*, const BlockStat*, uint32_t*);
 __global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_size_filter(const BlockDesc*, const BlockStat*, FilterParams, const uint32_t*, const uint8_t*,
-                              const float*, uint32_t*, uint64_t*, uint32_t*);
+                              const float*, uint32_t*, uint64_t*, uint32_t*, int);
 __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint32_t*);
 __global__ void k_slice_offsets(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint32_t*);

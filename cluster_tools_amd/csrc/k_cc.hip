@@ -274,7 +274,8 @@ __global__ void __launch_bounds__(256) k_word_prefix(const BlockDesc* __restrict
 __global__ void __launch_bounds__(256) k_seed_label(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                     const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ Wg,
                                                     const uint32_t* __restrict__ Wpg, const float* __restrict__ h,
-                                                    uint32_t* __restrict__ lab, uint64_t* __restrict__ key) {
+                                                    uint32_t* __restrict__ lab, uint64_t* __restrict__ key,
+                                                    int packed) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int Y = B.Y, X = B.X, Z = B.Z;
@@ -291,8 +292,9 @@ __global__ void __launch_bounds__(256) k_seed_label(const BlockDesc* __restrict_
         uint64_t k = kInfKey;
         if (PF[f] != kNoParent) {
             const uint32_t r = uf_find(PF, f);
-            l = (bitmap_rank(W, Wp, r) + 1u) | kFixedBit;
-            k = (uint64_t)ordf(h[B.base + i]) << 32;
+            const uint32_t lr = bitmap_rank(W, Wp, r) + 1u;
+            l = lr | kFixedBit;
+            k = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)lr : 0ull);
         }
         lab[B.base + i] = l;
         key[B.base + i] = k;

@@ -21,6 +21,8 @@
 // tiles for the next round; rounds repeat until no tile is active.
 //
 // Keys are uint64 (ordf(C) << 32 | d); labels carry kFixedBit for seeds.
+#include <type_traits>
+
 #include "ctws_kernels.h"
 
 namespace ctws {
@@ -202,5 +204,222 @@ template __global__ void k_flood<3>(const BlockDesc*, const BlockStat*, const fl
                                     const uint8_t*, uint8_t*, uint32_t*);
 template __global__ void k_flood<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint32_t*,
                                     const uint8_t*, uint8_t*, uint32_t*);
+
+}  // namespace ctws
+
+namespace ctws {
+
+// =========================================================================================
+// Packed flood: one uint64 per voxel, key = C (32) | d (12, saturating) | label (20), so the
+// min over neighbours of the packed word IS the (C, d, label) order.  Used when every block of
+// the batch has fewer than 2^20 seeds (the wide kernel above handles the rest).
+//
+// Tile: 16^3 (3-D) or 4 slices x 32 x 32 (2-D, no coupling between slices), 1-voxel halo in
+// LDS.  Each local iteration sweeps every axis: a thread owns one line along the axis and
+// relaxes it forward then backward in place (a change travels the whole line in one sweep),
+// then all threads switch to lines along the next axis.  LDS words are 64-bit and written
+// whole, so concurrent readers never see a torn key.
+// =========================================================================================
+constexpr uint64_t kPackInf = ~0ull;
+constexpr uint32_t kLabelBits = 20;
+constexpr uint64_t kLabelMask = (1ull << kLabelBits) - 1ull;
+constexpr uint64_t kDOne = 1ull << kLabelBits;
+constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
+
+__device__ __forceinline__ uint64_t f_packed(uint32_t hb, uint64_t best) {
+    const uint32_t c = (uint32_t)(best >> 32);
+    if (hb > c) return ((uint64_t)hb << 32) | (best & kLabelMask);
+    return ((best & kDMask) == kDMask) ? best : best + kDOne;
+}
+
+template <int ND>
+struct PTile;
+template <>
+struct PTile<3> {
+    static constexpr int TZ = 16, TY = 16, TX = 16, THREADS = 256;
+    static constexpr int HZ = TZ + 2, HY = TY + 2, HX = TX + 3;  // x padded (odd row length)
+};
+template <>
+struct PTile<2> {
+    static constexpr int TZ = 4, TY = 32, TX = 32, THREADS = 128;
+    static constexpr int HZ = TZ, HY = TY + 2, HX = TX + 3;
+};
+
+template <int ND>
+__global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const BlockDesc* __restrict__ D,
+                                                                     const BlockStat* S, const float* __restrict__ h,
+                                                                     uint64_t* __restrict__ key,
+                                                                     const uint32_t* __restrict__ lab,
+                                                                     const uint8_t* __restrict__ act_cur,
+                                                                     uint8_t* __restrict__ act_next,
+                                                                     uint32_t* __restrict__ counter) {
+    using T = PTile<ND>;
+    constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, NT = T::THREADS;
+    constexpr int HZ = T::HZ, HY = T::HY, HX = T::HX;
+    constexpr int HN = HZ * HY * HX;
+    constexpr int TN = TZ * TY * TX;
+    constexpr int ZOFF = (ND == 3) ? 1 : 0;
+    __shared__ uint64_t sk[HN];
+    __shared__ uint32_t sh[TN];
+    __shared__ uint8_t sf[TN];  // bit0: fixed (seed), bit1: changed, bit2: outside the block
+    __shared__ int sface[6];
+
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int t = blockIdx.x;
+    if (t >= B.tz * B.ty * B.tx) return;
+    if (!act_cur[B.tbase + t]) return;
+    const int txi = t % B.tx, tyi = (t / B.tx) % B.ty, tzi = t / (B.tx * B.ty);
+    const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const int64_t gb = B.base;
+    const int tid = threadIdx.x;
+
+    if (tid < 6) sface[tid] = 0;
+    int any_key = 0;
+    for (int c = tid; c < HN; c += NT) {
+        const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
+        const int gz = z0 + hz - ZOFF, gy = y0 + hy - 1, gx = x0 + hx - 1;
+        uint64_t k = kPackInf;
+        if (hx <= TX + 1 && gz >= 0 && gz < B.Z && gy >= 0 && gy < B.Y && gx >= 0 && gx < B.X)
+            k = key[gb + gz * YX + (int64_t)gy * B.X + gx];
+        sk[c] = k;
+        any_key |= k != kPackInf;
+    }
+    for (int c = tid; c < TN; c += NT) {
+        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+        const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
+        uint8_t f = 4;
+        uint32_t hb = 0;
+        if (gz < B.Z && gy < B.Y && gx < B.X) {
+            const int64_t gi = gb + gz * YX + (int64_t)gy * B.X + gx;
+            hb = ordf(h[gi]);
+            f = (lab[gi] & kFixedBit) ? 1 : 0;
+        }
+        sh[c] = hb;
+        sf[c] = f;
+    }
+    __syncthreads();
+
+    // nothing reached in the tile or its halo yet: nothing can change
+    if (!__syncthreads_or(any_key)) return;
+
+    // One sweep along `axis`: the thread's line lives in registers; the off-axis neighbour
+    // minimum is read once per voxel (independent LDS loads, issued together), then the line
+    // is relaxed forward and backward with the in-line neighbours taken from registers.
+    auto sweep = [&](auto axis_c, int a, int b2, bool& ch) {
+        constexpr int axis = decltype(axis_c)::value;
+        constexpr int len = axis == 0 ? TX : (axis == 1 ? TY : TZ);
+        constexpr int cstride = axis == 0 ? 1 : (axis == 1 ? HX : HX * HY);
+        constexpr int tstride = axis == 0 ? 1 : (axis == 1 ? TX : TX * TY);
+        constexpr int o1 = axis == 0 ? HX : 1;          // off-axis neighbour strides
+        constexpr int o2 = axis == 2 ? HX : HX * HY;
+        int lz = 0, ly = 0, lx = 0;
+        if (axis == 0) { lz = a; ly = b2; }
+        else if (axis == 1) { lz = a; lx = b2; }
+        else { ly = a; lx = b2; }
+        const int c0 = ((lz + ZOFF) * HY + (ly + 1)) * HX + (lx + 1);
+        const int t0 = (lz * TY + ly) * TX + lx;
+        uint64_t v[len], off[len];
+        uint32_t hb[len];
+        uint32_t upd = 0;
+#pragma unroll
+        for (int p = 0; p < len; ++p) {
+            const int c = c0 + p * cstride;
+            v[p] = sk[c];
+            uint64_t m = min(sk[c - o1], sk[c + o1]);
+            if (ND == 3) m = min(m, min(sk[c - o2], sk[c + o2]));
+            off[p] = m;
+            hb[p] = sh[t0 + p * tstride];
+            if (!(sf[t0 + p * tstride] & 5)) upd |= 1u << p;
+        }
+        const uint64_t before_lo = sk[c0 - cstride];
+        const uint64_t after_hi = sk[c0 + len * cstride];
+        uint32_t chg = 0;
+        auto step = [&](int p) {
+            if (!(upd & (1u << p))) return;
+            uint64_t b = min(off[p], p > 0 ? v[p - 1] : before_lo);
+            b = min(b, p + 1 < len ? v[p + 1] : after_hi);
+            if (b == kPackInf) return;
+            const uint64_t nk = f_packed(hb[p], b);
+            if (nk != v[p]) {
+                v[p] = nk;
+                chg |= 1u << p;
+            }
+        };
+#pragma unroll
+        for (int p = 0; p < len; ++p) step(p);
+#pragma unroll
+        for (int p = len - 1; p >= 0; --p) step(p);
+        if (chg) {
+            ch = true;
+#pragma unroll
+            for (int p = 0; p < len; ++p)
+                if (chg & (1u << p)) {
+                    sk[c0 + p * cstride] = v[p];
+                    sf[t0 + p * tstride] |= 2;
+                }
+        }
+    };
+
+    for (int it = 0; it < 1024; ++it) {
+        bool ch = false;
+        sweep(std::integral_constant<int, 0>(), tid / TY, tid % TY, ch);  // x lines: thread -> (z, y)
+        __syncthreads();
+        sweep(std::integral_constant<int, 1>(), tid / TX, tid % TX, ch);  // y lines: (z, x)
+        __syncthreads();
+        if constexpr (ND == 3) sweep(std::integral_constant<int, 2>(), tid / TX, tid % TX, ch);  // z: (y, x)
+        if (!__syncthreads_or(ch)) break;
+    }
+
+    // write back changed voxels; activate face neighbours
+    for (int c = tid; c < TN; c += NT) {
+        if (!(sf[c] & 2)) continue;
+        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+        const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
+        key[gb + gz * YX + (int64_t)gy * B.X + gx] = sk[((lz + ZOFF) * HY + (ly + 1)) * HX + (lx + 1)];
+        if (ND == 3) {
+            if (lz == 0) sface[0] = 1;
+            if (lz == TZ - 1) sface[1] = 1;
+        }
+        if (ly == 0) sface[2] = 1;
+        if (ly == TY - 1) sface[3] = 1;
+        if (lx == 0) sface[4] = 1;
+        if (lx == TX - 1) sface[5] = 1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int n = 0;
+        auto act = [&](int zz, int yy, int xx) {
+            if (zz < 0 || zz >= B.tz || yy < 0 || yy >= B.ty || xx < 0 || xx >= B.tx) return;
+            act_next[B.tbase + (zz * B.ty + yy) * B.tx + xx] = 1;
+            ++n;
+        };
+        if (sface[0]) act(tzi - 1, tyi, txi);
+        if (sface[1]) act(tzi + 1, tyi, txi);
+        if (sface[2]) act(tzi, tyi - 1, txi);
+        if (sface[3]) act(tzi, tyi + 1, txi);
+        if (sface[4]) act(tzi, tyi, txi - 1);
+        if (sface[5]) act(tzi, tyi, txi + 1);
+        if (n) atomicAdd(counter, (uint32_t)n);
+    }
+}
+
+template __global__ void k_flood_packed<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                           const uint32_t*, const uint8_t*, uint8_t*, uint32_t*);
+template __global__ void k_flood_packed<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                           const uint32_t*, const uint8_t*, uint8_t*, uint32_t*);
+
+// packed keys -> labels (keeps the seed bit of `lab`)
+__global__ void __launch_bounds__(256) k_unpack_labels(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                       const uint64_t* __restrict__ key, uint32_t* __restrict__ lab) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = key[B.base + i];
+        const uint32_t l = (k == kPackInf) ? 0u : (uint32_t)(k & kLabelMask);
+        lab[B.base + i] = (lab[B.base + i] & kFixedBit) | l;
+    }
+}
 
 }  // namespace ctws

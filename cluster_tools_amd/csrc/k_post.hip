@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
                                                      FilterParams fp, const uint32_t* __restrict__ counts,
                                                      const uint8_t* __restrict__ excl, const float* __restrict__ h,
                                                      uint32_t* __restrict__ lab, uint64_t* __restrict__ key,
-                                                     uint32_t* __restrict__ survivors) {
+                                                     uint32_t* __restrict__ survivors, int packed) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
         bool keep = l != 0 && (counts[B.base + l] >= fp.size_filter || (excl && excl[B.base + l]));
         if (keep) {
             lab[B.base + i] = l | kFixedBit;
-            key[B.base + i] = (uint64_t)ordf(h[B.base + i]) << 32;
+            key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
             const int z = (B.nd_ws == 2) ? (int)(i / YX) : 0;
             if (!survivors[B.sbase + z]) survivors[B.sbase + z] = 1;
         } else {

@@ -482,7 +482,9 @@ uint32_t watersheds_model(const float* h, const Dims& d, uint32_t* labels) {
                 labels[j] = e.label;
                 const uint32_t hb = ordf(h[j]);
                 const uint32_t cc = (uint32_t)(e.key >> 32);
-                const uint64_t k = hb > cc ? ((uint64_t)hb << 32) : e.key + 1ull;
+                // d saturates at 4095 (12-bit field of the GPU's packed key)
+                const uint64_t k = hb > cc ? ((uint64_t)hb << 32)
+                                           : ((e.key & 0xFFFFFFFFull) >= 4095ull ? e.key : e.key + 1ull);
                 pq.push({k, e.label, j});
             }
         }
