@@ -69,6 +69,7 @@ struct ctws_handle {
     std::vector<std::pair<const char*, float>> timings;
     std::vector<hipEvent_t> events;
     hipEvent_t fev[2] = {nullptr, nullptr};
+    uint64_t flood_tiles = 0, flood_iters = 0;
     // host-pointer staging
     DevBuf st_in, st_mask, st_init, st_out;
     // test hooks
@@ -345,6 +346,7 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
         hipEventCreate(&h->fev[1]);
     }
     float kms = 0.f;
+    uint32_t tiles_solved = 0, local_iters = 0;
     HIPCHK(hipMemsetAsync(w.act0, 1, (size_t)ntiles, h->stream));
     HIPCHK(hipMemsetAsync(w.act1, 0, (size_t)ntiles, h->stream));
     uint8_t* cur = w.act0;
@@ -352,7 +354,7 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
     dim3 g((unsigned)max_tiles, nb);
     int round = 0;
     for (; round < 1000000; ++round) {
-        HIPCHK(hipMemsetAsync(w.counter, 0, 4, h->stream));
+        HIPCHK(hipMemsetAsync(w.counter, 0, 12, h->stream));
         hipEventRecord(h->fev[0], h->stream);
         if (packed && nd == 3)
             k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
@@ -364,17 +366,21 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
             k_flood<2><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         LAUNCHCHK();
         hipEventRecord(h->fev[1], h->stream);
-        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 12, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
         float ms = 0.f;
         hipEventElapsedTime(&ms, h->fev[0], h->fev[1]);
         kms += ms;
+        tiles_solved += h->h_counter[1];
+        local_iters += h->h_counter[2];
         if (*h->h_counter == 0) break;
         HIPCHK(hipMemsetAsync(cur, 0, (size_t)ntiles, h->stream));
         std::swap(cur, nxt);
     }
     if (rounds_out) *rounds_out = round + 1;
     if (kernel_ms) *kernel_ms = kms;
+    h->flood_tiles += tiles_solved;
+    h->flood_iters += local_iters;
     return CTWS_OK;
 }
 
@@ -639,6 +645,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- flood ------------------------------------------------------------------------------
     int rounds1 = 0, rounds2 = 0;
+    h->flood_tiles = h->flood_iters = 0;
     float fk1 = 0.f, fk2 = 0.f;
     if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, &rounds1, &fk1)) != CTWS_OK) return r;
     if (packed) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
@@ -710,6 +717,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     h->timings.push_back({"regrow_rounds", (float)rounds2});
     h->timings.push_back({"flood_kernel_ms", fk1});
     h->timings.push_back({"flood_packed", packed ? 1.f : 0.f});
+    h->timings.push_back({"flood_tiles_solved", (float)h->flood_tiles});
+    h->timings.push_back({"flood_local_iters", (float)h->flood_iters});
     h->timings.push_back({"size_filter_kernel_ms", fk2});
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : CTWS_BLOCK_EMPTY;
@@ -864,7 +873,7 @@ int ctws_open(int device, ctws_handle** out) {
     ctws_handle* h = new ctws_handle();
     h->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_counter, 4, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_counter, 16, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * 128 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
         delete h;
         return CTWS_EHIP;

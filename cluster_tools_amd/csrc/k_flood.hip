@@ -336,16 +336,20 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
         const uint64_t before_lo = sk[c0 - cstride];
         const uint64_t after_hi = sk[c0 + len * cstride];
         uint32_t chg = 0;
+        // branch-free relaxation step: new C = max(h, C), d reset or incremented (saturating),
+        // label kept; f(INF) == INF, fixed / outside voxels keep their value
         auto step = [&](int p) {
-            if (!(upd & (1u << p))) return;
             uint64_t b = min(off[p], p > 0 ? v[p - 1] : before_lo);
             b = min(b, p + 1 < len ? v[p + 1] : after_hi);
-            if (b == kPackInf) return;
-            const uint64_t nk = f_packed(hb[p], b);
-            if (nk != v[p]) {
-                v[p] = nk;
-                chg |= 1u << p;
-            }
+            const uint32_t bh = (uint32_t)(b >> 32), bl = (uint32_t)b;
+            const bool above = hb[p] > bh;
+            const uint32_t nh = above ? hb[p] : bh;
+            const uint32_t sat = ((bl & 0xFFF00000u) == 0xFFF00000u) ? 0u : (1u << kLabelBits);
+            const uint32_t nl = above ? (bl & (uint32_t)kLabelMask) : bl + sat;
+            uint64_t nk = ((uint64_t)nh << 32) | nl;
+            nk = (upd & (1u << p)) ? nk : v[p];
+            chg |= (nk != v[p]) ? (1u << p) : 0u;
+            v[p] = nk;
         };
 #pragma unroll
         for (int p = 0; p < len; ++p) step(p);
@@ -362,14 +366,19 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
         }
     };
 
-    for (int it = 0; it < 1024; ++it) {
+    // Sweep x, y, z, x, ... until the tile is at its fixpoint: every axis swept at least once
+    // and the last ND - 1 sweeps changed nothing (the sweep before them then sees unchanged
+    // inputs again, so it would be a no-op too).
+    int iters = 0, since = 0;
+    for (int k = 0; k < 3 * 1024; ++k) {
         bool ch = false;
-        sweep(std::integral_constant<int, 0>(), tid / TY, tid % TY, ch);  // x lines: thread -> (z, y)
-        __syncthreads();
-        sweep(std::integral_constant<int, 1>(), tid / TX, tid % TX, ch);  // y lines: (z, x)
-        __syncthreads();
-        if constexpr (ND == 3) sweep(std::integral_constant<int, 2>(), tid / TX, tid % TX, ch);  // z: (y, x)
-        if (!__syncthreads_or(ch)) break;
+        const int axis = k % ND;
+        if (axis == 0) sweep(std::integral_constant<int, 0>(), tid / TY, tid % TY, ch);      // lines (z, y)
+        else if (axis == 1) sweep(std::integral_constant<int, 1>(), tid / TX, tid % TX, ch);  // (z, x)
+        else if constexpr (ND == 3) sweep(std::integral_constant<int, 2>(), tid / TX, tid % TX, ch);  // (y, x)
+        ++iters;
+        since = __syncthreads_or(ch) ? 0 : since + 1;
+        if (k + 1 >= ND && since >= ND - 1) break;
     }
 
     // write back changed voxels; activate face neighbours
@@ -402,6 +411,8 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
         if (sface[4]) act(tzi, tyi, txi - 1);
         if (sface[5]) act(tzi, tyi, txi + 1);
         if (n) atomicAdd(counter, (uint32_t)n);
+        atomicAdd(counter + 1, 1u);              // tiles solved
+        atomicAdd(counter + 2, (uint32_t)iters);  // local iterations
     }
 }
 
