@@ -48,7 +48,7 @@ struct Workspace {
     uint64_t* W = nullptr;
     uint32_t *Wp = nullptr, *csum = nullptr;
     uint32_t *smin = nullptr, *smax = nullptr, *sb = nullptr, *slmax = nullptr, *soff = nullptr, *surv = nullptr;
-    uint8_t *act0 = nullptr, *act1 = nullptr;
+    uint32_t *act0 = nullptr, *act1 = nullptr, *lines0 = nullptr, *lines1 = nullptr;
     BlockDesc* desc = nullptr;
     BlockStat* stat = nullptr;
     uint32_t* counter = nullptr;
@@ -69,7 +69,7 @@ struct ctws_handle {
     std::vector<std::pair<const char*, float>> timings;
     std::vector<hipEvent_t> events;
     hipEvent_t fev[2] = {nullptr, nullptr};
-    uint64_t flood_tiles = 0, flood_iters = 0;
+    uint64_t flood_tiles = 0, flood_iters = 0, flood_lines = 0;
     // host-pointer staging
     DevBuf st_in, st_mask, st_init, st_out;
     // test hooks
@@ -171,6 +171,8 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
     if (tiles > w.cap_tiles) {
         ALLOC(act0, tiles);
         ALLOC(act1, tiles);
+        ALLOC(lines0, tiles * kLineWords);
+        ALLOC(lines1, tiles * kLineWords);
         w.cap_tiles = tiles;
     }
     if (blocks > w.cap_blocks) {
@@ -338,8 +340,16 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
 }
 
 // ---- flood rounds until no tile is active -----------------------------------------------
+// tile extents of k_flood_packed (PTile) and k_flood (FloodTile)
+void flood_tile_dims(int nd, bool packed, int* tz, int* ty, int* tx) {
+    *tz = nd == 3 ? (packed ? 16 : 4) : (packed ? 4 : 1);
+    *ty = nd == 3 ? (packed ? 16 : 8) : 32;
+    *tx = packed ? (nd == 3 ? 16 : 32) : 64;
+}
+
+// preset: act0 already holds the tiles to solve in the first round (regrow); otherwise all.
 int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_t ntiles, const float* hm,
-              int* rounds_out, float* kernel_ms) {
+              bool preset, int* rounds_out, float* kernel_ms) {
     Workspace& w = h->ws;
     if (!h->fev[0]) {
         hipEventCreate(&h->fev[0]);
@@ -347,35 +357,43 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
     }
     float kms = 0.f;
     uint32_t tiles_solved = 0, local_iters = 0;
-    HIPCHK(hipMemsetAsync(w.act0, 1, (size_t)ntiles, h->stream));
-    HIPCHK(hipMemsetAsync(w.act1, 0, (size_t)ntiles, h->stream));
-    uint8_t* cur = w.act0;
-    uint8_t* nxt = w.act1;
+    if (!preset) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w.act0, 8u, (size_t)ntiles, h->stream));  // full solve
+    HIPCHK(hipMemsetAsync(w.act1, 0, sizeof(uint32_t) * (size_t)ntiles, h->stream));
+    HIPCHK(hipMemsetAsync(w.lines0, 0, sizeof(uint32_t) * kLineWords * (size_t)ntiles, h->stream));
+    HIPCHK(hipMemsetAsync(w.lines1, 0, sizeof(uint32_t) * kLineWords * (size_t)ntiles, h->stream));
+    uint32_t* cur = w.act0;
+    uint32_t* nxt = w.act1;
+    uint32_t* lcur = w.lines0;  // consumed (and cleared) by the packed kernel
+    uint32_t* lnxt = w.lines1;
     dim3 g((unsigned)max_tiles, nb);
     int round = 0;
     for (; round < 1000000; ++round) {
-        HIPCHK(hipMemsetAsync(w.counter, 0, 12, h->stream));
+        HIPCHK(hipMemsetAsync(w.counter, 0, 16, h->stream));
         hipEventRecord(h->fev[0], h->stream);
         if (packed && nd == 3)
-            k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
+            k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.cls, cur, nxt, lcur, lnxt,
+                                                        w.counter);
         else if (packed)
-            k_flood_packed<2><<<g, 128, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
+            k_flood_packed<2><<<g, 128, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.cls, cur, nxt, lcur, lnxt,
+                                                        w.counter);
         else if (nd == 3)
             k_flood<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         else
             k_flood<2><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         LAUNCHCHK();
         hipEventRecord(h->fev[1], h->stream);
-        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 12, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 16, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
         float ms = 0.f;
         hipEventElapsedTime(&ms, h->fev[0], h->fev[1]);
         kms += ms;
         tiles_solved += h->h_counter[1];
         local_iters += h->h_counter[2];
+        h->flood_lines += h->h_counter[3];
         if (*h->h_counter == 0) break;
-        HIPCHK(hipMemsetAsync(cur, 0, (size_t)ntiles, h->stream));
+        HIPCHK(hipMemsetAsync(cur, 0, sizeof(uint32_t) * (size_t)ntiles, h->stream));
         std::swap(cur, nxt);
+        std::swap(lcur, lnxt);
     }
     if (rounds_out) *rounds_out = round + 1;
     if (kernel_ms) *kernel_ms = kms;
@@ -493,9 +511,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
     // flood tile grids: the largest (wide kernel) bounds the per-tile arrays
     auto set_tiles = [&](bool packed) {
-        const int TZ = pl.nd_ws == 3 ? (packed ? 16 : 4) : (packed ? 4 : 1);
-        const int TY = pl.nd_ws == 3 ? (packed ? 16 : 8) : 32;
-        const int TX = packed ? (pl.nd_ws == 3 ? 16 : 32) : 64;
+        int TZ, TY, TX;
+        flood_tile_dims(pl.nd_ws, packed, &TZ, &TY, &TX);
         TT = 0;
         max_tiles = 0;
         for (auto& d : desc) {
@@ -631,7 +648,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             h->last_desc = desc;
         }
     }
-    k_seed_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.hm, w.lab, w.key, packed ? 1 : 0);
+    k_seed_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
+                                            packed ? 1 : 0);
     {
         dim3 gs((unsigned)((maxZ + 255) / 256), nb);
         k_slice_seed_base<<<gs, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
@@ -645,9 +663,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- flood ------------------------------------------------------------------------------
     int rounds1 = 0, rounds2 = 0;
-    h->flood_tiles = h->flood_iters = 0;
+    h->flood_tiles = h->flood_iters = h->flood_lines = 0;
     float fk1 = 0.f, fk2 = 0.f;
-    if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, &rounds1, &fk1)) != CTWS_OK) return r;
+    if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK) return r;
     if (packed) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     mark("flood");
     if (h->stop_after == CTWS_STOP_FLOOD) {
@@ -661,11 +679,13 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
         dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 1024), nb);
         k_hist<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, counts);
-        FilterParams fp{(uint32_t)cfg->size_filter};
-        k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, nullptr, w.hm, w.lab, w.key, w.surv,
-                                                 packed ? 1 : 0);
+        FilterParams fp{(uint32_t)cfg->size_filter, 0, 0, 0, w.act0};
+        flood_tile_dims(pl.nd_ws, packed, &fp.tz, &fp.ty, &fp.tx);
+        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+        k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, nullptr, w.hm, w.lab, w.key, w.cls,
+                                                 w.surv, packed ? 1 : 0);
         LAUNCHCHK();
-        if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, &rounds2, &fk2)) != CTWS_OK) return r;
+        if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds2, &fk2)) != CTWS_OK) return r;
         if (packed) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     }
     mark("size_filter");
@@ -719,6 +739,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     h->timings.push_back({"flood_packed", packed ? 1.f : 0.f});
     h->timings.push_back({"flood_tiles_solved", (float)h->flood_tiles});
     h->timings.push_back({"flood_local_iters", (float)h->flood_iters});
+    h->timings.push_back({"flood_lines_swept", (float)h->flood_lines});
     h->timings.push_back({"size_filter_kernel_ms", fk2});
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : CTWS_BLOCK_EMPTY;
@@ -888,7 +909,7 @@ void ctws_close(ctws_handle* h) {
     hipStreamSynchronize(h->stream);
     Workspace& w = h->ws;
     void* ptrs[] = {w.fin, w.dt, w.A, w.Bf, w.sm, w.hm, w.cls, w.P, w.PF, w.lab, w.key, w.W, w.Wp, w.csum,
-                    w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.desc, w.stat, w.counter,
+                    w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.lines0, w.lines1, w.desc, w.stat, w.counter,
                     w.taps, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p};
     for (void* p : ptrs)
         if (p) hipFree(p);

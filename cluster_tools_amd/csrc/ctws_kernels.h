@@ -29,6 +29,8 @@ struct GaussParams {
 };
 struct FilterParams {
     uint32_t size_filter;
+    int tz, ty, tx;  // flood tile extents: tiles holding a freed voxel are activated in act
+    uint32_t* act;
 };
 
 // k_edt.hip
@@ -61,7 +63,7 @@ __global__ void k_bitmap(const BlockDesc*, const BlockStat*, int, const uint32_t
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
 __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uint64_t*, const uint32_t*, uint32_t*);
 __global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
-                             const float*, uint32_t*, uint64_t*, int);
+                             const float*, uint32_t*, uint64_t*, uint8_t*, int);
 __global__ void k_crop_init(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_crop_union(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*, const uint64_t*,
@@ -69,12 +71,13 @@ __global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const ui
 
 // k_flood.hip
 template <int ND>
-__global__ void k_flood(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint32_t*, const uint8_t*,
-                        uint8_t*, uint32_t*);
+__global__ void k_flood(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint32_t*, const uint32_t*,
+                        uint32_t*, uint32_t*);
 
 template <int ND>
-__global__ void k_flood_packed(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint32_t*,
-                               const uint8_t*, uint8_t*, uint32_t*);
+__global__ void k_flood_packed(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint8_t*,
+                               const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+constexpr int kLineWords = 24;  // per tile: 8 words of line bits for each of x, y, z
 __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
 
 // k_post.hip
@@ -82,7 +85,7 @@ __global__ void k_slice_seed_base(const BlockDesc*, const BlockStat*, const uint
 __global__ void k_hist_zero(const BlockDesc*, const BlockStat*, uint32_t*);
 __global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_size_filter(const BlockDesc*, const BlockStat*, FilterParams, const uint32_t*, const uint8_t*,
-                              const float*, uint32_t*, uint64_t*, uint32_t*, int);
+                              const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, int);
 __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint32_t*);
 __global__ void k_slice_offsets(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint32_t*);

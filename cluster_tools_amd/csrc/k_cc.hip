@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) k_seed_label(const BlockDesc* __restrict_
                                                     const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ Wg,
                                                     const uint32_t* __restrict__ Wpg, const float* __restrict__ h,
                                                     uint32_t* __restrict__ lab, uint64_t* __restrict__ key,
-                                                    int packed) {
+                                                    uint8_t* __restrict__ fixedv, int packed) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int Y = B.Y, X = B.X, Z = B.Z;
@@ -298,6 +298,7 @@ __global__ void __launch_bounds__(256) k_seed_label(const BlockDesc* __restrict_
         }
         lab[B.base + i] = l;
         key[B.base + i] = k;
+        fixedv[B.base + i] = l ? 1 : 0;
     }
 }
 

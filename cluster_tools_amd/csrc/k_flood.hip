@@ -54,8 +54,8 @@ __device__ __forceinline__ uint64_t f_key(uint32_t hb, uint64_t bk) {
 template <int ND>
 __global__ void __launch_bounds__(256) k_flood(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                const float* __restrict__ h, uint64_t* __restrict__ key,
-                                               uint32_t* __restrict__ lab, const uint8_t* __restrict__ act_cur,
-                                               uint8_t* __restrict__ act_next, uint32_t* __restrict__ counter) {
+                                               uint32_t* __restrict__ lab, const uint32_t* __restrict__ act_cur,
+                                               uint32_t* __restrict__ act_next, uint32_t* __restrict__ counter) {
     using T = FloodTile<ND>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX;
     constexpr int HZ = T::HZ, HY = TY + 2, HX = TX + 2;
@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(256) k_flood(const BlockDesc* __restrict__ D, 
         int n = 0;
         auto act = [&](int zz, int yy, int xx) {
             if (zz < 0 || zz >= B.tz || yy < 0 || yy >= B.ty || xx < 0 || xx >= B.tx) return;
-            act_next[B.tbase + (zz * B.ty + yy) * B.tx + xx] = 1;
+            atomicOr(&act_next[B.tbase + (zz * B.ty + yy) * B.tx + xx], 8u);
             ++n;
         };
         if (sface[0]) act(tzi - 1, tyi, txi);
@@ -201,9 +201,9 @@ __global__ void __launch_bounds__(256) k_flood(const BlockDesc* __restrict__ D, 
 }
 
 template __global__ void k_flood<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint32_t*,
-                                    const uint8_t*, uint8_t*, uint32_t*);
+                                    const uint32_t*, uint32_t*, uint32_t*);
 template __global__ void k_flood<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint32_t*,
-                                    const uint8_t*, uint8_t*, uint32_t*);
+                                    const uint32_t*, uint32_t*, uint32_t*);
 
 }  // namespace ctws
 
@@ -245,79 +245,126 @@ struct PTile<2> {
     static constexpr int HZ = TZ, HY = TY + 2, HX = TX + 3;
 };
 
+// act[] per tile: bit3 = solve the whole tile (first round), bit0 = halo voxels changed; the
+// lines through the changed halo voxels are in lines[tile * kLineWords]: 8 words per axis
+// (x-lines, y-lines, z-lines), one bit per line, indexed as the dirty bitmaps below.
+constexpr uint32_t kActFull = 8u;
+
 template <int ND>
 __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const BlockDesc* __restrict__ D,
-                                                                     const BlockStat* S, const float* __restrict__ h,
-                                                                     uint64_t* __restrict__ key,
-                                                                     const uint32_t* __restrict__ lab,
-                                                                     const uint8_t* __restrict__ act_cur,
-                                                                     uint8_t* __restrict__ act_next,
-                                                                     uint32_t* __restrict__ counter) {
+                                                                        const BlockStat* S,
+                                                                        const float* __restrict__ h,
+                                                                        uint64_t* __restrict__ key,
+                                                                        const uint8_t* __restrict__ fixedv,
+                                                                        const uint32_t* __restrict__ act_cur,
+                                                                        uint32_t* __restrict__ act_next,
+                                                                        uint32_t* __restrict__ lines_cur,
+                                                                        uint32_t* __restrict__ lines_next,
+                                                                        uint32_t* __restrict__ counter) {
     using T = PTile<ND>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, NT = T::THREADS;
     constexpr int HZ = T::HZ, HY = T::HY, HX = T::HX;
     constexpr int HN = HZ * HY * HX;
     constexpr int TN = TZ * TY * TX;
     constexpr int ZOFF = (ND == 3) ? 1 : 0;
+    constexpr int NW = NT / 32;  // dirty-bitmap words per axis (one bit per line, NT lines)
+    static_assert(TZ * TY == NT && TZ * TX == NT && (ND == 2 || TY * TX == NT), "one line per thread");
     __shared__ uint64_t sk[HN];
     __shared__ uint32_t sh[TN];
     __shared__ uint8_t sf[TN];  // bit0: fixed (seed), bit1: changed, bit2: outside the block
-    __shared__ int sface[6];
+    __shared__ uint32_t dirty[3][NW];
+    __shared__ uint32_t sfl[6][NW];  // lines of the face neighbours whose halo voxel changed
 
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int t = blockIdx.x;
     if (t >= B.tz * B.ty * B.tx) return;
-    if (!act_cur[B.tbase + t]) return;
+    const uint32_t am = act_cur[B.tbase + t];
+    if (!am) return;
     const int txi = t % B.tx, tyi = (t / B.tx) % B.ty, tzi = t / (B.tx * B.ty);
     const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
     const int64_t YX = (int64_t)B.Y * B.X;
     const int64_t gb = B.base;
     const int tid = threadIdx.x;
 
-    if (tid < 6) sface[tid] = 0;
-    int any_key = 0;
-    for (int c = tid; c < HN; c += NT) {
+    if (tid < 6 * NW) sfl[tid / NW][tid % NW] = 0;
+    if (tid < kLineWords) {
+        uint32_t* lin = lines_cur + (int64_t)(B.tbase + t) * kLineWords;
+        const uint32_t v = lin[tid];
+        lin[tid] = 0;  // consumed: the array is next round's lines_next
+        if ((tid & 7) < NW) dirty[tid >> 3][tid & 7] = (am & kActFull) ? 0xFFFFFFFFu : v;
+    }
+    // All global loads of a phase are issued before the first LDS store so that their
+    // latencies overlap (a load/store loop serialises them at this occupancy).
+    // Phase 1: keys of the tile and its halo.
+    constexpr int NLK = (HN + NT - 1) / NT;
+    uint64_t kk[NLK];
+#pragma unroll
+    for (int i = 0; i < NLK; ++i) {
+        const int c = tid + i * NT;
         const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
         const int gz = z0 + hz - ZOFF, gy = y0 + hy - 1, gx = x0 + hx - 1;
-        uint64_t k = kPackInf;
-        if (hx <= TX + 1 && gz >= 0 && gz < B.Z && gy >= 0 && gy < B.Y && gx >= 0 && gx < B.X)
-            k = key[gb + gz * YX + (int64_t)gy * B.X + gx];
-        sk[c] = k;
-        any_key |= k != kPackInf;
+        kk[i] = kPackInf;
+        if (c < HN && hx <= TX + 1 && gz >= 0 && gz < B.Z && gy >= 0 && gy < B.Y && gx >= 0 && gx < B.X)
+            kk[i] = key[gb + gz * YX + (int64_t)gy * B.X + gx];
     }
-    for (int c = tid; c < TN; c += NT) {
+    int any_key = 0;
+#pragma unroll
+    for (int i = 0; i < NLK; ++i) {
+        const int c = tid + i * NT;
+        if (c < HN) sk[c] = kk[i];
+        any_key |= kk[i] != kPackInf;
+    }
+    // nothing reached in the tile or its halo yet: nothing can change
+    if (!__syncthreads_or(any_key)) return;
+    // Phase 2: heights and seed flags.
+    constexpr int NLT = TN / NT;
+    static_assert(TN % NT == 0, "");
+    float hv[NLT];
+    uint8_t fv[NLT];
+#pragma unroll
+    for (int i = 0; i < NLT; ++i) {
+        const int c = tid + i * NT;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
-        uint8_t f = 4;
-        uint32_t hb = 0;
+        fv[i] = 4;
+        hv[i] = 0.f;
         if (gz < B.Z && gy < B.Y && gx < B.X) {
             const int64_t gi = gb + gz * YX + (int64_t)gy * B.X + gx;
-            hb = ordf(h[gi]);
-            f = (lab[gi] & kFixedBit) ? 1 : 0;
+            hv[i] = h[gi];
+            fv[i] = fixedv[gi] ? 1 : 0;
         }
-        sh[c] = hb;
-        sf[c] = f;
+    }
+#pragma unroll
+    for (int i = 0; i < NLT; ++i) {
+        sh[tid + i * NT] = fv[i] == 4 ? 0u : ordf(hv[i]);
+        sf[tid + i * NT] = fv[i];
     }
     __syncthreads();
 
-    // nothing reached in the tile or its halo yet: nothing can change
-    if (!__syncthreads_or(any_key)) return;
+    // Line indices: x-lines (z, y) -> z*TY + y; y-lines (z, x) -> z*TX + x; z-lines (y, x) ->
+    // y*TX + x.  A thread owns line `tid` of the axis being swept.
+    auto mark = [&](int ax, int line) { atomicOr(&dirty[ax][line >> 5], 1u << (line & 31)); };
+    uint32_t nlines = 0;
 
-    // One sweep along `axis`: the thread's line lives in registers; the off-axis neighbour
-    // minimum is read once per voxel (independent LDS loads, issued together), then the line
-    // is relaxed forward and backward with the in-line neighbours taken from registers.
-    auto sweep = [&](auto axis_c, int a, int b2, bool& ch) {
+    // One sweep of the thread's line along `axis` (if dirty): the line lives in registers;
+    // the off-axis neighbour minimum is read once per voxel, then the line is relaxed forward
+    // and backward.  Changed voxels dirty the lines of the other axes through them.
+    auto sweep = [&](auto axis_c, bool& ch) {
         constexpr int axis = decltype(axis_c)::value;
         constexpr int len = axis == 0 ? TX : (axis == 1 ? TY : TZ);
         constexpr int cstride = axis == 0 ? 1 : (axis == 1 ? HX : HX * HY);
         constexpr int tstride = axis == 0 ? 1 : (axis == 1 ? TX : TX * TY);
         constexpr int o1 = axis == 0 ? HX : 1;          // off-axis neighbour strides
         constexpr int o2 = axis == 2 ? HX : HX * HY;
+        const uint32_t bit = 1u << (tid & 31);
+        const uint32_t old = atomicAnd(&dirty[axis][tid >> 5], ~bit);
+        if (!(old & bit)) return;
+        ++nlines;
         int lz = 0, ly = 0, lx = 0;
-        if (axis == 0) { lz = a; ly = b2; }
-        else if (axis == 1) { lz = a; lx = b2; }
-        else { ly = a; lx = b2; }
+        if (axis == 0) { lz = tid / TY; ly = tid % TY; }
+        else if (axis == 1) { lz = tid / TX; lx = tid % TX; }
+        else { ly = tid / TX; lx = tid % TX; }
         const int c0 = ((lz + ZOFF) * HY + (ly + 1)) * HX + (lx + 1);
         const int t0 = (lz * TY + ly) * TX + lx;
         uint64_t v[len], off[len];
@@ -336,16 +383,19 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
         const uint64_t before_lo = sk[c0 - cstride];
         const uint64_t after_hi = sk[c0 + len * cstride];
         uint32_t chg = 0;
-        // branch-free relaxation step: new C = max(h, C), d reset or incremented (saturating),
-        // label kept; f(INF) == INF, fixed / outside voxels keep their value
+        // Branch-free relaxation K(p) = f(min over the 6 neighbours): new C = max(h, C); d
+        // reset or incremented (saturating); label of the argmin neighbour.  f(INF) = INF;
+        // seeds and voxels outside the block keep their key.  (The label makes f
+        // non-monotone, so this is a replacement, not a min with the old key.)
         auto step = [&](int p) {
             uint64_t b = min(off[p], p > 0 ? v[p - 1] : before_lo);
             b = min(b, p + 1 < len ? v[p + 1] : after_hi);
             const uint32_t bh = (uint32_t)(b >> 32), bl = (uint32_t)b;
             const bool above = hb[p] > bh;
-            const uint32_t nh = above ? hb[p] : bh;
-            const uint32_t sat = ((bl & 0xFFF00000u) == 0xFFF00000u) ? 0u : (1u << kLabelBits);
-            const uint32_t nl = above ? (bl & (uint32_t)kLabelMask) : bl + sat;
+            const uint32_t nh = max(hb[p], bh);
+            uint32_t inc;
+            const bool ovf = __builtin_add_overflow(bl, 1u << kLabelBits, &inc);
+            const uint32_t nl = above ? (bl & (uint32_t)kLabelMask) : (ovf ? bl : inc);
             uint64_t nk = ((uint64_t)nh << 32) | nl;
             nk = (upd & (1u << p)) ? nk : v[p];
             chg |= (nk != v[p]) ? (1u << p) : 0u;
@@ -355,71 +405,113 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
         for (int p = 0; p < len; ++p) step(p);
 #pragma unroll
         for (int p = len - 1; p >= 0; --p) step(p);
-        if (chg) {
-            ch = true;
+        if (!chg) return;
+        ch = true;
 #pragma unroll
-            for (int p = 0; p < len; ++p)
-                if (chg & (1u << p)) {
-                    sk[c0 + p * cstride] = v[p];
-                    sf[t0 + p * tstride] |= 2;
+        for (int p = 0; p < len; ++p)
+            if (chg & (1u << p)) {
+                sk[c0 + p * cstride] = v[p];
+                sf[t0 + p * tstride] |= 2;
+            }
+        // dirty the other axes' lines through the changed voxels
+        if (axis == 0) {
+            // y-lines (z, x = p): bits z*TX + p, contiguous
+            const int yb = lz * TX;
+            atomicOr(&dirty[1][yb >> 5], chg << (yb & 31));
+            if (ND == 3) {  // z-lines (y, x = p)
+                const int zb = ly * TX;
+                atomicOr(&dirty[2][zb >> 5], chg << (zb & 31));
+            }
+        } else if (axis == 1) {
+            // x-lines (z, y = p): bits z*TY + p, contiguous
+            const int xb = lz * TY;
+            atomicOr(&dirty[0][xb >> 5], chg << (xb & 31));
+            if (ND == 3) {  // z-lines (y = p, x)
+                uint32_t m = chg;
+                while (m) {
+                    const int p = __builtin_ctz(m);
+                    m &= m - 1;
+                    mark(2, p * TX + lx);
                 }
+            }
+        } else {
+            // x-lines (z = p, y) and y-lines (z = p, x)
+            uint32_t m = chg;
+            while (m) {
+                const int p = __builtin_ctz(m);
+                m &= m - 1;
+                mark(0, p * TY + ly);
+                mark(1, p * TX + lx);
+            }
         }
     };
 
-    // Sweep x, y, z, x, ... until the tile is at its fixpoint: every axis swept at least once
-    // and the last ND - 1 sweeps changed nothing (the sweep before them then sees unchanged
-    // inputs again, so it would be a no-op too).
-    int iters = 0, since = 0;
-    for (int k = 0; k < 3 * 1024; ++k) {
+    // Sweep the axes in turn while any line is dirty.
+    int iters = 0;
+    for (int k = 0; k < 3 * 4096; ++k) {
         bool ch = false;
         const int axis = k % ND;
-        if (axis == 0) sweep(std::integral_constant<int, 0>(), tid / TY, tid % TY, ch);      // lines (z, y)
-        else if (axis == 1) sweep(std::integral_constant<int, 1>(), tid / TX, tid % TX, ch);  // (z, x)
-        else if constexpr (ND == 3) sweep(std::integral_constant<int, 2>(), tid / TX, tid % TX, ch);  // (y, x)
+        if (axis == 0) sweep(std::integral_constant<int, 0>(), ch);
+        else if (axis == 1) sweep(std::integral_constant<int, 1>(), ch);
+        else if constexpr (ND == 3) sweep(std::integral_constant<int, 2>(), ch);
         ++iters;
-        since = __syncthreads_or(ch) ? 0 : since + 1;
-        if (k + 1 >= ND && since >= ND - 1) break;
+        __syncthreads();
+        uint32_t any = 0;
+#pragma unroll
+        for (int ax = 0; ax < ND; ++ax)
+#pragma unroll
+            for (int w = 0; w < NW; ++w) any |= dirty[ax][w];
+        if (!any) break;
+        __syncthreads();
     }
 
-    // write back changed voxels; activate face neighbours
+    // write back changed voxels; collect the lines of the face neighbours whose halo changed
     for (int c = tid; c < TN; c += NT) {
         if (!(sf[c] & 2)) continue;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
         key[gb + gz * YX + (int64_t)gy * B.X + gx] = sk[((lz + ZOFF) * HY + (ly + 1)) * HX + (lx + 1)];
+        auto fl = [&](int f, int line) { atomicOr(&sfl[f][line >> 5], 1u << (line & 31)); };
         if (ND == 3) {
-            if (lz == 0) sface[0] = 1;
-            if (lz == TZ - 1) sface[1] = 1;
+            if (lz == 0) fl(0, ly * TX + lx);
+            if (lz == TZ - 1) fl(1, ly * TX + lx);
         }
-        if (ly == 0) sface[2] = 1;
-        if (ly == TY - 1) sface[3] = 1;
-        if (lx == 0) sface[4] = 1;
-        if (lx == TX - 1) sface[5] = 1;
+        if (ly == 0) fl(2, lz * TX + lx);
+        if (ly == TY - 1) fl(3, lz * TX + lx);
+        if (lx == 0) fl(4, lz * TY + ly);
+        if (lx == TX - 1) fl(5, lz * TY + ly);
     }
     __syncthreads();
+    if (tid < 6 * NW) {
+        const int f = tid / NW, wd = tid % NW;
+        const uint32_t bits = sfl[f][wd];
+        const int zz = tzi + (f == 0 ? -1 : f == 1 ? 1 : 0);
+        const int yy = tyi + (f == 2 ? -1 : f == 3 ? 1 : 0);
+        const int xx = txi + (f == 4 ? -1 : f == 5 ? 1 : 0);
+        if (bits && zz >= 0 && zz < B.tz && yy >= 0 && yy < B.ty && xx >= 0 && xx < B.tx) {
+            const int64_t nt = B.tbase + (zz * B.ty + yy) * B.tx + xx;
+            const int axis = f < 2 ? 2 : (f < 4 ? 1 : 0);
+            atomicOr(&lines_next[nt * kLineWords + axis * 8 + wd], bits);
+            atomicOr(&act_next[nt], 1u);
+            atomicAdd(counter, 1u);
+        }
+    }
+    // lines swept (wave-aggregated)
+    for (int o = 32; o > 0; o >>= 1) nlines += __shfl_xor(nlines, o);
+    if ((tid & 63) == 0) atomicAdd(counter + 3, nlines);
     if (tid == 0) {
-        int n = 0;
-        auto act = [&](int zz, int yy, int xx) {
-            if (zz < 0 || zz >= B.tz || yy < 0 || yy >= B.ty || xx < 0 || xx >= B.tx) return;
-            act_next[B.tbase + (zz * B.ty + yy) * B.tx + xx] = 1;
-            ++n;
-        };
-        if (sface[0]) act(tzi - 1, tyi, txi);
-        if (sface[1]) act(tzi + 1, tyi, txi);
-        if (sface[2]) act(tzi, tyi - 1, txi);
-        if (sface[3]) act(tzi, tyi + 1, txi);
-        if (sface[4]) act(tzi, tyi, txi - 1);
-        if (sface[5]) act(tzi, tyi, txi + 1);
-        if (n) atomicAdd(counter, (uint32_t)n);
         atomicAdd(counter + 1, 1u);              // tiles solved
-        atomicAdd(counter + 2, (uint32_t)iters);  // local iterations
+        atomicAdd(counter + 2, (uint32_t)iters);  // sweeps
     }
 }
 
 template __global__ void k_flood_packed<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                           const uint32_t*, const uint8_t*, uint8_t*, uint32_t*);
+                                           const uint8_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
+                                           uint32_t*);
 template __global__ void k_flood_packed<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                           const uint32_t*, const uint8_t*, uint8_t*, uint32_t*);
+                                           const uint8_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
+                                           uint32_t*);
+
 
 // packed keys -> labels (keeps the seed bit of `lab`)
 __global__ void __launch_bounds__(256) k_unpack_labels(const BlockDesc* __restrict__ D, const BlockStat* S,

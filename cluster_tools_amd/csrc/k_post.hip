@@ -84,7 +84,8 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
                                                      FilterParams fp, const uint32_t* __restrict__ counts,
                                                      const uint8_t* __restrict__ excl, const float* __restrict__ h,
                                                      uint32_t* __restrict__ lab, uint64_t* __restrict__ key,
-                                                     uint32_t* __restrict__ survivors, int packed) {
+                                                     uint8_t* __restrict__ fixedv, uint32_t* __restrict__ survivors,
+                                                     int packed) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -94,11 +95,17 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
         if (keep) {
             lab[B.base + i] = l | kFixedBit;
             key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
+            fixedv[B.base + i] = 1;
             const int z = (B.nd_ws == 2) ? (int)(i / YX) : 0;
             if (!survivors[B.sbase + z]) survivors[B.sbase + z] = 1;
         } else {
             lab[B.base + i] = 0;
             key[B.base + i] = kInfKey;
+            fixedv[B.base + i] = 0;
+            // only tiles with a free voxel can change in the regrow flood
+            const int x = (int)(i % B.X), y = (int)((i / B.X) % B.Y), z = (int)(i / YX);
+            uint32_t* a = fp.act + B.tbase + ((z / fp.tz) * B.ty + y / fp.ty) * B.tx + x / fp.tx;
+            if (!*a) atomicOr(a, 8u);
         }
     }
 }
