@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -53,6 +54,11 @@ struct Workspace {
     BlockStat* stat = nullptr;
     uint32_t* counter = nullptr;
     double* taps = nullptr;  // [6][128]
+    // pass 2 (two-pass watershed) relabel hash
+    int64_t cap_hash = 0;
+    uint64_t* hkey = nullptr;
+    uint32_t* hpos = nullptr;
+    uint32_t* p2err = nullptr;
 };
 
 constexpr int kMaxTaps = 127;  // radius <= 63
@@ -74,6 +80,7 @@ struct ctws_handle {
     DevBuf st_in, st_mask, st_init, st_out;
     // test hooks
     int stop_after = 0;
+    int trace = 0;  // CTWS_TRACE=1: per-round flood statistics on stderr
     std::vector<BlockDesc> last_desc;
     // RCCL
     ncclComm_t comm = nullptr;
@@ -130,7 +137,7 @@ int grow(ctws_handle* h, DevBuf& b, size_t bytes) {
 }
 
 int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks, int64_t slices, int64_t tiles,
-                     int64_t blocks) {
+                     int64_t blocks, int64_t hash) {
     Workspace& w = h->ws;
     int r = CTWS_OK;
 #define ALLOC(field, n) \
@@ -180,6 +187,12 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(stat, blocks);
         w.cap_blocks = blocks;
     }
+    if (hash > w.cap_hash) {
+        ALLOC(hkey, hash);
+        ALLOC(hpos, hash);
+        w.cap_hash = hash;
+    }
+    if (!w.p2err) ALLOC(p2err, 4);
     if (!w.counter) ALLOC(counter, 4);
     if (!w.taps) ALLOC(taps, 6 * 128);
 #undef ALLOC
@@ -217,7 +230,7 @@ struct BlockIO {
 
 struct Plan {
     // validated, derived configuration
-    int nd_ws, dt_2d;
+    int nd_ws, dt_2d, pass2;
     int pitch[3];
     bool seeds_smooth, weights_smooth;
     double sig_seeds[3], sig_weights[3];
@@ -226,10 +239,11 @@ struct Plan {
 int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
     p.nd_ws = cfg->apply_ws_2d ? 2 : 3;
     p.dt_2d = cfg->apply_dt_2d ? 1 : 0;
-    if (cfg->pass_id != 0) {
-        h->err = "two-pass pass 1 (_ws_pass2) is not implemented in this build";
-        return CTWS_EUNSUPPORTED;
+    if (cfg->pass_id != 0 && cfg->pass_id != 1) {
+        h->err = "pass_id must be 0 (_ws_block) or 1 (_ws_pass2)";
+        return CTWS_EINVAL;
     }
+    p.pass2 = cfg->pass_id == 1 ? 1 : 0;
     for (int k = 0; k < 3; ++k) p.pitch[k] = 1;
     if (cfg->has_pixel_pitch) {
         if (p.dt_2d) {
@@ -389,6 +403,10 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
         kms += ms;
         tiles_solved += h->h_counter[1];
         local_iters += h->h_counter[2];
+        if (h->trace)
+            fprintf(stderr, "[ctws] flood%s round %d: %.3f ms, tiles %u, sweeps %u, lines %u, next %u\n",
+                    preset ? " (regrow)" : "", round, ms, h->h_counter[1], h->h_counter[2], h->h_counter[3],
+                    h->h_counter[0]);
         h->flood_lines += h->h_counter[3];
         if (*h->h_counter == 0) break;
         HIPCHK(hipMemsetAsync(cur, 0, sizeof(uint32_t) * (size_t)ntiles, h->stream));
@@ -409,7 +427,8 @@ int64_t chunks_of(int64_t n) { return (words_of(n) + 255) / 256; }
 int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* blocks, const BlockIO* io, int nb) {
     Workspace& w = h->ws;
     std::vector<BlockDesc> desc(nb);
-    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0;
+    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0, TH = 0;
+    int64_t maxH = 0;
     int maxZ = 0, maxY = 0, maxX = 0, max_tiles = 0;
     int64_t maxN = 0, maxNI = 0;
     const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
@@ -457,6 +476,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             d.C = 1;
         }
         d.id_offset = (uint64_t)b.block_id * bvol;
+        d.pass2 = (uint32_t)pl.pass2;
+        if (pl.pass2) {
+            if (!d.init) {
+                h->err = "pass 2 needs initial_seeds (ds_out[input_bb]) for every block";
+                return CTWS_EINVAL;
+            }
+            int64_t cap = 4096;
+            while (cap < d.N / 4) cap <<= 1;
+            d.hbase = TH;
+            d.hcap = cap;
+            TH += cap;
+        }
         d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
                             (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
         T += d.N;
@@ -469,6 +500,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         maxX = std::max(maxX, d.X);
         maxN = std::max(maxN, d.N);
         maxNI = std::max(maxNI, d.NI);
+        maxH = std::max(maxH, d.hcap);
         // validation against what the kernels assume
         if (d.X > 1024 || d.Y > 2048 || d.Z > 2048 || d.N >= (1ll << 31)) {
             h->err = "outer block too large for the kernels (X <= 1024, Y, Z <= 2048, N < 2^31)";
@@ -530,7 +562,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     const int64_t TT_wide = TT;
     set_tiles(true);
     int r;
-    if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb)) != CTWS_OK) return r;
+    if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb, TH)) != CTWS_OK) return r;
     HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
     h->last_desc = desc;
     std::vector<BlockStat> st(nb);
@@ -600,6 +632,15 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             }
         }
     }
+    if (pl.pass2 && pl.nd_ws == 2) {
+        // two_pass_watershed.py:139: no maxima on initial seeds; per-slice dt stats again
+        k_p2_zero_dt<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.dt);
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)w.smin, 0xFFFFFFFFu, (size_t)TS, h->stream));
+        HIPCHK(hipMemsetAsync(w.smax, 0, sizeof(uint32_t) * TS, h->stream));
+        dim3 gs((unsigned)maxZ, nb);
+        k_dt_slice_stats<<<gs, 256, 0, h->stream>>>(w.desc, w.stat, w.dt, w.smin, w.smax);
+        LAUNCHCHK();
+    }
     mark("edt_yz");
 
     // ---- seed map smoothing, hmap -----------------------------------------------------------
@@ -634,6 +675,23 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     k_bitmap<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.csum);
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
+    const dim3 gsb((unsigned)((maxZ + 255) / 256), nb);
+    if (pl.pass2) {
+        // _apply_watershed_with_seeds: shifted seeds + initial seeds, relabelConsecutive
+        k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
+        HIPCHK(hipMemsetAsync(w.hkey, 0xFF, sizeof(uint64_t) * (size_t)TH, h->stream));
+        HIPCHK(hipMemsetAsync(w.hpos, 0xFF, sizeof(uint32_t) * (size_t)TH, h->stream));
+        HIPCHK(hipMemsetAsync(w.p2err, 0, sizeof(uint32_t) * 4, h->stream));
+        k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.sb, w.key);
+        k_p2_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.hkey, w.hpos, w.p2err);
+        HIPCHK(hipMemsetAsync(w.P, 0xFF, sizeof(uint32_t) * (size_t)T, h->stream));
+        const dim3 hg((unsigned)std::min<int64_t>((maxH + 255) / 256, 4096), nb);
+        k_p2_roots<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.P);
+        k_bitmap<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.P, w.W, w.csum);
+        k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
+        k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
+        LAUNCHCHK();
+    }
     // packed flood keys need labels < 2^20 in every block of the batch
     bool packed = true;
     {
@@ -648,11 +706,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             h->last_desc = desc;
         }
     }
-    k_seed_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
-                                            packed ? 1 : 0);
-    {
-        dim3 gs((unsigned)((maxZ + 255) / 256), nb);
-        k_slice_seed_base<<<gs, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
+    uint8_t* excl = nullptr;
+    if (pl.pass2) {
+        k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
+        k_p2_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
+                                              (uint32_t*)w.Bf, (uint32_t*)w.sm, packed ? 1 : 0);
+        excl = (uint8_t*)w.fin;  // free after the hmap
+        k_p2_excl_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, excl);
+        k_p2_excl<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, excl);
+    } else {
+        k_seed_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
+                                                packed ? 1 : 0);
+        k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
     }
     LAUNCHCHK();
     mark("seeds");
@@ -682,7 +747,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         FilterParams fp{(uint32_t)cfg->size_filter, 0, 0, 0, w.act0};
         flood_tile_dims(pl.nd_ws, packed, &fp.tz, &fp.ty, &fp.tx);
         HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-        k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, nullptr, w.hm, w.lab, w.key, w.cls,
+        k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, excl, w.hm, w.lab, w.key, w.cls,
                                                  w.surv, packed ? 1 : 0);
         LAUNCHCHK();
         if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds2, &fk2)) != CTWS_OK) return r;
@@ -690,6 +755,22 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
     mark("size_filter");
 
+    // ---- pass 2: per-slice offsets, takeDict, uncropped inner write --------------------------
+    if (pl.pass2) {
+        if (pl.nd_ws == 2) {
+            k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.sb, w.slmax);
+            k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
+            k_p2_check<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.soff, w.p2err);
+        }
+        HIPCHK(hipMemsetAsync(w.smin, 0, sizeof(uint32_t) * TS, h->stream));  // free after the hmap
+        k_slice_inmask<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.smin);
+        mark("finalize");
+        mark("crop_cc");
+        k_p2_output<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, (const uint32_t*)w.Bf, (const uint32_t*)w.sm,
+                                               w.soff);
+        LAUNCHCHK();
+        mark("output");
+    } else {
     // ---- 2-D offsets / mask -> final uint32 ws ---------------------------------------------
     if (pl.nd_ws == 2) {
         k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.sb, w.slmax);
@@ -720,6 +801,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     k_output<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF, w.W, w.Wp);
     LAUNCHCHK();
     mark("output");
+    }
 
     HIPCHK(hipMemcpyAsync(st.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
     std::vector<uint32_t> surv;
@@ -727,7 +809,25 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         surv.resize(TS);
         HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
     }
+    std::vector<uint32_t> sbh, inmask;
+    uint32_t p2err = 0;
+    if (pl.pass2) {
+        sbh.resize(TS);
+        inmask.resize(TS);
+        HIPCHK(hipMemcpyAsync(sbh.data(), w.sb, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipMemcpyAsync(inmask.data(), w.smin, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipMemcpyAsync(&p2err, w.p2err, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+    }
     HIPCHK(hipStreamSynchronize(h->stream));
+    if (p2err & 1u) {
+        h->err = "pass 2: relabel hash table full";
+        return CTWS_EUNSUPPORTED;
+    }
+    if (p2err & 2u) {
+        h->err = "pass 2 (2-D): a shifted new seed id equals an initial seed id of its slice after the uint32 "
+                 "wrap-around (two_pass_watershed.py:146-153); relabelConsecutive would merge them: not implemented";
+        return CTWS_EUNSUPPORTED;
+    }
     for (size_t i = 1; i < ev; ++i) {
         float ms = 0.f;
         hipEventElapsedTime(&ms, h->events[i - 1], h->events[i]);
@@ -742,14 +842,28 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     h->timings.push_back({"flood_lines_swept", (float)h->flood_lines});
     h->timings.push_back({"size_filter_kernel_ms", fk2});
     for (int i = 0; i < nb; ++i) {
-        blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : CTWS_BLOCK_EMPTY;
+        blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : (pl.pass2 ? CTWS_BLOCK_EMPTY_PASS2 : CTWS_BLOCK_EMPTY);
         blocks[i].max_label = st[i].active ? st[i].max_label : 0;
+        const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
+        if (st[i].active && pl.pass2) {
+            // a slice/block without any seed: vigra generates seeds from the hmap's local minima
+            // (watershedsNew with labels.any() == false).  Irrelevant where nothing lies inside
+            // the mask (the result is zeroed, max_id 0); otherwise not implemented.
+            for (int z = 0; z < ns; ++z) {
+                const int64_t s0 = desc[i].sbase + z;
+                const uint32_t nl = pl.nd_ws == 2 ? ((z + 1 < ns ? sbh[s0 + 1] : st[i].n_seeds) - sbh[s0]) : st[i].n_seeds;
+                if (!nl && inmask[s0]) {
+                    h->err = "pass 2: a slice/block without seeds inside the mask (auto-seeded watershed) is not "
+                             "implemented";
+                    return CTWS_EUNSUPPORTED;
+                }
+            }
+        }
         if (st[i].active && cfg->size_filter > 0) {
             // every segment of a slice/block below size_filter: vigra then seeds the regrow
             // from the local minima of the hmap (watershedsGraph with labels.any() == false)
-            const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
             for (int z = 0; z < ns; ++z)
-                if (!surv[desc[i].sbase + z]) {
+                if (!surv[desc[i].sbase + z] && (!pl.pass2 || inmask[desc[i].sbase + z])) {
                     h->err = "size filter removed every segment of a block/slice (auto-seeded regrow) "
                              "is not implemented";
                     return CTWS_EUNSUPPORTED;
@@ -864,6 +978,7 @@ int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, b
             }
             if ((r = run_batch(h, cfg, pl, bb.data(), io.data(), nb)) != CTWS_OK) return r;
             for (int i = 0; i < nb; ++i) {
+                if (bb[i].status == CTWS_BLOCK_EMPTY_PASS2) continue;  // nothing written (:240-242)
                 const size_t ob = (size_t)(bb[i].inner_shape[0] * bb[i].inner_shape[1] * bb[i].inner_shape[2]) * 8;
                 HIPCHK(hipMemcpyAsync(bb[i].output, io[i].out, ob, hipMemcpyDeviceToHost, h->stream));
             }
@@ -893,6 +1008,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (device < 0 || device >= n) return CTWS_EINVAL;
     ctws_handle* h = new ctws_handle();
     h->device = device;
+    if (const char* t = std::getenv("CTWS_TRACE")) h->trace = std::atoi(t);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, 16, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * 128 * sizeof(double), hipHostMallocDefault) != hipSuccess) {

@@ -35,7 +35,9 @@ struct BlockDesc {
     uint64_t id_offset;     // block_id * prod(block_shape)
     int tz, ty, tx, tbase;  // flood tile grid, offset into per-tile arrays
     uint32_t maxd;          // 3-D EDT: ceil(dmax) = sum_k (pitch_k n_k)^2
-    uint32_t _p2;
+    uint32_t pass2;         // 1: _ws_pass2 (two_pass_watershed.py:210-255)
+    int64_t hbase;          // pass 2: offset into the relabel hash arrays
+    int64_t hcap;           // pass 2: hash capacity of this block (power of two)
 };
 
 struct BlockStat {

@@ -90,4 +90,19 @@ __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*,
 __global__ void k_slice_offsets(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint32_t*);
 
+// k_pass2.hip (two-pass watershed, pass 2)
+__global__ void k_p2_zero_dt(const BlockDesc*, const BlockStat*, float*);
+__global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
+                            const uint32_t*, uint64_t*);
+__global__ void k_p2_insert(const BlockDesc*, const BlockStat*, const uint64_t*, uint64_t*, uint32_t*, uint32_t*);
+__global__ void k_p2_roots(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
+__global__ void k_p2_label(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, const uint64_t*,
+                           const uint32_t*, const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, uint32_t*, int);
+__global__ void k_p2_excl_zero(const BlockDesc*, const BlockStat*, uint8_t*);
+__global__ void k_p2_excl(const BlockDesc*, const BlockStat*, const uint32_t*, uint8_t*);
+__global__ void k_p2_check(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
+__global__ void k_p2_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*, const uint32_t*,
+                            const uint32_t*);
+__global__ void k_slice_inmask(const BlockDesc*, const BlockStat*, uint32_t*);
+
 }  // namespace ctws

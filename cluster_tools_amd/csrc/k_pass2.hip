@@ -1,0 +1,296 @@
+// k_pass2.hip — the second pass of the two-pass (checkerboard) watershed on gfx950.
+//
+// Reference: watershed/two_pass_watershed.py:210-255 (_ws_pass2) and :122-207
+// (_apply_watershed_with_seeds).  A pass-2 block is seeded by its own local maxima AND by the
+// pass-1 labels of its neighbours found in its halo (`initial_seeds = ds_out[input_bb]`):
+//
+//   2-D ws only:  dt[z][initial_seeds[z] != 0] = 0                         (:139)
+//   seeds = _make_seeds(dt);  seeds[outside mask] = 0                      (:141-144, :181-183)
+//   seeds[seeds != 0] += offset         (uint32 array: wraps mod 2^32)     (:147, :184)
+//   seeds[initial != 0] = initial       (uint64 -> uint32 setitem)         (:149, :187-188)
+//   seeds = relabelConsecutive(seeds)   (first appearance in vigra order)  (:153, :192)
+//   ws = watershed(hmap, seeds, size_filter, exclude=<initial ids>)        (:160, :199-202)
+//   ws = takeDict(new_to_old, ws);  ws[outside mask] = 0;  write ws[inner] (no CC relabel)
+//
+// In 2-D mode `offset` grows slice by slice by the max_id of the previous slices (:166-168),
+// which is only known after their floods.  relabelConsecutive numbers by first appearance,
+// so the offset changes the numbering only where a shifted new seed value equals an initial
+// value of the same slice.  The relabel therefore keys new seeds by (slice, tag 0, local
+// seed id) and initial seeds by (slice, tag 1, value); once the slice offsets are known,
+// k_p2_check verifies that no such equality exists (it raises CTWS_EUNSUPPORTED if one does).
+// In 3-D mode the offset is the constant block_id * prod(block_shape), so keys are the exact
+// uint32 values, as in the reference.
+//
+// relabelConsecutive is computed with a per-block open-addressing hash (key -> smallest
+// vigra scan-order key f holding it): the first positions become roots of a bitmap, and the
+// new id of a value is 1 + the rank of its first position (the machinery of k_cc.hip).
+#include "ctws_kernels.h"
+
+namespace ctws {
+
+#define BLOCK_LOOP(i, B)                                                                      \
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (B).N;              \
+         i += (int64_t)gridDim.x * blockDim.x)
+
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr uint64_t kInitTag = 1ull << 32;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// slot of `k` in the block's table, or -1 (absent / table full: the error bit is set)
+__device__ __forceinline__ int64_t hash_find(const uint64_t* hk, int64_t cap, uint64_t k) {
+    int64_t s = (int64_t)(mix64(k) & (uint64_t)(cap - 1));
+    for (int64_t p = 0; p < cap; ++p) {
+        const uint64_t v = hk[s];
+        if (v == k) return s;
+        if (v == kEmptyKey) return -1;
+        s = (s + 1) & (cap - 1);
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void inner_to_zyx(int64_t i, int64_t YX, int X, int& z, int& y, int& x) {
+    z = (int)(i / YX);
+    const int rem = (int)(i - z * YX);
+    y = rem / X;
+    x = rem - y * X;
+}
+
+// vigra scan-order key (F order; per slice in 2-D ws mode, slice-major across slices)
+__device__ __forceinline__ uint32_t scan_key(const BlockDesc& B, int z, int y, int x) {
+    return (B.nd_ws == 3) ? (uint32_t)(z + B.Z * (y + B.Y * x))
+                          : (uint32_t)((int64_t)z * B.Y * B.X + y + (int64_t)B.Y * x);
+}
+
+// 2-D ws: no maxima on initial seeds (two_pass_watershed.py:139)
+__global__ void __launch_bounds__(256) k_p2_zero_dt(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                    float* __restrict__ dt) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    BLOCK_LOOP(i, B) {
+        if (B.init[i] != 0) dt[B.base + i] = 0.0f;
+    }
+}
+
+// per-voxel relabel key (kEmptyKey: unlabelled); written into `vkey`
+__global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                   const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ Wg,
+                                                   const uint32_t* __restrict__ Wpg, const uint32_t* __restrict__ sb,
+                                                   uint64_t* __restrict__ vkey) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const uint32_t* PF = PFg + B.base;
+    BLOCK_LOOP(i, B) {
+        int z, y, x;
+        inner_to_zyx(i, YX, B.X, z, y, x);
+        const uint64_t u = B.init[i];
+        uint64_t k = kEmptyKey;
+        if (u != 0) {
+            // (uint32)u == 0: the setitem truncation makes the voxel background
+            if ((uint32_t)u != 0)
+                k = (B.nd_ws == 3) ? (uint64_t)(uint32_t)u : (((uint64_t)z << 33) | kInitTag | (uint32_t)u);
+        } else if (!B.mask || B.mask[i]) {
+            const uint32_t f = scan_key(B, z, y, x);
+            const uint32_t r = PF[f];  // flattened: the root
+            if (r != kNoParent) {
+                const uint32_t gl = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, r) + 1u;
+                if (B.nd_ws == 3) {
+                    const uint32_t v = gl + (uint32_t)B.id_offset;  // wraps to 0: background
+                    if (v) k = v;
+                } else k = ((uint64_t)z << 33) | (uint64_t)(gl - sb[B.sbase + z]);
+            }
+        }
+        vkey[B.base + i] = k;
+    }
+}
+
+// insert keys whose scan-order predecessor holds a different key (only those can be the
+// first appearance); the table keeps the smallest scan key per value
+__global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                   const uint64_t* __restrict__ vkey, uint64_t* __restrict__ hkey,
+                                                   uint32_t* __restrict__ hpos, uint32_t* __restrict__ err) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    uint64_t* hk = hkey + B.hbase;
+    uint32_t* hp = hpos + B.hbase;
+    const int64_t cap = B.hcap;
+    BLOCK_LOOP(i, B) {
+        const uint64_t k = vkey[B.base + i];
+        if (k == kEmptyKey) continue;
+        int z, y, x;
+        inner_to_zyx(i, YX, B.X, z, y, x);
+        // predecessor in scan order: z - 1 (3-D) / y - 1 (2-D)
+        if (B.nd_ws == 3 ? z > 0 : y > 0) {
+            const int64_t j = (B.nd_ws == 3) ? i - YX : i - B.X;
+            if (vkey[B.base + j] == k) continue;
+        }
+        const uint32_t f = scan_key(B, z, y, x);
+        int64_t s = (int64_t)(mix64(k) & (uint64_t)(cap - 1));
+        bool done = false;
+        for (int64_t p = 0; p < cap; ++p) {
+            uint64_t v = hk[s];
+            if (v == kEmptyKey) v = atomicCAS((unsigned long long*)&hk[s], (unsigned long long)kEmptyKey, k);
+            if (v == kEmptyKey || v == k) {
+                atomicMin(&hp[s], f);
+                done = true;
+                break;
+            }
+            s = (s + 1) & (cap - 1);
+        }
+        if (!done) atomicOr(err, 1u);  // table full
+    }
+}
+
+// first positions -> roots of the bitmap (P preset to kNoParent)
+__global__ void __launch_bounds__(256) k_p2_roots(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                  const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ hpos,
+                                                  uint32_t* __restrict__ P) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < B.hcap; s += (int64_t)gridDim.x * blockDim.x) {
+        if (hkey[B.hbase + s] == kEmptyKey) continue;
+        const uint32_t f = hpos[B.hbase + s];
+        P[B.base + f] = f;
+    }
+}
+
+// flood labels = new consecutive ids (block-global, slice-major in 2-D); old values per id
+__global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                  const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ hpos,
+                                                  const uint64_t* __restrict__ Wg, const uint32_t* __restrict__ Wpg,
+                                                  const float* __restrict__ h, uint32_t* __restrict__ lab,
+                                                  uint64_t* __restrict__ key /* in: vkey */,
+                                                  uint8_t* __restrict__ fixedv, uint32_t* __restrict__ oldv,
+                                                  uint32_t* __restrict__ oldt, int packed) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    BLOCK_LOOP(i, B) {
+        const uint64_t k = key[B.base + i];
+        if (k == kEmptyKey) {
+            lab[B.base + i] = 0;
+            fixedv[B.base + i] = 0;
+            continue;  // key stays kEmptyKey == kInfKey
+        }
+        const int64_t s = hash_find(hkey + B.hbase, B.hcap, k);
+        const uint32_t pos = s >= 0 ? hpos[B.hbase + s] : 0u;  // s < 0 cannot happen after insert
+        const uint32_t l = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, pos) + 1u;
+        lab[B.base + i] = l | kFixedBit;
+        key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
+        fixedv[B.base + i] = 1;
+        int z, y, x;
+        inner_to_zyx(i, YX, B.X, z, y, x);
+        if (scan_key(B, z, y, x) == pos) {
+            oldv[B.base + l] = (uint32_t)k;
+            oldt[B.base + l] = (uint32_t)((k >> 32) & 1u);
+        }
+    }
+}
+
+// size-filter exclusion (np.in1d(filter_ids, exclude)): a NEW id is kept when its numeric
+// value equals an initial value (3-D: unique initial ids, :199-202; 2-D: the initial seeds of
+// the slice, :160) — the mismatched id spaces of the reference
+__global__ void __launch_bounds__(256) k_p2_excl(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                 const uint32_t* __restrict__ sb, uint8_t* __restrict__ excl) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const uint32_t nl = S[blockIdx.y].n_seeds;
+    BLOCK_LOOP(i, B) {
+        const uint64_t u = B.init[i];
+        if (u == 0) continue;
+        if (B.nd_ws == 3) {
+            if (u <= nl) excl[B.base + u] = 1;
+        } else {
+            const int z = (int)(i / YX);
+            const uint32_t b0 = sb[B.sbase + z];
+            const uint32_t b1 = (z + 1 < B.Z) ? sb[B.sbase + z + 1] : nl;
+            if (u <= (uint64_t)(b1 - b0)) excl[B.base + b0 + u] = 1;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_p2_excl_zero(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                      uint8_t* __restrict__ excl) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t n = (int64_t)S[blockIdx.y].n_seeds + 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        excl[B.base + i] = 0;
+}
+
+// 2-D: with the slice offsets known, no shifted new seed may equal an initial value of its
+// slice (else relabelConsecutive would have merged them: unsupported, err bit 1)
+__global__ void __launch_bounds__(256) k_p2_check(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                  const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ soff,
+                                                  uint32_t* __restrict__ err) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active || B.nd_ws != 2) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    BLOCK_LOOP(i, B) {
+        const uint64_t u = B.init[i];
+        const int z = (int)(i / YX);
+        if (i == (int64_t)z * YX) {
+            // a shifted new seed that wraps to 0 would have become background
+            const uint32_t t0 = 0u - (uint32_t)B.id_offset - soff[B.sbase + z];
+            if (t0 && hash_find(hkey + B.hbase, B.hcap, ((uint64_t)z << 33) | t0) >= 0) atomicOr(err, 2u);
+        }
+        if (u == 0 || (uint32_t)u == 0) continue;
+        const uint32_t t = (uint32_t)u - (uint32_t)B.id_offset - soff[B.sbase + z];
+        if (t == 0) continue;
+        if (hash_find(hkey + B.hbase, B.hcap, ((uint64_t)z << 33) | t) >= 0) atomicOr(err, 2u);
+    }
+}
+
+// uint64 output of the inner block: takeDict(new_to_old), outside mask -> 0, no CC relabel,
+// no offset (two_pass_watershed.py:171-173, 203-206, 252)
+__global__ void __launch_bounds__(256) k_p2_output(const BlockDesc* __restrict__ D, BlockStat* S,
+                                                   const uint32_t* __restrict__ lab, const uint32_t* __restrict__ oldv,
+                                                   const uint32_t* __restrict__ oldt, const uint32_t* __restrict__ soff) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;  // dt is None: nothing is written (:240-242)
+    const int64_t yx = (int64_t)B.IY * B.IX;
+    uint32_t mx = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.NI; i += (int64_t)gridDim.x * blockDim.x) {
+        const int z = (int)(i / yx);
+        const int rem = (int)(i - z * yx);
+        const int y = rem / B.IX, x = rem - (rem / B.IX) * B.IX;
+        const int64_t o = ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0);
+        const uint32_t l = lab[B.base + o] & ~kFixedBit;
+        uint32_t v = 0;
+        if (l && (!B.mask || B.mask[o])) {
+            v = oldv[B.base + l];
+            if (B.nd_ws == 2 && !oldt[B.base + l]) v = v + (uint32_t)B.id_offset + soff[B.sbase + z + B.iz0];
+        }
+        mx = max(mx, v);
+        B.out[i] = v;
+    }
+    for (int s = 32; s > 0; s >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, s));
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(&S[blockIdx.y].max_label, mx);
+}
+
+}  // namespace ctws
+
+namespace ctws {
+// per slice (2-D ws) / block (3-D ws): 1 if any voxel lies inside the mask (all, without one)
+__global__ void __launch_bounds__(256) k_slice_inmask(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                      uint32_t* __restrict__ flag) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    BLOCK_LOOP(i, B) {
+        if (B.mask && !B.mask[i]) continue;
+        uint32_t* f = flag + B.sbase + (B.nd_ws == 2 ? (int)(i / YX) : 0);
+        if (!*f) *f = 1;
+    }
+}
+}  // namespace ctws

@@ -167,8 +167,9 @@ class Handle:
     # ---- device (torch) blocks ----------------------------------------------------------
     def ws_blocks_device(self, config, block_shape, blocks, pass_id=0):
         """Same with torch tensors resident on this GPU: blocks[i] has 'input' (outer tensor),
-        'output' (inner uint64/int64 tensor), optional 'mask' (uint8 tensor), 'inner_begin',
-        'crop_relabel', 'block_id'.  Returns [(status, max_label)]."""
+        'output' (inner uint64/int64 tensor), optional 'mask' (uint8 tensor), 'initial_seeds'
+        (outer int64 tensor, pass 2), 'inner_begin', 'crop_relabel', 'block_id'.
+        Returns [(status, max_label)]."""
         import torch
         cfg = make_cfg(config, block_shape, pass_id)
         n = len(blocks)
@@ -189,7 +190,12 @@ class Handle:
                 c.n_channels = 0
                 c.outer_shape[:] = list(inp.shape)
             if b.get('mask') is not None:
+                assert b['mask'].is_contiguous() and b['mask'].element_size() == 1
                 c.mask = b['mask'].data_ptr()
+            if b.get('initial_seeds') is not None:
+                s = b['initial_seeds']
+                assert s.is_contiguous() and s.element_size() == 8 and tuple(s.shape) == tuple(c.outer_shape)
+                c.initial_seeds = s.data_ptr()
             out = b['output']
             assert out.is_contiguous() and out.element_size() == 8
             c.inner_begin[:] = list(b.get('inner_begin', (0, 0, 0)))
@@ -214,5 +220,5 @@ class Handle:
         counts = np.ascontiguousarray(counts, dtype=np.int64)
         out = np.zeros(len(counts) * nranks, dtype=np.int64)
         self._check(lib().ctws_allgather_counts(self._h, counts.ctypes.data, len(counts), out.ctypes.data),
-                    'ctws_allgather_counts', 'ctws_debug_set_stop', 'ctws_debug_read')
+                    'ctws_allgather_counts')
         return out

@@ -1,0 +1,80 @@
+"""Two-pass (checkerboard) scenarios for the pass-2 parity tests.
+
+A small volume is cut into a 2 x 2 (y, x) block grid with a halo; the checkerboard colour of
+block 0 (blocks 0 and 3) runs pass 1 (`_ws_block`) in the oracle and writes a full output
+volume, then the other colour (blocks 1 and 2) runs `_ws_pass2` with
+`initial_seeds = out[outer bb]` (two_pass_watershed.py:224-228).  Both the GPU and the oracle
+pass 2 see the same initial seeds, so pass 2 is compared on its own.
+"""
+import numpy as np
+
+from cluster_tools_amd.synthetic import boundary_map, ellipsoid_mask
+from oracle import oracle as O
+
+VOL = (24, 128, 128)
+GRID_BLOCK = (24, 64, 64)
+
+D3 = dict(apply_dt_2d=False, apply_ws_2d=False)
+
+# name -> (task config, halo, block-id base, masked)
+SCENARIOS = {
+    '3d': (dict(D3), (0, 16, 16), 0, False),
+    '2d': ({}, (0, 16, 16), 0, False),
+    '3d_mask': (dict(D3), (0, 16, 16), 0, True),
+    '2d_mask': ({}, (0, 16, 16), 0, True),
+    '3d_wrap': (dict(D3), (0, 16, 16), 44000, False),     # block_id * V >= 2^32 (Appendix B.2)
+    '2d_wrap': ({}, (0, 12, 20), 44000, False),
+    '3d_nofilter': (dict(D3, size_filter=0), (0, 16, 16), 0, False),
+    '3d_bigfilter': (dict(D3, size_filter=400), (0, 16, 16), 0, False),
+    '2d_dt3d': (dict(apply_dt_2d=False), (0, 16, 16), 0, False),
+}
+
+
+def _blocks(block_shape, halo):
+    gy, gx = VOL[1] // GRID_BLOCK[1], VOL[2] // GRID_BLOCK[2]
+    out = []
+    for by in range(gy):
+        for bx in range(gx):
+            beg = (0, by * GRID_BLOCK[1], bx * GRID_BLOCK[2])
+            end = tuple(b + s for b, s in zip(beg, GRID_BLOCK))
+            obeg = tuple(max(0, b - h) for b, h in zip(beg, halo))
+            oend = tuple(min(v, e + h) for v, e, h in zip(VOL, end, halo))
+            out.append(dict(local_id=by * gx + bx, colour=(by + bx) % 2,
+                            outer=tuple(slice(a, b) for a, b in zip(obeg, oend)),
+                            inner_begin=tuple(b - o for b, o in zip(beg, obeg)),
+                            inner=tuple(slice(a, b) for a, b in zip(beg, end))))
+    return out
+
+
+def scenario(name, seed=3):
+    """-> (config, block_shape, list of pass-2 block dicts with initial_seeds)."""
+    config, halo, id_base, masked = SCENARIOS[name]
+    config = dict(config, halo=list(halo))
+    x = boundary_map(VOL, seed=seed)
+    mask = ellipsoid_mask(VOL) if masked else None
+    # the ids are block_id * prod(block_shape): the task's block_shape is the grid block
+    block_shape = GRID_BLOCK
+    out = np.zeros(VOL, np.uint64)
+    blocks = _blocks(block_shape, halo)
+
+    def as_block(b):
+        d = dict(input=x[b['outer']], block_id=id_base + b['local_id'], inner_begin=b['inner_begin'],
+                 inner_shape=GRID_BLOCK, crop_relabel=sum(halo) > 0)
+        if mask is not None:
+            d['mask'] = mask[b['outer']]
+        return d
+
+    first = [b for b in blocks if b['colour'] == 0]
+    res = O.ws_blocks(config, block_shape, [as_block(b) for b in first])
+    for b, r in zip(first, res):
+        if r['status'] in (0, 2):
+            out[b['inner']] = r['output']
+    second = []
+    for b in blocks:
+        if b['colour'] != 1:
+            continue
+        d = as_block(b)
+        d['crop_relabel'] = False
+        d['initial_seeds'] = out[b['outer']].copy()
+        second.append(d)
+    return config, block_shape, second

@@ -110,3 +110,63 @@ def test_watershed_workflow(tmp_path, name, with_mask):
         table = f['relabel_watershed'][:]
     _check_result(res.astype('uint64'), with_mask)
     assert len(np.unique(res)) == len(table)
+
+
+def _oracle_two_pass(x, c, mask):
+    """The reference's TwoPassWatershed over the volume via the oracle: pass 1 on the
+    checkerboard colour of block 0, then pass 2 on the other colour with the pass-1 labels
+    as initial seeds (all pass-2 blocks read before any writes: one GPU batch)."""
+    blocking = Blocking([0, 0, 0], list(SHAPE), BLOCK_SHAPE)
+    lists = vu.make_checkerboard_block_lists(blocking)
+    out = np.zeros(SHAPE, np.uint64)
+    halo = c.get('halo', [0, 0, 0])
+
+    def bbs(bid):
+        if sum(halo) > 0:
+            bh = blocking.getBlockWithHalo(bid, halo)
+            return (vu.block_to_bb(bh.outerBlock), vu.block_to_bb(bh.innerBlock),
+                    vu.block_to_bb(bh.innerBlockLocal))
+        ib = vu.block_to_bb(blocking.getBlock(bid))
+        return ib, ib, tuple(slice(0, s.stop - s.start) for s in ib)
+
+    for pass_id, blist in enumerate(lists):
+        blocks, obbs = [], []
+        for bid in blist:
+            ib, ob, il = bbs(bid)
+            b = dict(input=x[ib], block_id=bid, inner_begin=[s.start for s in il],
+                     inner_shape=[s.stop - s.start for s in il], crop_relabel=(ob != ib) and pass_id == 0)
+            if mask is not None:
+                b['mask'] = mask[ib]
+            if pass_id == 1:
+                b['initial_seeds'] = out[ib].copy()
+            blocks.append(b)
+            obbs.append(ob)
+        for ob, r in zip(obbs, O.ws_blocks(c, BLOCK_SHAPE, blocks, pass_id=pass_id)):
+            if r['status'] in (0, 2):
+                out[ob] = r['output']
+    return out
+
+
+@pytest.mark.parametrize('name', ['ws_2d', 'ws_3d'])
+def test_two_pass_workflow(tmp_path, name):
+    """test_watershed.py:102-103,121-122 (two_pass=True) with the halo configs, pass 2 on GPU."""
+    from cluster_tools_amd.watershed import WatershedWorkflow
+    from cluster_tools_amd.watershed.two_pass_watershed import TwoPassWatershedLocal
+    cfg_dir, inp, x, c = _setup(tmp_path, name, False)
+    c2 = TwoPassWatershedLocal.default_task_config()
+    c2.update(CONFIGS[name])
+    c2['gpu_batch_blocks'] = 1000  # every block of a pass in one batch
+    with open(os.path.join(cfg_dir, 'two_pass_watershed.config'), 'w') as f:
+        json.dump(c2, f)
+    out = str(tmp_path / 'ws.n5')
+    wf = WatershedWorkflow(input_path=inp, input_key='boundaries', output_path=out, output_key='ws',
+                           config_dir=cfg_dir, tmp_folder=str(tmp_path / 'tmp'), target='local', max_jobs=1,
+                           two_pass=True)
+    assert luigi.build([wf], local_scheduler=True)
+    with vu.file_reader(out, 'r') as f:
+        res = f['ws'][:].astype('uint64')
+    _check_result(res, False)
+    ref = _oracle_two_pass(x, c2, None)
+    vis, vim = vi_scores(res, ref)
+    print('two-pass %s: VI %.2e' % (name, vis + vim))
+    assert vis + vim <= 0.01, (vis, vim)
