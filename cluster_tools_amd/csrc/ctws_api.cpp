@@ -59,9 +59,15 @@ struct Workspace {
     uint64_t* hkey = nullptr;
     uint32_t* hpos = nullptr;
     uint32_t* p2err = nullptr;
+    // frontier bitmaps of the descent flood
+    int64_t cap_front = 0;
+    uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
+    uint32_t* fflags = nullptr;
 };
 
-constexpr int kMaxTaps = 127;  // radius <= 63
+constexpr int kCounterBytes = 4 * (4 + 4 * kStatSlots);  // flood flag + statistics slots
+constexpr int kFrontierBatch = 8;        // frontier iterations per host check
+constexpr int kFrontierMaxIters = 256;   // then the tile flood takes over
 
 }  // namespace
 
@@ -80,7 +86,9 @@ struct ctws_handle {
     DevBuf st_in, st_mask, st_init, st_out;
     // test hooks
     int stop_after = 0;
-    int trace = 0;  // CTWS_TRACE=1: per-round flood statistics on stderr
+    int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
+    int no_descent = 0;  // CTWS_NO_DESCENT=1: flood from the seeds alone (test hook)
+    int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     std::vector<BlockDesc> last_desc;
     // RCCL
     ncclComm_t comm = nullptr;
@@ -137,7 +145,7 @@ int grow(ctws_handle* h, DevBuf& b, size_t bytes) {
 }
 
 int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks, int64_t slices, int64_t tiles,
-                     int64_t blocks, int64_t hash) {
+                     int64_t blocks, int64_t hash, int64_t front) {
     Workspace& w = h->ws;
     int r = CTWS_OK;
 #define ALLOC(field, n) \
@@ -193,7 +201,14 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         w.cap_hash = hash;
     }
     if (!w.p2err) ALLOC(p2err, 4);
-    if (!w.counter) ALLOC(counter, 4);
+    if (front > w.cap_front) {
+        ALLOC(front0, front);
+        ALLOC(front1, front);
+        ALLOC(fopen, front);
+        w.cap_front = front;
+    }
+    if (!w.fflags) ALLOC(fflags, kFrontierBatch);
+    if (!w.counter) ALLOC(counter, kCounterBytes / 4);
     if (!w.taps) ALLOC(taps, 6 * 128);
 #undef ALLOC
     return CTWS_OK;
@@ -382,7 +397,7 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
     dim3 g((unsigned)max_tiles, nb);
     int round = 0;
     for (; round < 1000000; ++round) {
-        HIPCHK(hipMemsetAsync(w.counter, 0, 16, h->stream));
+        HIPCHK(hipMemsetAsync(w.counter, 0, kCounterBytes, h->stream));
         hipEventRecord(h->fev[0], h->stream);
         if (packed && nd == 3)
             k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.cls, cur, nxt, lcur, lnxt,
@@ -396,8 +411,13 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
             k_flood<2><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         LAUNCHCHK();
         hipEventRecord(h->fev[1], h->stream);
-        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 16, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, kCounterBytes, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
+        for (int k = 1; k < 4; ++k) {
+            uint32_t t = 0;
+            for (int sl = 0; sl < kStatSlots; ++sl) t += h->h_counter[4 + sl * 4 + k];
+            h->h_counter[k] = t;
+        }
         float ms = 0.f;
         hipEventElapsedTime(&ms, h->fev[0], h->fev[1]);
         kms += ms;
@@ -427,8 +447,8 @@ int64_t chunks_of(int64_t n) { return (words_of(n) + 255) / 256; }
 int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* blocks, const BlockIO* io, int nb) {
     Workspace& w = h->ws;
     std::vector<BlockDesc> desc(nb);
-    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0, TH = 0;
-    int64_t maxH = 0;
+    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0, TH = 0, TF = 0;
+    int64_t maxH = 0, maxRows = 0, maxIRows = 0;
     int maxZ = 0, maxY = 0, maxX = 0, max_tiles = 0;
     int64_t maxN = 0, maxNI = 0;
     const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
@@ -490,6 +510,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
                             (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
+        d.fbase = TF;
+        TF += (int64_t)d.Z * d.Y * ((d.X + 63) / 64);
         T += d.N;
         TI += d.NI;
         TW += words_of(d.N);
@@ -501,6 +523,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         maxN = std::max(maxN, d.N);
         maxNI = std::max(maxNI, d.NI);
         maxH = std::max(maxH, d.hcap);
+        maxRows = std::max(maxRows, (int64_t)d.Z * d.Y);
+        maxIRows = std::max(maxIRows, (int64_t)d.IZ * d.IY);
         // validation against what the kernels assume
         if (d.X > 1024 || d.Y > 2048 || d.Z > 2048 || d.N >= (1ll << 31)) {
             h->err = "outer block too large for the kernels (X <= 1024, Y, Z <= 2048, N < 2^31)";
@@ -562,7 +586,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     const int64_t TT_wide = TT;
     set_tiles(true);
     int r;
-    if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb, TH)) != CTWS_OK) return r;
+    if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb, TH, TF)) != CTWS_OK) return r;
     HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
     h->last_desc = desc;
     std::vector<BlockStat> st(nb);
@@ -580,6 +604,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     const dim3 vg((unsigned)std::min<int64_t>((maxN + 255) / 256, 4096), nb);
     const dim3 ig((unsigned)std::min<int64_t>((maxNI + 255) / 256, 4096), nb);
     const dim3 wg((unsigned)((words_of(maxN) + 255) / 256), nb);
+    // row-tile kernels: kRows rows (z, y) per workgroup iteration
+    const dim3 rg((unsigned)std::min<int64_t>((maxRows + kRows - 1) / kRows, 16384), nb);
+    const dim3 rig((unsigned)std::min<int64_t>((maxIRows + kRows - 1) / kRows, 16384), nb);
     size_t ev = 0;
     h->timings.clear();
     std::vector<const char*> names;
@@ -664,17 +691,20 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     mark("hmap");
 
     // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
-    k_localmax<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls);
+    k_localmax<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls);
     LAUNCHCHK();
     k_plateau_init<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
     k_plateau_union<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
     k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
-    k_seed_init<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF);
-    k_seed_union<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF);
+    k_seed_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF);
+    k_seed_union<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF);
     k_flatten<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF);
-    k_bitmap<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.csum);
+    HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+    k_roots_bitmap<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
+    k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
+    k_root_label<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.Wp);
     const dim3 gsb((unsigned)((maxZ + 255) / 256), nb);
     if (pl.pass2) {
         // _apply_watershed_with_seeds: shifted seeds + initial seeds, relabelConsecutive
@@ -682,12 +712,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         HIPCHK(hipMemsetAsync(w.hkey, 0xFF, sizeof(uint64_t) * (size_t)TH, h->stream));
         HIPCHK(hipMemsetAsync(w.hpos, 0xFF, sizeof(uint32_t) * (size_t)TH, h->stream));
         HIPCHK(hipMemsetAsync(w.p2err, 0, sizeof(uint32_t) * 4, h->stream));
-        k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.sb, w.key);
+        k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.sb, w.key);
         k_p2_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.hkey, w.hpos, w.p2err);
-        HIPCHK(hipMemsetAsync(w.P, 0xFF, sizeof(uint32_t) * (size_t)T, h->stream));
+        HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
         const dim3 hg((unsigned)std::min<int64_t>((maxH + 255) / 256, 4096), nb);
-        k_p2_roots<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.P);
-        k_bitmap<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.P, w.W, w.csum);
+        k_p2_roots<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W);
+        k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
         k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
         k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
         LAUNCHCHK();
@@ -715,8 +745,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_p2_excl_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, excl);
         k_p2_excl<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, excl);
     } else {
-        k_seed_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
-                                                packed ? 1 : 0);
+        k_seed_label<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.hm, w.lab, w.key, w.cls, packed ? 1 : 0);
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
     }
     LAUNCHCHK();
@@ -730,7 +759,88 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int rounds1 = 0, rounds2 = 0;
     h->flood_tiles = h->flood_iters = h->flood_lines = 0;
     float fk1 = 0.f, fk2 = 0.f;
-    if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK) return r;
+    int jumps = 0, fallback = 0, fiters = 0;
+    if (packed && !h->no_descent) {
+        // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
+        if (pl.nd_ws == 3) k_descent_parent<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P);
+        else k_descent_parent<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P);
+        LAUNCHCHK();
+        mark("descent_parent");
+        for (jumps = 1; jumps <= 64; ++jumps) {
+            HIPCHK(hipMemsetAsync(w.counter, 0, 4, h->stream));
+            k_descent_jump<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.P, w.counter);
+            LAUNCHCHK();
+            HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 4, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            if (!h->h_counter[0]) break;
+        }
+        mark("descent_jump");
+        int TZ, TY, TX;
+        flood_tile_dims(pl.nd_ws, true, &TZ, &TY, &TX);
+        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+        k_descent_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P, w.key, w.cls, w.fopen, w.front0);
+        LAUNCHCHK();
+        mark("flood_descent");
+        // frontier relaxation of the remaining voxels (k_frontier, one voxel per lane)
+        uint64_t* fcur = w.front0;
+        uint64_t* fnext = w.front1;
+        const dim3 fg((unsigned)std::min<int64_t>((TF / nb + 64 * 4 - 1) / (64 * 4) + 1, 2048), nb);
+        bool converged = false;
+        for (fiters = 0; fiters < kFrontierMaxIters && !converged;) {
+            HIPCHK(hipMemsetAsync(w.fflags, 0, sizeof(uint32_t) * kFrontierBatch, h->stream));
+            for (int k = 0; k < kFrontierBatch; ++k) {
+                if (pl.nd_ws == 3)
+                    k_frontier<3><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext,
+                                                             w.fflags + k);
+                else
+                    k_frontier<2><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext,
+                                                             w.fflags + k);
+                std::swap(fcur, fnext);
+            }
+            LAUNCHCHK();
+            HIPCHK(hipMemcpyAsync(h->h_counter, w.fflags, sizeof(uint32_t) * kFrontierBatch, hipMemcpyDeviceToHost,
+                                  h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            for (int k = 0; k < kFrontierBatch; ++k) {
+                ++fiters;
+                if (!h->h_counter[k]) {
+                    converged = true;
+                    break;
+                }
+            }
+        }
+        if (!converged) {
+            // long paths (e.g. large exact plateaus): finish with the tile flood from here
+            HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+            k_frontier_tiles<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, w.act0, TZ, TY, TX);
+            LAUNCHCHK();
+            if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds1, &fk1)) != CTWS_OK)
+                return r;
+        }
+        mark("flood_relax");
+        // fixpoint check (exact height ties can break the descent argument): else flood again
+        HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
+        if (pl.nd_ws == 3) k_flood_verify<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, w.counter);
+        else k_flood_verify<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, w.counter);
+        LAUNCHCHK();
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        if (h->trace && h->h_counter[0]) {
+            fprintf(stderr, "[ctws] flood verify: violations at");
+            for (uint32_t k = 0; k < std::min(8u, h->h_counter[1]); ++k) fprintf(stderr, " %u", h->h_counter[2 + k]);
+            fprintf(stderr, "\n");
+        }
+        if (h->h_counter[0] && !h->no_fallback) {
+            fallback = 1;
+            k_flood_reset<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.key, w.cls);
+            LAUNCHCHK();
+            if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK)
+                return r;
+        }
+    } else {
+        mark("flood_descent");
+        if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK) return r;
+    }
     if (packed) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     mark("flood");
     if (h->stop_after == CTWS_STOP_FLOOD) {
@@ -789,16 +899,19 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     for (int i = 0; i < nb; ++i) any_crop |= desc[i].crop != 0;
     if (any_crop) {
         const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
-        k_crop_init<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
-        k_crop_union<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
+        k_crop_init<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
+        k_crop_union<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
         k_flatten<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF);
-        k_bitmap<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.csum);
+        HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+        k_roots_bitmap<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
+        k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
         k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
         k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
+        k_root_label<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp);
         LAUNCHCHK();
     }
     mark("crop_cc");
-    k_output<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF, w.W, w.Wp);
+    k_output<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
     LAUNCHCHK();
     mark("output");
     }
@@ -834,6 +947,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         h->timings.push_back({names[i], ms});
     }
     h->timings.push_back({"flood_rounds", (float)rounds1});
+    h->timings.push_back({"descent_jumps", (float)jumps});
+    h->timings.push_back({"frontier_iters", (float)fiters});
+    h->timings.push_back({"flood_fallback", (float)fallback});
     h->timings.push_back({"regrow_rounds", (float)rounds2});
     h->timings.push_back({"flood_kernel_ms", fk1});
     h->timings.push_back({"flood_packed", packed ? 1.f : 0.f});
@@ -1009,8 +1125,10 @@ int ctws_open(int device, ctws_handle** out) {
     ctws_handle* h = new ctws_handle();
     h->device = device;
     if (const char* t = std::getenv("CTWS_TRACE")) h->trace = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_NO_DESCENT")) h->no_descent = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_counter, 16, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * 128 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
         delete h;
         return CTWS_EHIP;

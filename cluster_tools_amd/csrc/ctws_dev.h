@@ -15,6 +15,8 @@ constexpr uint32_t kInfD2 = 0x3FFFFFFFu;             // "no foreground" squared 
 constexpr uint64_t kInfKey = 0xFFFFFFFFFFFFFFFFull;  // flood key of an unreached voxel
 constexpr uint32_t kNoParent = 0xFFFFFFFFu;          // union-find: background
 constexpr uint32_t kFixedBit = 0x80000000u;          // flood label: voxel is a seed
+constexpr uint32_t kRootBit = 0x80000000u;           // CC parent slot of a labelled root
+constexpr int kRows = 4;                             // rows per workgroup iteration (row tiles)
 
 struct BlockDesc {
     int Z, Y, X, nd_ws;     // outer shape; nd_ws = 2 (per-slice ws) or 3
@@ -38,6 +40,7 @@ struct BlockDesc {
     uint32_t pass2;         // 1: _ws_pass2 (two_pass_watershed.py:210-255)
     int64_t hbase;          // pass 2: offset into the relabel hash arrays
     int64_t hcap;           // pass 2: hash capacity of this block (power of two)
+    int64_t fbase;          // offset into the frontier bitmaps (Z*Y rows of ceil(X/64) words)
 };
 
 struct BlockStat {
@@ -102,6 +105,62 @@ __device__ __forceinline__ void uf_union(uint32_t* P, uint32_t a, uint32_t b) {
         if (old == b) return;
         b = old;
     }
+}
+
+// label of a CC member from its parent slot p = P[i] after k_root_label (0: background)
+__device__ __forceinline__ uint32_t cc_label(const uint32_t* P, uint32_t p) {
+    if (p == kNoParent) return 0u;
+    if (p & kRootBit) return p & ~kRootBit;
+    return P[p] & ~kRootBit;
+}
+
+// ---- contention-free updates of per-block / per-slice scalars ------------------------------
+// Same-address atomics serialise (~3 ns each): one per wave on a batch-wide scalar costs more
+// than the streaming pass itself.  Reduce over the workgroup first (every thread must call),
+// then one lane updates, and only when the (possibly stale, monotone) value does not cover it.
+template <class Op>
+__device__ __forceinline__ uint32_t wg_reduce_u32(uint32_t v, Op op) {
+    for (int s = 32; s > 0; s >>= 1) v = op(v, (uint32_t)__shfl_xor((int)v, s));
+    __shared__ uint32_t red[16];
+    const int nw = (int)((blockDim.x + 63) >> 6);
+    __syncthreads();  // red[] may still be read by a previous reduction
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    v = red[0];
+    for (int k = 1; k < nw; ++k) v = op(v, red[k]);
+    return v;
+}
+struct OpMax {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+struct OpMin {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; }
+};
+struct OpAdd {
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+__device__ __forceinline__ void atomic_max_if(uint32_t* p, uint32_t v) {
+    if (v > *(volatile uint32_t*)p) atomicMax(p, v);
+}
+__device__ __forceinline__ void atomic_min_if(uint32_t* p, uint32_t v) {
+    if (v < *(volatile uint32_t*)p) atomicMin(p, v);
+}
+
+// Strided staging loop with U independent loads in flight: for p in [begin, end) step
+// `step`, st(p, ld(p)).  A plain loop issues one load, waits for it and stores it (one
+// memory latency per element); here the U loads of a batch are issued back to back.
+template <int U, class LoadF, class StoreF>
+__device__ __forceinline__ void staged_loop(int begin, int end, int step, LoadF ld, StoreF st) {
+    using T = decltype(ld(0));
+    int p = begin;
+    for (; p + (U - 1) * step < end; p += U * step) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld(p + u * step);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st(p + u * step, v[u]);
+    }
+    for (; p < end; p += step) st(p, ld(p));
 }
 
 // rank of key f among set bits of a per-block bitmap with per-word exclusive prefix

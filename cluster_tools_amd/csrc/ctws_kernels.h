@@ -59,15 +59,16 @@ __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uin
 __global__ void k_seed_init(const BlockDesc*, const BlockStat*, const uint8_t*, const uint32_t*, uint32_t*);
 __global__ void k_seed_union(const BlockDesc*, const BlockStat*, uint32_t*);
 __global__ void k_flatten(const BlockDesc*, const BlockStat*, int, uint32_t*);
-__global__ void k_bitmap(const BlockDesc*, const BlockStat*, int, const uint32_t*, uint64_t*, uint32_t*);
+__global__ void k_roots_bitmap(const BlockDesc*, const BlockStat*, int, const uint32_t*, uint64_t*);
+__global__ void k_bitmap_csum(const BlockDesc*, const BlockStat*, int, const uint64_t*, uint32_t*);
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
 __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uint64_t*, const uint32_t*, uint32_t*);
-__global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
-                             const float*, uint32_t*, uint64_t*, uint8_t*, int);
+__global__ void k_root_label(const BlockDesc*, const BlockStat*, int, uint32_t*, const uint64_t*, const uint32_t*);
+__global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const float*, uint32_t*, uint64_t*,
+                             uint8_t*, int);
 __global__ void k_crop_init(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_crop_union(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
-__global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*, const uint64_t*,
-                         const uint32_t*);
+__global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*);
 
 // k_flood.hip
 template <int ND>
@@ -77,8 +78,22 @@ __global__ void k_flood(const BlockDesc*, const BlockStat*, const float*, uint64
 template <int ND>
 __global__ void k_flood_packed(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint8_t*,
                                const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
-constexpr int kLineWords = 24;  // per tile: 8 words of line bits for each of x, y, z
+constexpr int kLineWords = 24;
+constexpr int kStatSlots = 64;  // flood statistics: counter[4 + slot * 4 + k]  // per tile: 8 words of line bits for each of x, y, z
 __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
+template <int ND>
+__global__ void k_descent_parent(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint32_t*);
+__global__ void k_descent_jump(const BlockDesc*, const BlockStat*, uint32_t*, uint32_t*);
+__global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
+                               uint64_t*, uint8_t*, uint64_t*, uint64_t*);
+template <int ND>
+__global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
+                           const uint64_t*, uint64_t*, uint32_t*);
+__global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
+template <int ND>
+__global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint32_t*,
+                               uint32_t*);
+__global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint8_t*);
 
 // k_post.hip
 __global__ void k_slice_seed_base(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
@@ -92,10 +107,9 @@ __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t
 
 // k_pass2.hip (two-pass watershed, pass 2)
 __global__ void k_p2_zero_dt(const BlockDesc*, const BlockStat*, float*);
-__global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
-                            const uint32_t*, uint64_t*);
+__global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint64_t*);
 __global__ void k_p2_insert(const BlockDesc*, const BlockStat*, const uint64_t*, uint64_t*, uint32_t*, uint32_t*);
-__global__ void k_p2_roots(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
+__global__ void k_p2_roots(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint64_t*);
 __global__ void k_p2_label(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, const uint64_t*,
                            const uint32_t*, const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, uint32_t*, int);
 __global__ void k_p2_excl_zero(const BlockDesc*, const BlockStat*, uint8_t*);

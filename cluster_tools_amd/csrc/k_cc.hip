@@ -5,12 +5,18 @@
 // labelVolumeWithBackground, uint64 id offset), :310-321 (empty block).
 //
 // Numbering.  vigra numbers components 1..k by their first voxel in vigra scan order,
-// which for a plain numpy array is the F-order index (axis 0 fastest).  The union-find
-// parent arrays here are therefore keyed by the F-order key
-//     3-D: f = z + Z*(y + Y*x)        2-D (per slice): f = z*Y*X + (y + Y*x)
-// and union links the larger root under the smaller, so every root is its component's
-// first voxel.  The label of a root is 1 + (number of roots with a smaller key), read from
-// a per-block bitmap of roots (1 bit per key) and its per-word exclusive prefix.
+// which for a plain numpy array is the F-order index (axis 0 fastest), the *scan key*
+//     3-D: f = z + Z*(y + Y*x)        2-D (per slice): f = z*Y*X + (y + Y*x).
+// Union-find parents are indexed by the C-order voxel index (so every pass is coalesced),
+// and a union links the root with the larger scan key under the one with the smaller, so
+// every root is its component's first voxel in scan order.  Roots set their scan-key bit in
+// a per-block bitmap; the label of a root is 1 + (number of roots with a smaller key), from
+// the bitmap's per-word exclusive prefix.  After k_root_label every root slot holds
+// (label | kRootBit) and every other member points straight at its root.
+//
+// Voxel passes walk row tiles: a workgroup iteration covers kRows consecutive rows (z, y)
+// and each thread an x column, so coordinates need no divisions and the loads of the rows
+// are independent (issued together).
 #include "ctws_kernels.h"
 
 namespace ctws {
@@ -19,6 +25,58 @@ namespace ctws {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (B).N;              \
          i += (int64_t)gridDim.x * blockDim.x)
 
+// row-tile traversal of an (nz, ny, nx) C-order volume; BODY sees z, y, x, i (local index)
+#define ROW_TILES(nz, ny, nx, ...)                                                           \
+    {                                                                                         \
+        const int64_t nrows_ = (int64_t)(nz) * (ny);                                          \
+        for (int64_t r0_ = (int64_t)blockIdx.x * kRows; r0_ < nrows_; r0_ += (int64_t)gridDim.x * kRows) \
+            for (int x = threadIdx.x; x < (nx); x += blockDim.x) {                           \
+                _Pragma("unroll") for (int rr_ = 0; rr_ < kRows; ++rr_) {                      \
+                    const int64_t row_ = r0_ + rr_;                                           \
+                    if (row_ >= nrows_) break;                                                \
+                    const int z = (int)(row_ / (ny));                                         \
+                    const int y = (int)(row_ - (int64_t)z * (ny));                            \
+                    const int64_t i = row_ * (nx) + x;                                        \
+                    (void)z;                                                                  \
+                    (void)y;                                                                  \
+                    __VA_ARGS__                                                               \
+                }                                                                             \
+            }                                                                                 \
+    }
+
+__device__ __forceinline__ uint32_t scan_key_of(const BlockDesc& B, int z, int y, int x) {
+    return (B.nd_ws == 3) ? (uint32_t)(z + B.Z * (y + B.Y * x))
+                          : (uint32_t)((int64_t)z * B.Y * B.X + y + (int64_t)B.Y * x);
+}
+// scan key of a C-order index (outer block, or the inner block when inner != 0)
+__device__ __forceinline__ uint32_t scan_key_idx(const BlockDesc& B, int inner, uint32_t c) {
+    const int Y = inner ? B.IY : B.Y, X = inner ? B.IX : B.X;
+    const uint32_t yx = (uint32_t)Y * (uint32_t)X;
+    const int z = (int)(c / yx);
+    const uint32_t rem = c - (uint32_t)z * yx;
+    const int y = (int)(rem / (uint32_t)X);
+    const int x = (int)(rem - (uint32_t)y * (uint32_t)X);
+    if (inner) return (uint32_t)(z + B.IZ * (y + B.IY * x));
+    return scan_key_of(B, z, y, x);
+}
+
+// union by scan key: the root with the smaller key becomes the parent
+__device__ __forceinline__ void uf_union_scan(uint32_t* P, uint32_t a, uint32_t b, const BlockDesc& B, int inner) {
+    while (true) {
+        a = uf_find(P, a);
+        b = uf_find(P, b);
+        if (a == b) return;
+        if (scan_key_idx(B, inner, a) > scan_key_idx(B, inner, b)) {
+            const uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        const uint32_t old = atomicCAS(&P[b], b, a);
+        if (old == b) return;
+        b = old;
+    }
+}
+
 // ---- local maxima classification ---------------------------------------------------------
 // cls bit0: a neighbour is strictly greater; bit1: a neighbour is equal (plateau voxel).
 // Neighbourhood: 6 (3-D ws) or 8 in-plane (2-D ws), as localMaxima3D / localMaxima.
@@ -26,41 +84,44 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
                                                   const float* __restrict__ v, uint8_t* __restrict__ cls) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const int Y = B.Y, X = B.X;
+    const int Y = B.Y, X = B.X, Z = B.Z;
     const int64_t YX = (int64_t)Y * X;
-    const float* p = v + B.base;
+    const float* __restrict__ p = v + B.base;
+    uint8_t* __restrict__ cl = cls + B.base;
     uint32_t nplat = 0;
-    BLOCK_LOOP(i, B) {
-        const int z = (int)(i / YX);
-        const int rem = (int)(i - z * YX);
-        const int y = rem / X, x = rem - (rem / X) * X;
+    const float NEG = -__builtin_huge_valf();
+    ROW_TILES(Z, Y, X, {
         const float c = p[i];
-        bool gt = false, eq = false;
-        auto chk = [&](int64_t j) {
-            const float w = p[j];
-            gt |= w > c;
-            eq |= w == c;
-        };
+        float w[8];
         if (B.nd_ws == 3) {
-            if (z > 0) chk(i - YX);
-            if (z + 1 < B.Z) chk(i + YX);
-            if (y > 0) chk(i - X);
-            if (y + 1 < Y) chk(i + X);
-            if (x > 0) chk(i - 1);
-            if (x + 1 < X) chk(i + 1);
+            w[0] = z > 0 ? p[i - YX] : NEG;
+            w[1] = z + 1 < Z ? p[i + YX] : NEG;
+            w[2] = y > 0 ? p[i - X] : NEG;
+            w[3] = y + 1 < Y ? p[i + X] : NEG;
+            w[4] = x > 0 ? p[i - 1] : NEG;
+            w[5] = x + 1 < X ? p[i + 1] : NEG;
+            w[6] = w[7] = NEG;
         } else {
-            for (int dy = -1; dy <= 1; ++dy)
-                for (int dx = -1; dx <= 1; ++dx) {
-                    if (!dy && !dx) continue;
-                    const int yy = y + dy, xx = x + dx;
-                    if (yy < 0 || yy >= Y || xx < 0 || xx >= X) continue;
-                    chk(i + dy * X + dx);
-                }
+            const bool yl = y > 0, yh = y + 1 < Y, xl = x > 0, xh = x + 1 < X;
+            w[0] = yl && xl ? p[i - X - 1] : NEG;
+            w[1] = yl ? p[i - X] : NEG;
+            w[2] = yl && xh ? p[i - X + 1] : NEG;
+            w[3] = xl ? p[i - 1] : NEG;
+            w[4] = xh ? p[i + 1] : NEG;
+            w[5] = yh && xl ? p[i + X - 1] : NEG;
+            w[6] = yh ? p[i + X] : NEG;
+            w[7] = yh && xh ? p[i + X + 1] : NEG;
         }
-        cls[B.base + i] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
+        bool gt = false, eq = false;
+        _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+            gt |= w[k] > c;
+            eq |= w[k] == c;
+        }
+        cl[i] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
         nplat += eq;
-    }
-    if (nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
+    })
+    nplat = wg_reduce_u32(nplat, OpAdd());
+    if (threadIdx.x == 0 && nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
 }
 
 // ---- plateau resolution: CC of equal values over plateau voxels (C-order keys) -----------
@@ -131,83 +192,73 @@ __device__ __forceinline__ bool is_max(const uint8_t* cl, const uint32_t* P, int
     return !(cl[uf_find(P, (uint32_t)i)] & 4);
 }
 
-// F-order key helpers
-__device__ __forceinline__ uint32_t fkey3(int z, int y, int x, int Z, int Y) {
-    return (uint32_t)(z + Z * (y + Y * x));
-}
-
 // ---- seed CC: init / union over maxima voxels (direct nbhd; in-plane in 2-D) -------------
-// PF is keyed by F-order key.  Background keys get kNoParent so the bitmap sees no root.
+// PF (C-order index) = self for maxima voxels, kNoParent for the background.
 __global__ void __launch_bounds__(256) k_seed_init(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                    const uint8_t* __restrict__ cls, const uint32_t* __restrict__ Pp,
                                                    uint32_t* __restrict__ PF) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const int Y = B.Y, X = B.X, Z = B.Z;
-    const int64_t YX = (int64_t)Y * X;
     const uint8_t* cl = cls + B.base;
     const uint32_t* P = Pp + B.base;
-    BLOCK_LOOP(i, B) {
-        const int z = (int)(i / YX);
-        const int rem = (int)(i - z * YX);
-        const int y = rem / X, x = rem - (rem / X) * X;
-        const uint32_t f = (B.nd_ws == 3) ? fkey3(z, y, x, Z, Y) : (uint32_t)(z * YX + y + Y * x);
-        PF[B.base + f] = is_max(cl, P, i) ? f : kNoParent;
-    }
+    uint32_t* F = PF + B.base;
+    const bool plat = S[blockIdx.y].plateau != 0;
+    ROW_TILES(B.Z, B.Y, B.X, {
+        const uint8_t c = cl[i];
+        bool m = !(c & 1);
+        if (m && (c & 2) && plat) m = is_max(cl, P, i);
+        F[i] = m ? (uint32_t)i : kNoParent;
+    })
 }
 
 __global__ void __launch_bounds__(256) k_seed_union(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                     uint32_t* __restrict__ PFg) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const int Y = B.Y, X = B.X, Z = B.Z;
-    const int64_t YX = (int64_t)Y * X;
-    uint32_t* PF = PFg + B.base;
-    BLOCK_LOOP(i, B) {
-        const int z = (int)(i / YX);
-        const int rem = (int)(i - z * YX);
-        const int y = rem / X, x = rem - (rem / X) * X;
-        if (B.nd_ws == 3) {
-            const uint32_t f = fkey3(z, y, x, Z, Y);
-            if (PF[f] == kNoParent) continue;
-            if (z > 0 && PF[f - 1] != kNoParent) uf_union(PF, f, f - 1);
-            if (y > 0 && PF[f - Z] != kNoParent) uf_union(PF, f, f - Z);
-            if (x > 0 && PF[f - Z * Y] != kNoParent) uf_union(PF, f, f - (uint32_t)(Z * Y));
-        } else {
-            const uint32_t f = (uint32_t)(z * YX + y + Y * x);
-            if (PF[f] == kNoParent) continue;
-            if (y > 0 && PF[f - 1] != kNoParent) uf_union(PF, f, f - 1);
-            if (x > 0 && PF[f - Y] != kNoParent) uf_union(PF, f, f - Y);
+    const int64_t YX = (int64_t)B.Y * B.X;
+    uint32_t* P = PFg + B.base;
+    ROW_TILES(B.Z, B.Y, B.X, {
+        if (P[i] != kNoParent) {
+            const uint32_t u = (uint32_t)i;
+            if (B.nd_ws == 3 && z > 0 && P[i - YX] != kNoParent) uf_union_scan(P, u, (uint32_t)(i - YX), B, 0);
+            if (y > 0 && P[i - B.X] != kNoParent) uf_union_scan(P, u, (uint32_t)(i - B.X), B, 0);
+            if (x > 0 && P[i - 1] != kNoParent) uf_union_scan(P, u, u - 1, B, 0);
         }
-    }
+    })
 }
 
 // ---- root bitmap + exclusive prefix -----------------------------------------------------
 // keys per block: n = N (seeds, outer) or NI (crop, inner); words = n/64 + 1, chunks of 256
-// words.  inner != 0 selects NI and the inner-sized parent array offset (ibase).
-__global__ void __launch_bounds__(256) k_bitmap(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
-                                                const uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg,
-                                                uint32_t* __restrict__ csum) {
+// words.  inner != 0 selects NI and the inner-sized parent array offset (ibase).  W must be
+// zeroed beforehand.
+__global__ void __launch_bounds__(256) k_roots_bitmap(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
+                                                      const uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active || (inner && !B.crop)) return;
+    const uint32_t* P = PFg + (inner ? B.ibase : B.base);
+    uint64_t* W = Wg + B.wbase;
+    const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
+    ROW_TILES(nz, ny, nx, {
+        if (P[i] == (uint32_t)i) {
+            const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
+            atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
+        }
+    })
+}
+
+// popcount sums of 256-word chunks
+__global__ void __launch_bounds__(256) k_bitmap_csum(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
+                                                     const uint64_t* __restrict__ Wg, uint32_t* __restrict__ csum) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || (inner && !B.crop)) return;
     const int64_t n = inner ? B.NI : B.N;
     const int64_t nw = n / 64 + 1;
     if ((int64_t)blockIdx.x * 256 >= nw) return;
-    const uint32_t* PF = PFg + (inner ? B.ibase : B.base);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // each wave builds 64 words; one word = ballot over 64 consecutive keys (coalesced)
-    uint32_t c = 0;
-    for (int j = 0; j < 64; ++j) {
-        const int64_t w = (int64_t)blockIdx.x * 256 + wv * 64 + j;
-        if (w >= nw) break;
-        const int64_t f = w * 64 + lane;
-        const bool root = f < n && PF[f] == (uint32_t)f;
-        const uint64_t bits = __ballot(root);
-        if (lane == 0) Wg[B.wbase + w] = bits;
-        c += (uint32_t)__popcll(bits);
-    }
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t c = w < nw ? (uint32_t)__popcll(Wg[B.wbase + w]) : 0u;
+    for (int s = 32; s > 0; s >>= 1) c += (uint32_t)__shfl_xor((int)c, s);
     __shared__ uint32_t red[4];
-    if (lane == 0) red[wv] = c;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) csum[B.cbase + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
@@ -269,130 +320,109 @@ __global__ void __launch_bounds__(256) k_word_prefix(const BlockDesc* __restrict
     if (w < nw) Wp[B.wbase + w] = csum[B.cbase + blockIdx.x] + woff + x - v;
 }
 
+// roots: slot <- (1 + rank of the root's scan key) | kRootBit (after k_flatten)
+__global__ void __launch_bounds__(256) k_root_label(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
+                                                    uint32_t* __restrict__ PFg, const uint64_t* __restrict__ Wg,
+                                                    const uint32_t* __restrict__ Wpg) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active || (inner && !B.crop)) return;
+    uint32_t* P = PFg + (inner ? B.ibase : B.base);
+    const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
+    ROW_TILES(nz, ny, nx, {
+        if (P[i] == (uint32_t)i) {
+            const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
+            P[i] = (bitmap_rank(Wg + B.wbase, Wpg + B.wbase, f) + 1u) | kRootBit;
+        }
+    })
+}
+
 // ---- seed labels + flood initialisation --------------------------------------------------
 // labels = vigra label (| kFixedBit: seed), keys = (ordf(h) << 32) for seeds, INF otherwise.
 __global__ void __launch_bounds__(256) k_seed_label(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                    const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ Wg,
-                                                    const uint32_t* __restrict__ Wpg, const float* __restrict__ h,
+                                                    const uint32_t* __restrict__ PFg, const float* __restrict__ h,
                                                     uint32_t* __restrict__ lab, uint64_t* __restrict__ key,
                                                     uint8_t* __restrict__ fixedv, int packed) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const int Y = B.Y, X = B.X, Z = B.Z;
-    const int64_t YX = (int64_t)Y * X;
-    const uint32_t* PF = PFg + B.base;
-    const uint64_t* W = Wg + B.wbase;
-    const uint32_t* Wp = Wpg + B.wbase;
-    BLOCK_LOOP(i, B) {
-        const int z = (int)(i / YX);
-        const int rem = (int)(i - z * YX);
-        const int y = rem / X, x = rem - (rem / X) * X;
-        const uint32_t f = (B.nd_ws == 3) ? fkey3(z, y, x, Z, Y) : (uint32_t)(z * YX + y + Y * x);
-        uint32_t l = 0;
+    const uint32_t* P = PFg + B.base;
+    ROW_TILES(B.Z, B.Y, B.X, {
+        const int64_t gi = B.base + i;
+        const uint32_t l = cc_label(P, P[i]);
         uint64_t k = kInfKey;
-        if (PF[f] != kNoParent) {
-            const uint32_t r = uf_find(PF, f);
-            const uint32_t lr = bitmap_rank(W, Wp, r) + 1u;
-            l = lr | kFixedBit;
-            k = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)lr : 0ull);
-        }
-        lab[B.base + i] = l;
-        key[B.base + i] = k;
-        fixedv[B.base + i] = l ? 1 : 0;
-    }
+        if (l) k = ((uint64_t)ordf(h[gi]) << 32) | (packed ? (uint64_t)l : 0ull);
+        lab[gi] = l ? (l | kFixedBit) : 0u;
+        key[gi] = k;
+        fixedv[gi] = l ? 1 : 0;
+    })
 }
 
 // ---- halo crop CC (labelVolumeWithBackground, 6-nbhd, equal values, bg 0) -----------------
-__device__ __forceinline__ void inner_coords(const BlockDesc& B, int64_t i, int& z, int& y, int& x) {
-    const int64_t yx = (int64_t)B.IY * B.IX;
-    z = (int)(i / yx);
-    const int rem = (int)(i - z * yx);
-    y = rem / B.IX;
-    x = rem - y * B.IX;
-}
 __device__ __forceinline__ int64_t outer_of_inner(const BlockDesc& B, int z, int y, int x) {
     return ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0);
 }
-
-#define INNER_LOOP(i, B)                                                                      \
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (B).NI;             \
-         i += (int64_t)gridDim.x * blockDim.x)
 
 __global__ void __launch_bounds__(256) k_crop_init(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                    const uint32_t* __restrict__ ws, uint32_t* __restrict__ PFg) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || !B.crop) return;
-    uint32_t* PF = PFg + B.ibase;
-    INNER_LOOP(i, B) {
-        int z, y, x;
-        inner_coords(B, i, z, y, x);
-        const uint32_t f = fkey3(z, y, x, B.IZ, B.IY);
-        PF[f] = ws[B.base + outer_of_inner(B, z, y, x)] ? f : kNoParent;
-    }
+    uint32_t* P = PFg + B.ibase;
+    ROW_TILES(B.IZ, B.IY, B.IX, { P[i] = ws[B.base + outer_of_inner(B, z, y, x)] ? (uint32_t)i : kNoParent; })
 }
 
 __global__ void __launch_bounds__(256) k_crop_union(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                     const uint32_t* __restrict__ ws, uint32_t* __restrict__ PFg) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || !B.crop) return;
-    uint32_t* PF = PFg + B.ibase;
+    uint32_t* P = PFg + B.ibase;
     const uint32_t* w = ws + B.base;
-    INNER_LOOP(i, B) {
-        int z, y, x;
-        inner_coords(B, i, z, y, x);
+    const int64_t oyx = (int64_t)B.Y * B.X, iyx = (int64_t)B.IY * B.IX;
+    ROW_TILES(B.IZ, B.IY, B.IX, {
         const int64_t o = outer_of_inner(B, z, y, x);
         const uint32_t v = w[o];
-        if (!v) continue;
-        const uint32_t f = fkey3(z, y, x, B.IZ, B.IY);
-        if (z > 0 && w[o - (int64_t)B.Y * B.X] == v) uf_union(PF, f, f - 1);
-        if (y > 0 && w[o - B.X] == v) uf_union(PF, f, f - B.IZ);
-        if (x > 0 && w[o - 1] == v) uf_union(PF, f, f - (uint32_t)(B.IZ * B.IY));
-    }
+        if (v) {
+            const uint32_t u = (uint32_t)i;
+            if (z > 0 && w[o - oyx] == v) uf_union_scan(P, u, (uint32_t)(i - iyx), B, 1);
+            if (y > 0 && w[o - B.X] == v) uf_union_scan(P, u, (uint32_t)(i - B.IX), B, 1);
+            if (x > 0 && w[o - 1] == v) uf_union_scan(P, u, u - 1, B, 1);
+        }
+    })
 }
 
 // ---- uint64 output: (crop CC label | ws) + id offset on in-mask voxels ---------------------
 __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D, BlockStat* S,
-                                                const uint32_t* __restrict__ ws, const uint32_t* __restrict__ PFg,
-                                                const uint64_t* __restrict__ Wg, const uint32_t* __restrict__ Wpg) {
+                                                const uint32_t* __restrict__ ws, const uint32_t* __restrict__ PFg) {
     const BlockDesc& B = D[blockIdx.y];
     const bool active = S[blockIdx.y].active;
+    const uint32_t* P = PFg + B.ibase;
+    uint64_t* __restrict__ out = B.out;
     uint32_t mx = 0;
-    INNER_LOOP(i, B) {
-        int z, y, x;
-        inner_coords(B, i, z, y, x);
+    ROW_TILES(B.IZ, B.IY, B.IX, {
         const int64_t o = outer_of_inner(B, z, y, x);
         const bool inm = !B.mask || B.mask[o];
-        uint64_t v;
-        if (!active) {
-            v = 0;  // empty block: constant offset (watershed.py:310-321)
-        } else {
+        uint64_t v = 0;  // empty block: constant offset (watershed.py:310-321)
+        if (active) {
             uint32_t l = ws[B.base + o];
-            if (B.crop && l) {
-                const uint32_t r = uf_find(PFg + B.ibase, fkey3(z, y, x, B.IZ, B.IY));
-                l = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, r) + 1u;
-            }
+            if (B.crop && l) l = cc_label(P, P[i]);
             mx = max(mx, l);
             v = l;
         }
-        B.out[i] = inm ? v + B.id_offset : v;
-    }
-    for (int s = 32; s > 0; s >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, s));
-    if ((threadIdx.x & 63) == 0 && mx) atomicMax(&S[blockIdx.y].max_label, mx);
+        out[i] = inm ? v + B.id_offset : v;
+    })
+    mx = wg_reduce_u32(mx, OpMax());
+    if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);
 }
 
-}  // namespace ctws
-
-namespace ctws {
 // point every element of a union-find forest directly at its root
 __global__ void __launch_bounds__(256) k_flatten(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
                                                  uint32_t* __restrict__ PFg) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || (inner && !B.crop)) return;
     const int64_t n = inner ? B.NI : B.N;
-    uint32_t* PF = PFg + (inner ? B.ibase : B.base);
+    uint32_t* P = PFg + (inner ? B.ibase : B.base);
     for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n; f += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t p = PF[f];
-        if (p != kNoParent && p != (uint32_t)f) PF[f] = uf_find(PF, p);
+        const uint32_t p = P[f];
+        if (p != kNoParent && p != (uint32_t)f) P[f] = uf_find(P, p);
     }
 }
+
 }  // namespace ctws

@@ -44,8 +44,8 @@ __global__ void __launch_bounds__(256) k_input_minmax(const BlockDesc* __restric
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        atomicMin(&S[blockIdx.y].in_min, min(min(rmn[0], rmn[1]), min(rmn[2], rmn[3])));
-        atomicMax(&S[blockIdx.y].in_max, max(max(rmx[0], rmx[1]), max(rmx[2], rmx[3])));
+        atomic_min_if(&S[blockIdx.y].in_min, min(min(rmn[0], rmn[1]), min(rmn[2], rmn[3])));
+        atomic_max_if(&S[blockIdx.y].in_max, max(max(rmx[0], rmx[1]), max(rmx[2], rmx[3])));
     }
 }
 
@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(256) k_prep_edt_x(const BlockDesc* __restrict_
     const float den = unordf(S[blockIdx.y].in_max) - mn;  // max(x - min) == max - min (monotone rounding)
     const int64_t rbase = row * X;
     uint32_t fgcount = 0;
-    for (int x = lane; x < X; x += 64) {
+    auto ld = [&](int x) -> float {
         const int64_t i = rbase + x;
         float v;
         if (B.n_channels == 0) {
@@ -88,13 +88,17 @@ __global__ void __launch_bounds__(256) k_prep_edt_x(const BlockDesc* __restrict_
         }
         if (pp.invert) v = 1.0f - v;
         if (B.mask && !B.mask[i]) v = 1.0f;
-        fin[B.base + i] = v;
+        return v;
+    };
+    staged_loop<8>(lane, X, 64, ld, [&](int x, float v) {
+        fin[B.base + rbase + x] = v;
         const int f = v > pp.threshold;
         sdist[x] = f;
         fgcount += f;
-    }
+    });
     // any foreground in the block? (_apply_dt: np.sum(threshd) == 0 -> None)
-    if (__ballot(fgcount != 0) != 0ull && lane == 0) atomicOr(&S[blockIdx.y].fg, 1u);
+    if (__ballot(fgcount != 0) != 0ull && lane == 0 && !*(volatile uint32_t*)&S[blockIdx.y].fg)
+        atomicOr(&S[blockIdx.y].fg, 1u);
     __builtin_amdgcn_wave_barrier();
     // chunk per lane: [lane*K, lane*K + K)
     const int K = (X + 63) >> 6;
@@ -200,8 +204,12 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
     const int r0 = threadIdx.x / W;
     constexpr int RS = 256 / W;
     const bool colok = xb + c < B.X;
-    for (int p = r0; p < L; p += RS)
-        col[p * W + c] = colok ? gin[B.base + obase + p * lstride + xb + c] : kInfD2;
+    {
+        const uint32_t* gsrc = gin + B.base + obase + xb + (colok ? c : 0);
+        staged_loop<8>(
+            r0, L, RS, [&](int p) { return colok ? gsrc[p * lstride] : kInfD2; },
+            [&](int p, uint32_t v) { col[p * W + c] = v; });
+    }
     __syncthreads();
     uint32_t mn = 0xFFFFFFFFu, mx = 0u;
     const uint32_t maxd = ep.per_slice ? (uint32_t)(B.Y * B.Y + B.X * B.X) : B.maxd;
@@ -244,11 +252,11 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
         if (threadIdx.x == 0) {
             mn = min(min(rmn[0], rmn[1]), min(rmn[2], rmn[3]));
             mx = max(max(rmx[0], rmx[1]), max(rmx[2], rmx[3]));
-            atomicMin(&S[blockIdx.y].dt_min, mn);
-            atomicMax(&S[blockIdx.y].dt_max, mx);
+            atomic_min_if(&S[blockIdx.y].dt_min, mn);
+            atomic_max_if(&S[blockIdx.y].dt_max, mx);
             if (ep.axis == 1) {
-                atomicMin(&slice_min[B.sbase + o], mn);
-                atomicMax(&slice_max[B.sbase + o], mx);
+                atomic_min_if(&slice_min[B.sbase + o], mn);
+                atomic_max_if(&slice_max[B.sbase + o], mx);
             }
         }
     }

@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(256) k_flood(const BlockDesc* __restrict__ D, 
         if (sface[3]) act(tzi, tyi + 1, txi);
         if (sface[4]) act(tzi, tyi, txi - 1);
         if (sface[5]) act(tzi, tyi, txi + 1);
-        if (n) atomicAdd(counter, (uint32_t)n);
+        if (n && !*(volatile uint32_t*)counter) atomicOr(counter, 1u);
     }
 }
 
@@ -492,16 +492,17 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
             const int64_t nt = B.tbase + (zz * B.ty + yy) * B.tx + xx;
             const int axis = f < 2 ? 2 : (f < 4 ? 1 : 0);
             atomicOr(&lines_next[nt * kLineWords + axis * 8 + wd], bits);
-            atomicOr(&act_next[nt], 1u);
-            atomicAdd(counter, 1u);
+            if (!act_next[nt]) atomicOr(&act_next[nt], 1u);
+            if (!*(volatile uint32_t*)counter) atomicOr(counter, 1u);  // another round is needed
         }
     }
-    // lines swept (wave-aggregated)
-    for (int o = 32; o > 0; o >>= 1) nlines += __shfl_xor(nlines, o);
-    if ((tid & 63) == 0) atomicAdd(counter + 3, nlines);
+    // statistics, spread over kStatSlots slots (same-address atomics serialise)
+    nlines = wg_reduce_u32(nlines, OpAdd());
     if (tid == 0) {
-        atomicAdd(counter + 1, 1u);              // tiles solved
-        atomicAdd(counter + 2, (uint32_t)iters);  // sweeps
+        uint32_t* st = counter + 4 + (blockIdx.x % kStatSlots) * 4;
+        atomicAdd(st + 1, 1u);              // tiles solved
+        atomicAdd(st + 2, (uint32_t)iters);  // sweeps
+        atomicAdd(st + 3, nlines);           // lines swept
     }
 }
 
@@ -522,6 +523,320 @@ __global__ void __launch_bounds__(256) k_unpack_labels(const BlockDesc* __restri
         const uint64_t k = key[B.base + i];
         const uint32_t l = (k == kPackInf) ? 0u : (uint32_t)(k & kLabelMask);
         lab[B.base + i] = (lab[B.base + i] & kFixedBit) | l;
+    }
+}
+
+}  // namespace ctws
+
+namespace ctws {
+
+// =========================================================================================
+// Descent pre-pass of the packed flood.
+//
+// Let sd(q) be the neighbour with the smallest height strictly below h(q) (6-nbhd; 4-nbhd in
+// plane for 2-D ws), defined only when that smallest height is attained by ONE neighbour.  If
+// the chain q -> sd(q) -> ... ends in a seed s, the reversed chain is a path from s on which
+// the height rises to h(q), so C(q) = h(q); every other neighbour p has C(p) >= h(p) >
+// h(sd(q)) = C(sd(q)), so sd(q) is q's unique argmin neighbour, d(q) = 0 (h(q) > C(sd(q))),
+// and by induction along the chain the fixpoint key of q is (h(q), 0, label(s)).  Such voxels
+// are final before any relaxation: they are written as fixed keys and only the remaining
+// voxels (catchments of local minima of h that hold no seed, and of tie voxels) are flooded.
+// k_flood_verify re-checks K(q) = f(min_p K(p)) everywhere; on a violation the batch is
+// flooded again from the seeds alone.
+// =========================================================================================
+
+// parent = strictly steepest descent neighbour (self for seeds and local minima)
+template <int ND>
+__global__ void __launch_bounds__(256) k_descent_parent(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                        const float* __restrict__ h, const uint32_t* __restrict__ lab,
+                                                        uint32_t* __restrict__ par) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const float* hb = h + B.base;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const int64_t nrows = (int64_t)B.Z * B.Y;
+    for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
+        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
+#pragma unroll
+            for (int rr = 0; rr < kRows; ++rr) {
+                const int64_t row = r0 + rr;
+                if (row >= nrows) break;
+                const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
+                const int64_t i = row * B.X + x;
+                uint32_t best = ordf(hb[i]);
+                int64_t bi = i;
+                bool tie = false;
+                auto cand = [&](bool ok, int64_t j) {
+                    if (!ok) return;
+                    const uint32_t v = ordf(hb[j]);
+                    tie = (v == best) || (tie && v > best);
+                    if (v < best) {
+                        best = v;
+                        bi = j;
+                    }
+                };
+                if (ND == 3) {
+                    cand(z > 0, i - YX);
+                    cand(z + 1 < B.Z, i + YX);
+                }
+                cand(y > 0, i - B.X);
+                cand(y + 1 < B.Y, i + B.X);
+                cand(x > 0, i - 1);
+                cand(x + 1 < B.X, i + 1);
+                // an exact tie at the lowest neighbour height: the parent is decided by the
+                // labels, so q (and what drains through it) is left to the flood
+                if (tie || (lab[B.base + i] & kFixedBit)) bi = i;
+                par[B.base + i] = (uint32_t)bi;
+            }
+        }
+}
+template __global__ void k_descent_parent<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
+                                             uint32_t*);
+template __global__ void k_descent_parent<2>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
+                                             uint32_t*);
+
+// pointer jumping: par <- par[par[par]] (flag[0] set while some pointer still moves)
+__global__ void __launch_bounds__(256) k_descent_jump(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                      uint32_t* __restrict__ parg, uint32_t* __restrict__ flag) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    uint32_t* par = parg + B.base;
+    bool moved = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = par[i];
+        const uint32_t pp = par[p];
+        if (pp != p) {
+            par[i] = par[pp];
+            moved = true;
+        }
+    }
+    if (__ballot(moved) && (threadIdx.x & 63) == 0 && !*(volatile uint32_t*)flag) atomicOr(flag, 1u);
+}
+
+// voxels whose descent ends in a seed get their final key, fixed; the others wait for the
+// flood (INF key).  Bitmaps, one word per 64 voxels of a row (the 64 lanes of a wave cover
+// exactly one word): open = not final yet, chg = final (the first "changed" set, whose
+// neighbours form the first frontier).
+__global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                      const float* __restrict__ h, const uint32_t* __restrict__ lab,
+                                                      const uint32_t* __restrict__ par, uint64_t* __restrict__ key,
+                                                      uint8_t* __restrict__ fixedv, uint64_t* __restrict__ open,
+                                                      uint64_t* __restrict__ chg) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t nrows = (int64_t)B.Z * B.Y;
+    const int wpr = (B.X + 63) >> 6;
+    for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
+        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
+#pragma unroll
+            for (int rr = 0; rr < kRows; ++rr) {
+                const int64_t row = r0 + rr;
+                if (row >= nrows) break;
+                const int64_t gi = B.base + row * B.X + x;
+                const uint32_t lr = lab[B.base + par[gi]];
+                const bool res = (lr & kFixedBit) != 0;
+                key[gi] = res ? (((uint64_t)ordf(h[gi]) << 32) | (uint64_t)(lr & (uint32_t)kLabelMask)) : kPackInf;
+                fixedv[gi] = res ? 1 : 0;
+                const uint64_t op = __ballot(!res);
+                const uint64_t fi = __ballot(res);
+                if ((threadIdx.x & 63) == 0) {
+                    open[B.fbase + row * wpr + (x >> 6)] = op;
+                    chg[B.fbase + row * wpr + (x >> 6)] = fi;
+                }
+            }
+        }
+}
+
+// One iteration of the frontier relaxation.  frontier = (neighbours of the voxels changed in
+// the previous iteration) & open; every frontier voxel recomputes K = f(min of its
+// neighbours' keys) in place (monotone: keys only decrease, so a neighbour updated in the same
+// launch is fine; a stale read is repaired by the next iteration, as the neighbour's change
+// is recorded).  A wave owns 64 consecutive words: it builds their frontier from the previous
+// changed bitmap, expands the set bits into an LDS list and relaxes 64 voxels per step, one
+// per lane; its changed bits collect in LDS and are stored whole (no memset, no global
+// atomics).
+constexpr int kFrontierWaves = 4;
+template <int ND>
+__global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                  const float* __restrict__ h, uint64_t* __restrict__ key,
+                                                  const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
+                                                  uint64_t* __restrict__ cnext, uint32_t* __restrict__ flag) {
+    __shared__ uint64_t schg[kFrontierWaves][64];
+    __shared__ int srow[kFrontierWaves][64];
+    __shared__ uint16_t slist[kFrontierWaves][64 * 64];
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t ws = (int64_t)B.Y * wpr;
+    const int64_t nwords = (int64_t)B.Z * ws;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const uint64_t* cp = cprev + B.fbase;
+    const uint64_t* op = open + B.fbase;
+    uint64_t* cn = cnext + B.fbase;
+    uint64_t* kb = key + B.base;
+    const float* hb = h + B.base;
+    bool any = false;
+    for (int64_t w0 = ((int64_t)blockIdx.x * kFrontierWaves + wv) * 64; w0 < nwords;
+         w0 += (int64_t)gridDim.x * kFrontierWaves * 64) {
+        const int64_t wl = w0 + lane;
+        uint64_t f = 0ull;
+        int row = 0, xw = 0;
+        if (wl < nwords) {
+            row = (int)(wl / wpr);
+            xw = (int)(wl - (int64_t)row * wpr);
+            const int z = row / B.Y, y = row - z * B.Y;
+            const uint64_t c = cp[wl];
+            f = (c << 1) | (c >> 1);
+            if (xw > 0) f |= cp[wl - 1] >> 63;
+            if (xw + 1 < wpr) f |= cp[wl + 1] << 63;
+            if (y > 0) f |= cp[wl - wpr];
+            if (y + 1 < B.Y) f |= cp[wl + wpr];
+            if (ND == 3) {
+                if (z > 0) f |= cp[wl - ws];
+                if (z + 1 < B.Z) f |= cp[wl + ws];
+            }
+            f &= op[wl];  // open voxels only (their x < X)
+        }
+        schg[wv][lane] = 0ull;
+        srow[wv][lane] = row * 64 + xw;  // row < 2^25 (Z * Y <= 2^22)
+        // exclusive prefix of the per-word bit counts -> list offsets
+        const int cnt = __popcll(f);
+        int incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        const int total = __shfl(incl, 63);
+        int off = incl - cnt;
+        while (f) {
+            const int b = __builtin_ctzll(f);
+            f &= f - 1;
+            slist[wv][off++] = (uint16_t)((lane << 6) | b);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (int t = 0; t < total; t += 64) {
+            if (t + lane < total) {
+                const int e = slist[wv][t + lane];
+                const int j = e >> 6, b = e & 63;
+                const int rx = srow[wv][j];
+                const int r = rx >> 6, xq = rx & 63;
+                const int z = r / B.Y, y = r - z * B.Y;
+                const int x = xq * 64 + b;
+                const int64_t i = (int64_t)r * B.X + x;
+                uint64_t m = kPackInf;
+                if (ND == 3) {
+                    if (z > 0) m = min(m, kb[i - YX]);
+                    if (z + 1 < B.Z) m = min(m, kb[i + YX]);
+                }
+                if (y > 0) m = min(m, kb[i - B.X]);
+                if (y + 1 < B.Y) m = min(m, kb[i + B.X]);
+                if (x > 0) m = min(m, kb[i - 1]);
+                if (x + 1 < B.X) m = min(m, kb[i + 1]);
+                if (m != kPackInf) {
+                    const uint64_t k = f_packed(ordf(hb[i]), m);
+                    if (k != kb[i]) {
+                        kb[i] = k;
+                        atomicOr((unsigned long long*)&schg[wv][j], 1ull << b);
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (wl < nwords) {
+            const uint64_t c = schg[wv][lane];
+            cn[wl] = c;
+            any |= c != 0ull;
+        }
+    }
+    if (__ballot(any) && lane == 0 && !*(volatile uint32_t*)flag) atomicOr(flag, 1u);
+}
+template __global__ void k_frontier<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
+                                       const uint64_t*, uint64_t*, uint32_t*);
+template __global__ void k_frontier<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
+                                       const uint64_t*, uint64_t*, uint32_t*);
+
+// tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
+__global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                        const uint64_t* __restrict__ open, uint32_t* __restrict__ act,
+                                                        int tz, int ty, int tx) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t bits = open[B.fbase + w];
+        if (!bits) continue;
+        const int64_t row = w / wpr;
+        const int xw = (int)(w - row * wpr);
+        const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
+        while (bits) {
+            const int b = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            const int x = xw * 64 + b;
+            uint32_t* a = act + B.tbase + ((z / tz) * B.ty + y / ty) * B.tx + x / tx;
+            if (!*a) atomicOr(a, kActFull);
+        }
+    }
+}
+
+// fixpoint check of the packed flood: K(q) == f(min_p K(p)) for every non-seed voxel
+template <int ND>
+__global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                      const float* __restrict__ h, const uint64_t* __restrict__ key,
+                                                      const uint32_t* __restrict__ lab, uint32_t* __restrict__ flag) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const uint64_t* k = key + B.base;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const int64_t nrows = (int64_t)B.Z * B.Y;
+    bool bad = false;
+    for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
+        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
+#pragma unroll
+            for (int rr = 0; rr < kRows; ++rr) {
+                const int64_t row = r0 + rr;
+                if (row >= nrows) break;
+                const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
+                const int64_t i = row * B.X + x;
+                uint64_t m = kPackInf;
+                if (ND == 3) {
+                    if (z > 0) m = min(m, k[i - YX]);
+                    if (z + 1 < B.Z) m = min(m, k[i + YX]);
+                }
+                if (y > 0) m = min(m, k[i - B.X]);
+                if (y + 1 < B.Y) m = min(m, k[i + B.X]);
+                if (x > 0) m = min(m, k[i - 1]);
+                if (x + 1 < B.X) m = min(m, k[i + 1]);
+                const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(h[B.base + i]), m);
+                const bool b1 = !(lab[B.base + i] & kFixedBit) && e != k[i];
+                if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
+                    const uint32_t slot = atomicAdd(&flag[1], 1u);
+                    if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + i);
+                }
+                bad |= b1;
+            }
+        }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+template __global__ void k_flood_verify<3>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
+                                           const uint32_t*, uint32_t*);
+template __global__ void k_flood_verify<2>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
+                                           const uint32_t*, uint32_t*);
+
+// seeds only (fallback after a failed verification)
+__global__ void __launch_bounds__(256) k_flood_reset(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     const float* __restrict__ h, const uint32_t* __restrict__ lab,
+                                                     uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t l = lab[B.base + i];
+        const bool s = (l & kFixedBit) != 0;
+        key[B.base + i] = s ? (((uint64_t)ordf(h[B.base + i]) << 32) | (uint64_t)(l & (uint32_t)kLabelMask)) : kPackInf;
+        fixedv[B.base + i] = s ? 1 : 0;
     }
 }
 

@@ -78,18 +78,20 @@ __global__ void __launch_bounds__(256) k_gauss_col(const BlockDesc* __restrict__
     const int ntap = 2 * gp.r + 1;
     for (int j = threadIdx.x; j < ntap; j += 256) k[j] = taps[j];
     const bool colok = xb + c < B.X;
-    for (int p = r0; p < L; p += RS) {
-        float v = 0.0f;
-        if (colok) {
-            const int64_t li = obase + p * lstride + xb + c;
-            if (gp.hmap_src) {
-                const int z = (gp.axis == 1) ? o : p;
-                v = hmap_value(B, S[blockIdx.y], hp, in, dt, smin, smax, li, z);
-            } else {
-                v = in[B.base + li];
-            }
-        }
-        col[p * W + c] = v;
+    if (gp.hmap_src) {
+        const BlockStat& st = S[blockIdx.y];
+        staged_loop<8>(
+            r0, L, RS,
+            [&](int p) {
+                const int64_t li = obase + p * lstride + xb + (colok ? c : 0);
+                return hmap_value(B, st, hp, in, dt, smin, smax, li, (gp.axis == 1) ? o : p);
+            },
+            [&](int p, float v) { col[p * W + c] = colok ? v : 0.0f; });
+    } else {
+        const float* gsrc = in + B.base + obase + xb + (colok ? c : 0);
+        staged_loop<8>(
+            r0, L, RS, [&](int p) { return gsrc[p * lstride]; },
+            [&](int p, float v) { col[p * W + c] = colok ? v : 0.0f; });
     }
     __syncthreads();
     if (!colok) return;
@@ -132,11 +134,14 @@ __global__ void __launch_bounds__(256) k_gauss_row(const BlockDesc* __restrict__
     const int64_t rbase = row * X;
     if (rowok) {
         const int z = (int)(row / B.Y);
-        for (int x = lane; x < X; x += 64) {
-            float v;
-            if (gp.hmap_src) v = hmap_value(B, S[blockIdx.y], hp, in, dt, smin, smax, rbase + x, z);
-            else v = in[B.base + rbase + x];
-            rowb[x] = v;
+        if (gp.hmap_src) {
+            const BlockStat& st = S[blockIdx.y];
+            staged_loop<8>(
+                lane, X, 64, [&](int x) { return hmap_value(B, st, hp, in, dt, smin, smax, rbase + x, z); },
+                [&](int x, float v) { rowb[x] = v; });
+        } else {
+            const float* gsrc = in + B.base + rbase;
+            staged_loop<8>(lane, X, 64, [&](int x) { return gsrc[x]; }, [&](int x, float v) { rowb[x] = v; });
         }
     }
     __syncthreads();

@@ -81,8 +81,7 @@ __global__ void __launch_bounds__(256) k_p2_zero_dt(const BlockDesc* __restrict_
 
 // per-voxel relabel key (kEmptyKey: unlabelled); written into `vkey`
 __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                   const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ Wg,
-                                                   const uint32_t* __restrict__ Wpg, const uint32_t* __restrict__ sb,
+                                                   const uint32_t* __restrict__ PFg, const uint32_t* __restrict__ sb,
                                                    uint64_t* __restrict__ vkey) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
@@ -98,10 +97,8 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
             if ((uint32_t)u != 0)
                 k = (B.nd_ws == 3) ? (uint64_t)(uint32_t)u : (((uint64_t)z << 33) | kInitTag | (uint32_t)u);
         } else if (!B.mask || B.mask[i]) {
-            const uint32_t f = scan_key(B, z, y, x);
-            const uint32_t r = PF[f];  // flattened: the root
-            if (r != kNoParent) {
-                const uint32_t gl = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, r) + 1u;
+            const uint32_t gl = cc_label(PF, PF[i]);  // seed label (0: background)
+            if (gl) {
                 if (B.nd_ws == 3) {
                     const uint32_t v = gl + (uint32_t)B.id_offset;  // wraps to 0: background
                     if (v) k = v;
@@ -150,16 +147,16 @@ __global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__
     }
 }
 
-// first positions -> roots of the bitmap (P preset to kNoParent)
+// first positions -> bits of the root bitmap (zeroed beforehand)
 __global__ void __launch_bounds__(256) k_p2_roots(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                   const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ hpos,
-                                                  uint32_t* __restrict__ P) {
+                                                  uint64_t* __restrict__ W) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < B.hcap; s += (int64_t)gridDim.x * blockDim.x) {
         if (hkey[B.hbase + s] == kEmptyKey) continue;
         const uint32_t f = hpos[B.hbase + s];
-        P[B.base + f] = f;
+        atomicOr((unsigned long long*)&W[B.wbase + (f >> 6)], 1ull << (f & 63));
     }
 }
 
@@ -274,8 +271,8 @@ __global__ void __launch_bounds__(256) k_p2_output(const BlockDesc* __restrict__
         mx = max(mx, v);
         B.out[i] = v;
     }
-    for (int s = 32; s > 0; s >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, s));
-    if ((threadIdx.x & 63) == 0 && mx) atomicMax(&S[blockIdx.y].max_label, mx);
+    mx = wg_reduce_u32(mx, OpMax());
+    if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);
 }
 
 }  // namespace ctws

@@ -131,9 +131,9 @@ __global__ void __launch_bounds__(256) k_slice_max(const BlockDesc* __restrict__
         const int z0 = __shfl(z, 0);
         if (__all(z == z0 || z < 0)) {
             for (int s = 32; s > 0; s >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, s));
-            if ((threadIdx.x & 63) == 0 && v && z0 >= 0) atomicMax(&smax[B.sbase + z0], v);
+            if ((threadIdx.x & 63) == 0 && v && z0 >= 0) atomic_max_if(&smax[B.sbase + z0], v);
         } else if (v) {
-            atomicMax(&smax[B.sbase + z], v);
+            atomic_max_if(&smax[B.sbase + z], v);
         }
     }
 }
