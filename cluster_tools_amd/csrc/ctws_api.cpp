@@ -63,6 +63,7 @@ struct Workspace {
     int64_t cap_front = 0;
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
     uint32_t* fflags = nullptr;
+    uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: changed
 };
 
 constexpr int kCounterBytes = 4 * (4 + 4 * kStatSlots);  // flood flag + statistics slots
@@ -205,6 +206,8 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(front0, front);
         ALLOC(front1, front);
         ALLOC(fopen, front);
+        ALLOC(fchunk0, front / 64 + 1);
+        ALLOC(fchunk1, front / 64 + 1);
         w.cap_front = front;
     }
     if (!w.fflags) ALLOC(fflags, kFrontierBatch);
@@ -511,7 +514,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
                             (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
         d.fbase = TF;
-        TF += (int64_t)d.Z * d.Y * ((d.X + 63) / 64);
+        TF += ((int64_t)d.Z * d.Y * ((d.X + 63) / 64) + 63) & ~(int64_t)63;  // chunk aligned
         T += d.N;
         TI += d.NI;
         TW += words_of(d.N);
@@ -759,22 +762,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int rounds1 = 0, rounds2 = 0;
     h->flood_tiles = h->flood_iters = h->flood_lines = 0;
     float fk1 = 0.f, fk2 = 0.f;
-    int jumps = 0, fallback = 0, fiters = 0;
+    int fallback = 0, fiters = 0;
     if (packed && !h->no_descent) {
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
-        if (pl.nd_ws == 3) k_descent_parent<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P);
-        else k_descent_parent<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P);
-        LAUNCHCHK();
-        mark("descent_parent");
-        for (jumps = 1; jumps <= 64; ++jumps) {
-            HIPCHK(hipMemsetAsync(w.counter, 0, 4, h->stream));
-            k_descent_jump<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.P, w.counter);
+        {
+            // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
+            const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;
+            const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
+            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P);
+            else k_descent_tile<2><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P);
             LAUNCHCHK();
-            HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 4, hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
-            if (!h->h_counter[0]) break;
         }
-        mark("descent_jump");
+        mark("descent_tile");
         int TZ, TY, TX;
         flood_tile_dims(pl.nd_ws, true, &TZ, &TY, &TX);
         HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
@@ -784,18 +783,22 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // frontier relaxation of the remaining voxels (k_frontier, one voxel per lane)
         uint64_t* fcur = w.front0;
         uint64_t* fnext = w.front1;
+        uint32_t* ccur = w.fchunk0;
+        uint32_t* cnext = w.fchunk1;
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ccur, 1u, (size_t)(TF / 64 + 1), h->stream));
         const dim3 fg((unsigned)std::min<int64_t>((TF / nb + 64 * 4 - 1) / (64 * 4) + 1, 2048), nb);
         bool converged = false;
         for (fiters = 0; fiters < kFrontierMaxIters && !converged;) {
             HIPCHK(hipMemsetAsync(w.fflags, 0, sizeof(uint32_t) * kFrontierBatch, h->stream));
             for (int k = 0; k < kFrontierBatch; ++k) {
                 if (pl.nd_ws == 3)
-                    k_frontier<3><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext,
-                                                             w.fflags + k);
+                    k_frontier<3><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur,
+                                                             cnext, w.fflags + k);
                 else
-                    k_frontier<2><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext,
-                                                             w.fflags + k);
+                    k_frontier<2><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur,
+                                                             cnext, w.fflags + k);
                 std::swap(fcur, fnext);
+                std::swap(ccur, cnext);
             }
             LAUNCHCHK();
             HIPCHK(hipMemcpyAsync(h->h_counter, w.fflags, sizeof(uint32_t) * kFrontierBatch, hipMemcpyDeviceToHost,
@@ -947,7 +950,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         h->timings.push_back({names[i], ms});
     }
     h->timings.push_back({"flood_rounds", (float)rounds1});
-    h->timings.push_back({"descent_jumps", (float)jumps});
     h->timings.push_back({"frontier_iters", (float)fiters});
     h->timings.push_back({"flood_fallback", (float)fallback});
     h->timings.push_back({"regrow_rounds", (float)rounds2});

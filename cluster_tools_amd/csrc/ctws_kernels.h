@@ -82,13 +82,12 @@ constexpr int kLineWords = 24;
 constexpr int kStatSlots = 64;  // flood statistics: counter[4 + slot * 4 + k]  // per tile: 8 words of line bits for each of x, y, z
 __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
 template <int ND>
-__global__ void k_descent_parent(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint32_t*);
-__global__ void k_descent_jump(const BlockDesc*, const BlockStat*, uint32_t*, uint32_t*);
+__global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint32_t*);
 __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
                                uint64_t*, uint8_t*, uint64_t*, uint64_t*);
 template <int ND>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                           const uint64_t*, uint64_t*, uint32_t*);
+                           const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>
 __global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint32_t*,

@@ -545,73 +545,126 @@ namespace ctws {
 // flooded again from the seeds alone.
 // =========================================================================================
 
-// parent = strictly steepest descent neighbour (self for seeds and local minima)
+// Descent inside a tile: tile (3-D 16^3, 2-D 1 x 64 x 64) + 1-voxel halo of heights in LDS;
+// every tile voxel gets its steepest-descent parent (itself for seeds, local minima and ties),
+// then pointer jumping in LDS runs each chain to its end inside the tile: a root of the tile
+// or the first voxel outside it.  exit[q] = that voxel (block C-order index); chains that
+// leave the tile are finished by k_descent_init following exit[] across tiles (a hop per tile
+// crossed).  One pass over the volume instead of a global pointer-jumping pass per doubling.
 template <int ND>
-__global__ void __launch_bounds__(256) k_descent_parent(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                        const float* __restrict__ h, const uint32_t* __restrict__ lab,
-                                                        uint32_t* __restrict__ par) {
+struct DTile;
+template <>
+struct DTile<3> {
+    static constexpr int TZ = 16, TY = 16, TX = 16, HZ = 18;
+};
+template <>
+struct DTile<2> {
+    static constexpr int TZ = 1, TY = 64, TX = 64, HZ = 1;
+};
+
+template <int ND>
+__global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                      const float* __restrict__ h, const uint32_t* __restrict__ lab,
+                                                      uint32_t* __restrict__ exitp) {
+    using T = DTile<ND>;
+    constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, HZ = T::HZ, HY = TY + 2, HX = TX + 2;
+    constexpr int HN = HZ * HY * HX, TN = TZ * TY * TX;
+    constexpr int ZOFF = ND == 3 ? 1 : 0;
+    __shared__ uint32_t sh[HN];  // ordered heights (0xFFFFFFFF outside the block)
+    __shared__ int sp[TN];       // pointer: < TN interior voxel, >= TN halo voxel (TN + halo index)
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const float* hb = h + B.base;
+    const int ntx = (B.X + TX - 1) / TX, nty = (B.Y + TY - 1) / TY, ntz = (B.Z + TZ - 1) / TZ;
+    const int t = blockIdx.x;
+    if (t >= ntx * nty * ntz) return;
+    const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
+    const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
     const int64_t YX = (int64_t)B.Y * B.X;
-    const int64_t nrows = (int64_t)B.Z * B.Y;
-    for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
-        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
-#pragma unroll
-            for (int rr = 0; rr < kRows; ++rr) {
-                const int64_t row = r0 + rr;
-                if (row >= nrows) break;
-                const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
-                const int64_t i = row * B.X + x;
-                uint32_t best = ordf(hb[i]);
-                int64_t bi = i;
-                bool tie = false;
-                auto cand = [&](bool ok, int64_t j) {
-                    if (!ok) return;
-                    const uint32_t v = ordf(hb[j]);
-                    tie = (v == best) || (tie && v > best);
-                    if (v < best) {
-                        best = v;
-                        bi = j;
-                    }
-                };
-                if (ND == 3) {
-                    cand(z > 0, i - YX);
-                    cand(z + 1 < B.Z, i + YX);
+    const float* hb = h + B.base;
+    staged_loop<8>(
+        (int)threadIdx.x, HN, 256,
+        [&](int c) -> uint32_t {
+            const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
+            const int gz = z0 + hz - ZOFF, gy = y0 + hy - 1, gx = x0 + hx - 1;
+            if (gz < 0 || gz >= B.Z || gy < 0 || gy >= B.Y || gx < 0 || gx >= B.X) return 0xFFFFFFFFu;
+            return ordf(hb[gz * YX + (int64_t)gy * B.X + gx]);
+        },
+        [&](int c, uint32_t v) { sh[c] = v; });
+    __syncthreads();
+    // parents
+    for (int c = threadIdx.x; c < TN; c += 256) {
+        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+        const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
+        int p = c;
+        if (gz < B.Z && gy < B.Y && gx < B.X && !(lab[B.base + gz * YX + (int64_t)gy * B.X + gx] & kFixedBit)) {
+            const int hc = ((lz + ZOFF) * HY + ly + 1) * HX + lx + 1;
+            uint32_t best = sh[hc];
+            int bh = -1;
+            bool tie = false;
+            auto cand = [&](int o) {
+                const uint32_t v = sh[hc + o];
+                tie = (v == best) || (tie && v > best);
+                if (v < best) {
+                    best = v;
+                    bh = hc + o;
                 }
-                cand(y > 0, i - B.X);
-                cand(y + 1 < B.Y, i + B.X);
-                cand(x > 0, i - 1);
-                cand(x + 1 < B.X, i + 1);
-                // an exact tie at the lowest neighbour height: the parent is decided by the
-                // labels, so q (and what drains through it) is left to the flood
-                if (tie || (lab[B.base + i] & kFixedBit)) bi = i;
-                par[B.base + i] = (uint32_t)bi;
+            };
+            if (ND == 3) {
+                cand(-HX * HY);
+                cand(HX * HY);
+            }
+            cand(-HX);
+            cand(HX);
+            cand(-1);
+            cand(1);
+            // an exact tie at the lowest neighbour height: left to the flood (see above)
+            if (bh >= 0 && !tie) {
+                const int hx = bh % HX, hy = (bh / HX) % HY, hz = bh / (HX * HY);
+                const bool inside = hx >= 1 && hx <= TX && hy >= 1 && hy <= TY && (ND == 2 || (hz >= 1 && hz <= TZ));
+                p = inside ? ((hz - ZOFF) * TY + (hy - 1)) * TX + (hx - 1) : TN + bh;
             }
         }
-}
-template __global__ void k_descent_parent<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                             uint32_t*);
-template __global__ void k_descent_parent<2>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                             uint32_t*);
-
-// pointer jumping: par <- par[par[par]] (flag[0] set while some pointer still moves)
-__global__ void __launch_bounds__(256) k_descent_jump(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                      uint32_t* __restrict__ parg, uint32_t* __restrict__ flag) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
-    uint32_t* par = parg + B.base;
-    bool moved = false;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t p = par[i];
-        const uint32_t pp = par[p];
-        if (pp != p) {
-            par[i] = par[pp];
-            moved = true;
-        }
+        sp[c] = p;
     }
-    if (__ballot(moved) && (threadIdx.x & 63) == 0 && !*(volatile uint32_t*)flag) atomicOr(flag, 1u);
+    __syncthreads();
+    // pointer jumping inside the tile
+    for (int it = 0; it < 16; ++it) {
+        bool moved = false;
+        for (int c = threadIdx.x; c < TN; c += 256) {
+            const int p = sp[c];
+            if (p < TN) {
+                const int pp = sp[p];
+                if (pp != p) {
+                    sp[c] = pp;
+                    moved = true;
+                }
+            }
+        }
+        if (!__syncthreads_or(moved)) break;
+    }
+    for (int c = threadIdx.x; c < TN; c += 256) {
+        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+        const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
+        if (gz >= B.Z || gy >= B.Y || gx >= B.X) continue;
+        const int p = sp[c];
+        int ez, ey, ex;
+        if (p < TN) {
+            ex = x0 + p % TX;
+            ey = y0 + (p / TX) % TY;
+            ez = z0 + p / (TX * TY);
+        } else {
+            const int q = p - TN;
+            ex = x0 + q % HX - 1;
+            ey = y0 + (q / HX) % HY - 1;
+            ez = z0 + q / (HX * HY) - ZOFF;
+        }
+        exitp[B.base + gz * YX + (int64_t)gy * B.X + gx] = (uint32_t)(ez * YX + (int64_t)ey * B.X + ex);
+    }
 }
+template __global__ void k_descent_tile<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
+                                           uint32_t*);
+template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
+                                           uint32_t*);
 
 // voxels whose descent ends in a seed get their final key, fixed; the others wait for the
 // flood (INF key).  Bitmaps, one word per 64 voxels of a row (the 64 lanes of a wave cover
@@ -633,7 +686,13 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
                 const int64_t row = r0 + rr;
                 if (row >= nrows) break;
                 const int64_t gi = B.base + row * B.X + x;
-                const uint32_t lr = lab[B.base + par[gi]];
+                uint32_t r = par[gi];
+                for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
+                    const uint32_t n = par[B.base + r];
+                    if (n == r) break;
+                    r = n;
+                }
+                const uint32_t lr = lab[B.base + r];
                 const bool res = (lr & kFixedBit) != 0;
                 key[gi] = res ? (((uint64_t)ordf(h[gi]) << 32) | (uint64_t)(lr & (uint32_t)kLabelMask)) : kPackInf;
                 fixedv[gi] = res ? 1 : 0;
@@ -656,14 +715,36 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
 // per lane; its changed bits collect in LDS and are stored whole (no memset, no global
 // atomics).
 constexpr int kFrontierWaves = 4;
+constexpr int kFrontierUnroll = 4;  // list entries per lane in flight
+
+// position of the k-th (0-based) set bit of w (k < popcount(w))
+__device__ __forceinline__ int kth_set_bit(uint64_t w, int k) {
+    int pos = 0;
+#pragma unroll
+    for (int half = 32; half > 0; half >>= 1) {
+        const uint64_t lo = w & ((1ull << half) - 1ull);
+        const int c = __popcll(lo);
+        if (k >= c) {
+            k -= c;
+            w >>= half;
+            pos += half;
+        } else {
+            w = lo;
+        }
+    }
+    return pos;
+}
+
 template <int ND>
 __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                   const float* __restrict__ h, uint64_t* __restrict__ key,
                                                   const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
-                                                  uint64_t* __restrict__ cnext, uint32_t* __restrict__ flag) {
+                                                  uint64_t* __restrict__ cnext, const uint32_t* __restrict__ fprev,
+                                                  uint32_t* __restrict__ fnext, uint32_t* __restrict__ flag) {
     __shared__ uint64_t schg[kFrontierWaves][64];
+    __shared__ uint64_t sfw[kFrontierWaves][64];
+    __shared__ int spre[kFrontierWaves][64];
     __shared__ int srow[kFrontierWaves][64];
-    __shared__ uint16_t slist[kFrontierWaves][64 * 64];
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -676,9 +757,29 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     uint64_t* cn = cnext + B.fbase;
     uint64_t* kb = key + B.base;
     const float* hb = h + B.base;
+    const uint32_t* fp = fprev + (B.fbase >> 6);
+    uint32_t* fnx = fnext + (B.fbase >> 6);
+    const int64_t nchunks = (nwords + 63) >> 6;
+    // word w of the previous changed bitmap (0 when its chunk was quiet)
+    auto cw = [&](int64_t w) -> uint64_t { return fp[w >> 6] ? cp[w] : 0ull; };
     bool any = false;
     for (int64_t w0 = ((int64_t)blockIdx.x * kFrontierWaves + wv) * 64; w0 < nwords;
          w0 += (int64_t)gridDim.x * kFrontierWaves * 64) {
+        const int64_t ch0 = w0 >> 6;
+        {
+            // quiet neighbourhood: nothing to do in this chunk
+            uint32_t q = fp[ch0];
+            if (ch0 > 0) q |= fp[ch0 - 1];
+            if (ch0 + 1 < nchunks) q |= fp[ch0 + 1];
+            if (ND == 3) {
+                if (w0 - ws >= 0) q |= fp[(w0 - ws) >> 6] | fp[(w0 - ws + 63) >> 6];
+                if (w0 + ws < nwords) q |= fp[(w0 + ws) >> 6] | fp[min(nwords - 1, w0 + ws + 63) >> 6];
+            }
+            if (!q) {
+                if (lane == 0) fnx[ch0] = 0u;
+                continue;
+            }
+        }
         const int64_t wl = w0 + lane;
         uint64_t f = 0ull;
         int row = 0, xw = 0;
@@ -686,21 +787,20 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             row = (int)(wl / wpr);
             xw = (int)(wl - (int64_t)row * wpr);
             const int z = row / B.Y, y = row - z * B.Y;
-            const uint64_t c = cp[wl];
+            const uint64_t c = cw(wl);
             f = (c << 1) | (c >> 1);
-            if (xw > 0) f |= cp[wl - 1] >> 63;
-            if (xw + 1 < wpr) f |= cp[wl + 1] << 63;
-            if (y > 0) f |= cp[wl - wpr];
-            if (y + 1 < B.Y) f |= cp[wl + wpr];
+            if (xw > 0) f |= cw(wl - 1) >> 63;
+            if (xw + 1 < wpr) f |= cw(wl + 1) << 63;
+            if (y > 0) f |= cw(wl - wpr);
+            if (y + 1 < B.Y) f |= cw(wl + wpr);
             if (ND == 3) {
-                if (z > 0) f |= cp[wl - ws];
-                if (z + 1 < B.Z) f |= cp[wl + ws];
+                if (z > 0) f |= cw(wl - ws);
+                if (z + 1 < B.Z) f |= cw(wl + ws);
             }
             f &= op[wl];  // open voxels only (their x < X)
         }
-        schg[wv][lane] = 0ull;
-        srow[wv][lane] = row * 64 + xw;  // row < 2^25 (Z * Y <= 2^22)
-        // exclusive prefix of the per-word bit counts -> list offsets
+        // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list is
+        // bit (e - pre[j]) of word j, the last j with pre[j] <= e
         const int cnt = __popcll(f);
         int incl = cnt;
         for (int o = 1; o < 64; o <<= 1) {
@@ -708,55 +808,80 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             if (lane >= o) incl += t;
         }
         const int total = __shfl(incl, 63);
-        int off = incl - cnt;
-        while (f) {
-            const int b = __builtin_ctzll(f);
-            f &= f - 1;
-            slist[wv][off++] = (uint16_t)((lane << 6) | b);
-        }
-        __builtin_amdgcn_wave_barrier();
+        schg[wv][lane] = 0ull;
+        sfw[wv][lane] = f;
+        spre[wv][lane] = incl - cnt;
+        srow[wv][lane] = row * 64 + xw;  // row < 2^25 (Z * Y <= 2^22)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        for (int t = 0; t < total; t += 64) {
-            if (t + lane < total) {
-                const int e = slist[wv][t + lane];
-                const int j = e >> 6, b = e & 63;
-                const int rx = srow[wv][j];
-                const int r = rx >> 6, xq = rx & 63;
-                const int z = r / B.Y, y = r - z * B.Y;
-                const int x = xq * 64 + b;
-                const int64_t i = (int64_t)r * B.X + x;
-                uint64_t m = kPackInf;
-                if (ND == 3) {
-                    if (z > 0) m = min(m, kb[i - YX]);
-                    if (z + 1 < B.Z) m = min(m, kb[i + YX]);
-                }
-                if (y > 0) m = min(m, kb[i - B.X]);
-                if (y + 1 < B.Y) m = min(m, kb[i + B.X]);
-                if (x > 0) m = min(m, kb[i - 1]);
-                if (x + 1 < B.X) m = min(m, kb[i + 1]);
-                if (m != kPackInf) {
-                    const uint64_t k = f_packed(ordf(hb[i]), m);
-                    if (k != kb[i]) {
-                        kb[i] = k;
-                        atomicOr((unsigned long long*)&schg[wv][j], 1ull << b);
+        __builtin_amdgcn_wave_barrier();
+        for (int t0 = 0; t0 < total; t0 += 64 * kFrontierUnroll) {
+            int64_t vi[kFrontierUnroll];
+            int vj[kFrontierUnroll], vb[kFrontierUnroll];
+            uint64_t nb[kFrontierUnroll][6];
+            uint64_t own[kFrontierUnroll];
+            float hv[kFrontierUnroll];
+#pragma unroll
+            for (int u = 0; u < kFrontierUnroll; ++u) {
+                const int e = t0 + u * 64 + lane;
+                vi[u] = -1;
+                vj[u] = 0;
+                vb[u] = 0;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) nb[u][k] = kPackInf;
+                own[u] = kPackInf;
+                hv[u] = 0.0f;
+                if (e < total) {
+                    int j = 0;
+#pragma unroll
+                    for (int step = 32; step > 0; step >>= 1)
+                        if (spre[wv][j + step] <= e) j += step;
+                    const int b = kth_set_bit(sfw[wv][j], e - spre[wv][j]);
+                    const int rx = srow[wv][j];
+                    const int r = rx >> 6, xq = rx & 63;
+                    const int z = r / B.Y, y = r - z * B.Y;
+                    const int x = xq * 64 + b;
+                    const int64_t i = (int64_t)r * B.X + x;
+                    vi[u] = i;
+                    vj[u] = j;
+                    vb[u] = b;
+                    if (ND == 3) {
+                        if (z > 0) nb[u][0] = kb[i - YX];
+                        if (z + 1 < B.Z) nb[u][1] = kb[i + YX];
                     }
+                    if (y > 0) nb[u][2] = kb[i - B.X];
+                    if (y + 1 < B.Y) nb[u][3] = kb[i + B.X];
+                    if (x > 0) nb[u][4] = kb[i - 1];
+                    if (x + 1 < B.X) nb[u][5] = kb[i + 1];
+                    own[u] = kb[i];
+                    hv[u] = hb[i];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kFrontierUnroll; ++u) {
+                if (vi[u] < 0) continue;
+                uint64_t m = min(min(min(nb[u][0], nb[u][1]), min(nb[u][2], nb[u][3])), min(nb[u][4], nb[u][5]));
+                if (m == kPackInf) continue;
+                const uint64_t k = f_packed(ordf(hv[u]), m);
+                if (k != own[u]) {
+                    kb[vi[u]] = k;
+                    atomicOr((unsigned long long*)&schg[wv][vj[u]], 1ull << vb[u]);
                 }
             }
         }
-        __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (wl < nwords) {
-            const uint64_t c = schg[wv][lane];
-            cn[wl] = c;
-            any |= c != 0ull;
-        }
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t c = schg[wv][lane];
+        const bool chunk_changed = __ballot(c != 0ull) != 0ull;
+        if (chunk_changed && wl < nwords) cn[wl] = c;
+        if (lane == 0) fnx[ch0] = chunk_changed ? 1u : 0u;
+        any |= chunk_changed;
     }
     if (__ballot(any) && lane == 0 && !*(volatile uint32_t*)flag) atomicOr(flag, 1u);
 }
 template __global__ void k_frontier<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                                       const uint64_t*, uint64_t*, uint32_t*);
+                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*);
 template __global__ void k_frontier<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                                       const uint64_t*, uint64_t*, uint32_t*);
+                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*);
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
