@@ -90,6 +90,7 @@ struct ctws_handle {
     int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
     int no_descent = 0;  // CTWS_NO_DESCENT=1: flood from the seeds alone (test hook)
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
+    int verify = 0;      // CTWS_VERIFY=1: check the flood fixpoint, =2: fail on a violation (tests)
     std::vector<BlockDesc> last_desc;
     // RCCL
     ncclComm_t comm = nullptr;
@@ -822,6 +823,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         mark("flood_relax");
         // fixpoint check (exact height ties can break the descent argument): else flood again
+        if (h->verify) {
         HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
         if (pl.nd_ws == 3) k_flood_verify<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, w.counter);
         else k_flood_verify<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, w.counter);
@@ -833,6 +835,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             for (uint32_t k = 0; k < std::min(8u, h->h_counter[1]); ++k) fprintf(stderr, " %u", h->h_counter[2 + k]);
             fprintf(stderr, "\n");
         }
+        if (h->h_counter[0] && h->verify >= 2) {
+            h->err = "flood fixpoint check failed (CTWS_VERIFY=2)";
+            return CTWS_EHIP;
+        }
         if (h->h_counter[0] && !h->no_fallback) {
             fallback = 1;
             k_flood_reset<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.key, w.cls);
@@ -840,11 +846,14 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK)
                 return r;
         }
+        }
     } else {
         mark("flood_descent");
         if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK) return r;
     }
-    if (packed) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
+    // with a size filter the histogram and the filter read the labels from the packed keys
+    if (packed && (cfg->size_filter <= 0 || h->stop_after == CTWS_STOP_FLOOD))
+        k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     mark("flood");
     if (h->stop_after == CTWS_STOP_FLOOD) {
         HIPCHK(hipStreamSynchronize(h->stream));
@@ -856,7 +865,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         uint32_t* counts = (uint32_t*)w.A;
         k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
         dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 1024), nb);
-        k_hist<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, counts);
+        k_hist<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, packed ? 1 : 0, counts);
         FilterParams fp{(uint32_t)cfg->size_filter, 0, 0, 0, w.act0};
         flood_tile_dims(pl.nd_ws, packed, &fp.tz, &fp.ty, &fp.tx);
         HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
@@ -1129,6 +1138,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_TRACE")) h->trace = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_DESCENT")) h->no_descent = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * 128 * sizeof(double), hipHostMallocDefault) != hipSuccess) {

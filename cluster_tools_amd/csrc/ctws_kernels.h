@@ -97,7 +97,7 @@ __global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, 
 // k_post.hip
 __global__ void k_slice_seed_base(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
 __global__ void k_hist_zero(const BlockDesc*, const BlockStat*, uint32_t*);
-__global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
+__global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, uint32_t*);
 __global__ void k_size_filter(const BlockDesc*, const BlockStat*, FilterParams, const uint32_t*, const uint8_t*,
                               const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, int);
 __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint32_t*);

@@ -42,8 +42,18 @@ __global__ void __launch_bounds__(256) k_hist_zero(const BlockDesc* __restrict__
 // Each workgroup counts a contiguous range in an LDS histogram (labels <= n_seeds fit in
 // 16K bins) and flushes its non-zero bins with one global atomic each.
 constexpr int kHistBins = 16384;
+// label of voxel i after the flood: from the packed key (packed flood), else from lab
+__device__ __forceinline__ uint32_t flood_label(const uint32_t* lab, const uint64_t* key, int packed, int64_t i) {
+    if (packed) {
+        const uint64_t k = key[i];
+        return k == kInfKey ? 0u : (uint32_t)(k & ((1ull << 20) - 1ull));
+    }
+    return lab[i] & ~kFixedBit;
+}
+
 __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                              const uint32_t* __restrict__ lab, uint32_t* __restrict__ counts) {
+                                              const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
+                                              int packed, uint32_t* __restrict__ counts) {
     __shared__ uint32_t sh[kHistBins];
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
@@ -59,7 +69,7 @@ __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, c
     for (int64_t ib = i0; ib < i1; ib += 256) {
         const int64_t i = ib + threadIdx.x;
         const bool ok = i < i1;
-        const uint32_t l = ok ? (lab[B.base + i] & ~kFixedBit) : 0xFFFFFFFFu;
+        const uint32_t l = ok ? flood_label(lab, key, packed, B.base + i) : 0xFFFFFFFFu;
         const uint32_t l0 = __shfl(l, 0);
         const uint64_t same = __ballot(ok && l == l0);
         const uint64_t act = __ballot(ok);
@@ -90,7 +100,7 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
     BLOCK_LOOP(i, B) {
-        const uint32_t l = lab[B.base + i] & ~kFixedBit;
+        const uint32_t l = flood_label(lab, key, packed, B.base + i);
         bool keep = l != 0 && (counts[B.base + l] >= fp.size_filter || (excl && excl[B.base + l]));
         if (keep) {
             lab[B.base + i] = l | kFixedBit;

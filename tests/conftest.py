@@ -3,6 +3,9 @@ import sys
 
 import pytest
 
+# the flood's fixpoint check runs in every test and a violation is an error
+os.environ.setdefault('CTWS_VERIFY', '2')
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
