@@ -316,6 +316,22 @@ void record(ctws_handle* h, size_t idx) {
 }
 
 // ---- Gaussian passes over the active axes, z -> y -> x --------------------------------------
+#define CTWS_R12(M) M(1), M(2), M(3), M(4), M(5), M(6), M(7), M(8), M(9), M(10), M(11), M(12)
+#define CTWS_ROWR(R) &k_gauss_row_r<R>
+#define CTWS_COL32(R) &k_gauss_col_r<32, R>
+#define CTWS_COL16(R) &k_gauss_col_r<16, R>
+#define CTWS_COL8(R) &k_gauss_col_r<8, R>
+using GaussKernel = decltype(&k_gauss_row_r<1>);
+const GaussKernel kGaussRowR[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_ROWR)};
+const GaussKernel kGaussColR32[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_COL32)};
+const GaussKernel kGaussColR16[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_COL16)};
+const GaussKernel kGaussColR8[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_COL8)};
+#undef CTWS_R12
+#undef CTWS_ROWR
+#undef CTWS_COL32
+#undef CTWS_COL16
+#undef CTWS_COL8
+
 int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, const float* src, float* dst,
               int nb, int maxZ, int maxY, int maxX, HmapParams hp, int taps_slot) {
     Workspace& w = h->ws;
@@ -346,7 +362,27 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
         float* out = (i == na - 1) ? dst : ((i % 2 == 0) ? w.A : w.Bf);
         GaussParams gp{a, r, (i == 0 && hmap_src) ? 1 : 0};
         const float* in = (i == 0 && hmap_src) ? w.fin : cur;
-        if (a == 2) {
+        if (r >= 1 && r <= kGaussMaxR) {
+            // sliding-window kernels (k_gauss.hip)
+            if (a == 2) {
+                // rows per wave shrink with X: size the grid for the widest block
+                const int rpw = 64 / ((maxX + 15) / 16);
+                dim3 g((unsigned)(((int64_t)maxZ * maxY + 4 * rpw - 1) / (4 * rpw)), nb);
+                const size_t lds = 4 * 2 * (size_t)(64 * 17 + 64) * 4;
+                hipLaunchKernelGGL(kGaussRowR[r], g, dim3(256), lds, h->stream, w.desc, w.stat, gp, hp,
+                                   (const double*)dtaps, in, (const float*)w.dt, (const uint32_t*)w.smin,
+                                   (const uint32_t*)w.smax, out);
+            } else {
+                const int Lm = a == 0 ? maxZ : maxY;
+                const int other = a == 0 ? maxY : maxZ;
+                const int W = col_width(Lm);
+                dim3 g((unsigned)((int64_t)other * ((maxX + W - 1) / W)), nb);
+                const size_t lds = (size_t)Lm * W * 4;
+                auto kern = W == 32 ? kGaussColR32[r] : (W == 16 ? kGaussColR16[r] : kGaussColR8[r]);
+                hipLaunchKernelGGL(kern, g, dim3(256), lds, h->stream, w.desc, w.stat, gp, hp, (const double*)dtaps,
+                                   in, (const float*)w.dt, (const uint32_t*)w.smin, (const uint32_t*)w.smax, out);
+            }
+        } else if (a == 2) {
             dim3 g((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
             const size_t lds = 2 * 128 * 4 + 4 * (size_t)maxX * 4;
             k_gauss_row<<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax, out);

@@ -50,6 +50,13 @@ __global__ void k_gauss_col(const BlockDesc*, const BlockStat*, GaussParams, Hma
                             const float*, const uint32_t*, const uint32_t*, float*);
 __global__ void k_gauss_row(const BlockDesc*, const BlockStat*, GaussParams, HmapParams, const double*, const float*,
                             const float*, const uint32_t*, const uint32_t*, float*);
+constexpr int kGaussMaxR = 12;  // sliding-window kernels for radius <= 12 (sigma < 4)
+template <int W, int R>
+__global__ void k_gauss_col_r(const BlockDesc*, const BlockStat*, GaussParams, HmapParams, const double*, const float*,
+                              const float*, const uint32_t*, const uint32_t*, float*);
+template <int R>
+__global__ void k_gauss_row_r(const BlockDesc*, const BlockStat*, GaussParams, HmapParams, const double*, const float*,
+                              const float*, const uint32_t*, const uint32_t*, float*);
 
 // k_cc.hip
 __global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*);

@@ -158,4 +158,188 @@ __global__ void __launch_bounds__(256) k_gauss_row(const BlockDesc* __restrict__
     }
 }
 
+// =========================================================================================
+// Sliding-window variants for radius R <= kGaussMaxR (compile time).  A thread computes a run
+// of consecutive outputs and keeps the 2R+1 inputs of the current output in registers, already
+// converted to double: per output one LDS read + one conversion instead of 2R+1 of each, and
+// the taps sit in registers.  The arithmetic (double products summed over ascending source
+// positions, separate multiply and add) is exactly that of the generic kernels above.
+// =========================================================================================
+template <int R>
+__device__ __forceinline__ void load_taps(const double* __restrict__ taps, double (&k)[2 * R + 1]) {
+#pragma unroll
+    for (int j = 0; j <= 2 * R; ++j) k[j] = taps[j];
+}
+
+// out[p] for p in [p0, p1) from src(i) (i in [0, L), reflect border), written via put(p, v)
+template <int R, class Src, class Put>
+__device__ __forceinline__ void gauss_run(const double (&k)[2 * R + 1], int L, int p0, int p1, Src src, Put put) {
+    double win[2 * R + 1];
+#pragma unroll
+    for (int m = 0; m <= 2 * R; ++m) win[m] = (double)src(reflect_idx(p0 - R + m, L));
+    for (int p = p0; p < p1; ++p) {
+        double sum = 0.0;
+#pragma unroll
+        for (int m = 0; m <= 2 * R; ++m) sum += k[2 * R - m] * win[m];
+        put(p, (float)sum);
+#pragma unroll
+        for (int m = 0; m < 2 * R; ++m) win[m] = win[m + 1];
+        win[2 * R] = (double)src(reflect_idx(p + 1 + R, L));
+    }
+}
+
+template <int W, int R>
+__global__ void __launch_bounds__(256) k_gauss_col_r(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     GaussParams gp, HmapParams hp, const double* __restrict__ taps,
+                                                     const float* __restrict__ in, const float* __restrict__ dt,
+                                                     const uint32_t* smin, const uint32_t* smax,
+                                                     float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) int smem_i[];
+    float* col = (float*)smem_i;
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int nxc = (B.X + W - 1) / W;
+    const int L = (gp.axis == 1) ? B.Y : B.Z;
+    const int other = (gp.axis == 1) ? B.Z : B.Y;
+    const int t = blockIdx.x;
+    if (t >= other * nxc) return;
+    const int o = t / nxc, xc = t % nxc;
+    const int xb = xc * W;
+    const int64_t lstride = (gp.axis == 1) ? B.X : (int64_t)B.Y * B.X;
+    const int64_t obase = (gp.axis == 1) ? (int64_t)o * B.Y * B.X : (int64_t)o * B.X;
+    const int c = threadIdx.x % W;
+    const int r0 = threadIdx.x / W;
+    constexpr int RS = 256 / W;
+    const bool colok = xb + c < B.X;
+    if (gp.hmap_src) {
+        const BlockStat& st = S[blockIdx.y];
+        staged_loop<8>(
+            r0, L, RS,
+            [&](int p) {
+                const int64_t li = obase + p * lstride + xb + (colok ? c : 0);
+                return hmap_value(B, st, hp, in, dt, smin, smax, li, (gp.axis == 1) ? o : p);
+            },
+            [&](int p, float v) { col[p * W + c] = colok ? v : 0.0f; });
+    } else {
+        const float* gsrc = in + B.base + obase + xb + (colok ? c : 0);
+        staged_loop<8>(
+            r0, L, RS, [&](int p) { return gsrc[p * lstride]; },
+            [&](int p, float v) { col[p * W + c] = colok ? v : 0.0f; });
+    }
+    double k[2 * R + 1];
+    load_taps<R>(taps, k);
+    __syncthreads();
+    if (!colok) return;
+    const int seg = (L + RS - 1) / RS;
+    const int p0 = r0 * seg, p1 = min(L, p0 + seg);
+    if (p0 >= p1) return;
+    float* gdst = out + B.base + obase + xb + c;
+    gauss_run<R>(
+        k, L, p0, p1, [&](int i) { return col[i * W + c]; }, [&](int p, float v) { gdst[p * lstride] = v; });
+}
+
+// Row pass: a lane computes a run of kRowSeg consecutive x; a wave holds 64 / ceil(X / kRowSeg)
+// rows.  The rows sit in LDS with one pad word per run (stride kRowSeg + 1: no bank
+// conflicts); outputs go back through LDS so the global stores are coalesced.
+constexpr int kRowSeg = 16;
+constexpr int kRowWaveFloats = 64 * (kRowSeg + 1) + 64;  // per wave and buffer
+
+__host__ __device__ constexpr int gauss_rows_per_wave(int X) { return 64 / ((X + kRowSeg - 1) / kRowSeg); }
+
+template <int R>
+__global__ void __launch_bounds__(256) k_gauss_row_r(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     GaussParams gp, HmapParams hp, const double* __restrict__ taps,
+                                                     const float* __restrict__ in, const float* __restrict__ dt,
+                                                     const uint32_t* smin, const uint32_t* smax,
+                                                     float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) int smem_i[];
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int X = B.X;
+    const int lpr = (X + kRowSeg - 1) / kRowSeg;  // lanes per row
+    const int rpw = 64 / lpr;                      // rows per wave
+    const int pitch = X + X / kRowSeg + 1;         // padded row length in LDS
+    float* rowb = (float*)smem_i + wave * 2 * kRowWaveFloats;
+    float* outb = rowb + kRowWaveFloats;
+    auto pos = [&](int x) { return x + x / kRowSeg; };
+    const int64_t nrows = (int64_t)B.Z * B.Y;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * rpw;
+    if (row0 >= nrows) return;
+    const int nr = (int)min((int64_t)rpw, nrows - row0);
+    // stage nr rows (lane-strided, coalesced)
+    const int nval = nr * X;
+    if (gp.hmap_src) {
+        const BlockStat& st = S[blockIdx.y];
+        staged_loop<8>(
+            lane, nval, 64,
+            [&](int v) {
+                const int rr = v / X, x = v - rr * X;
+                const int64_t row = row0 + rr;
+                return hmap_value(B, st, hp, in, dt, smin, smax, row * X + x, (int)(row / B.Y));
+            },
+            [&](int v, float val) {
+                const int rr = v / X, x = v - rr * X;
+                rowb[rr * pitch + pos(x)] = val;
+            });
+    } else {
+        const float* gsrc = in + B.base + row0 * X;
+        staged_loop<8>(
+            lane, nval, 64, [&](int v) { return gsrc[v]; },
+            [&](int v, float val) {
+                const int rr = v / X, x = v - rr * X;
+                rowb[rr * pitch + pos(x)] = val;
+            });
+    }
+    double k[2 * R + 1];
+    load_taps<R>(taps, k);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int rr = lane / lpr, sidx = lane - rr * lpr;
+    if (rr < nr) {
+        const int p0 = sidx * kRowSeg, p1 = min(X, p0 + kRowSeg);
+        const float* rb = rowb + rr * pitch;
+        float* ob = outb + rr * pitch;
+        if (p0 < p1)
+            gauss_run<R>(
+                k, X, p0, p1, [&](int i) { return rb[pos(i)]; }, [&](int p, float v) { ob[pos(p)] = v; });
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float* gdst = out + B.base + row0 * X;
+    for (int v = lane; v < nval; v += 64) {
+        const int r2 = v / X, x = v - r2 * X;
+        gdst[v] = outb[r2 * pitch + pos(x)];
+    }
+}
+
+#define CTWS_GAUSS_R(R)                                                                                          \
+    template __global__ void k_gauss_col_r<32, R>(const BlockDesc*, const BlockStat*, GaussParams, HmapParams,      \
+                                                  const double*, const float*, const float*, const uint32_t*,       \
+                                                  const uint32_t*, float*);                                        \
+    template __global__ void k_gauss_col_r<16, R>(const BlockDesc*, const BlockStat*, GaussParams, HmapParams,      \
+                                                  const double*, const float*, const float*, const uint32_t*,       \
+                                                  const uint32_t*, float*);                                        \
+    template __global__ void k_gauss_col_r<8, R>(const BlockDesc*, const BlockStat*, GaussParams, HmapParams,       \
+                                                 const double*, const float*, const float*, const uint32_t*,        \
+                                                 const uint32_t*, float*);                                         \
+    template __global__ void k_gauss_row_r<R>(const BlockDesc*, const BlockStat*, GaussParams, HmapParams,          \
+                                              const double*, const float*, const float*, const uint32_t*,           \
+                                              const uint32_t*, float*);
+CTWS_GAUSS_R(1)
+CTWS_GAUSS_R(2)
+CTWS_GAUSS_R(3)
+CTWS_GAUSS_R(4)
+CTWS_GAUSS_R(5)
+CTWS_GAUSS_R(6)
+CTWS_GAUSS_R(7)
+CTWS_GAUSS_R(8)
+CTWS_GAUSS_R(9)
+CTWS_GAUSS_R(10)
+CTWS_GAUSS_R(11)
+CTWS_GAUSS_R(12)
+#undef CTWS_GAUSS_R
+
 }  // namespace ctws
