@@ -731,20 +731,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     mark("hmap");
 
     // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
-    k_localmax<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls);
+    k_localmax<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
     LAUNCHCHK();
-    k_plateau_init<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
     k_plateau_union<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
     k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
     k_seed_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF);
     k_seed_union<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF);
-    k_flatten<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF);
     HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-    k_roots_bitmap<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
+    k_flatten_roots<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
     k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
-    k_root_label<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.Wp);
+    k_root_label<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.Wp);
     const dim3 gsb((unsigned)((maxZ + 255) / 256), nb);
     if (pl.pass2) {
         // _apply_watershed_with_seeds: shifted seeds + initial seeds, relabelConsecutive
@@ -777,6 +775,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
     }
     uint8_t* excl = nullptr;
+    const bool descent = packed && !h->no_descent;
+    const bool cc_seeds = descent && !pl.pass2 && h->stop_after != CTWS_STOP_SEEDS;
+    const uint32_t* cc = cc_seeds ? w.PF : nullptr;
     if (pl.pass2) {
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
         k_p2_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
@@ -785,7 +786,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_p2_excl_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, excl);
         k_p2_excl<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, excl);
     } else {
-        k_seed_label<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.hm, w.lab, w.key, w.cls, packed ? 1 : 0);
+        // the descent flood reads the seeds from the CC parents directly (cc_seeds)
+        if (!cc_seeds)
+            k_seed_label<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.hm, w.lab, w.key, w.cls, packed ? 1 : 0);
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
     }
     LAUNCHCHK();
@@ -800,21 +803,22 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     h->flood_tiles = h->flood_iters = h->flood_lines = 0;
     float fk1 = 0.f, fk2 = 0.f;
     int fallback = 0, fiters = 0;
-    if (packed && !h->no_descent) {
+    if (descent) {
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
         {
             // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
             const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;
             const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
-            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P);
-            else k_descent_tile<2><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P);
+            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
+            else k_descent_tile<2><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
             LAUNCHCHK();
         }
         mark("descent_tile");
         int TZ, TY, TX;
         flood_tile_dims(pl.nd_ws, true, &TZ, &TY, &TX);
         HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-        k_descent_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.P, w.key, w.cls, w.fopen, w.front0);
+        k_descent_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P, w.key, w.cls, w.fopen,
+                                                  w.front0);
         LAUNCHCHK();
         mark("flood_descent");
         // frontier relaxation of the remaining voxels (k_frontier, one voxel per lane)
@@ -861,8 +865,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // fixpoint check (exact height ties can break the descent argument): else flood again
         if (h->verify) {
         HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
-        if (pl.nd_ws == 3) k_flood_verify<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, w.counter);
-        else k_flood_verify<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, w.counter);
+        if (pl.nd_ws == 3) k_flood_verify<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
+        else k_flood_verify<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
         LAUNCHCHK();
         HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
@@ -877,7 +881,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         if (h->h_counter[0] && !h->no_fallback) {
             fallback = 1;
-            k_flood_reset<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, w.key, w.cls);
+            k_flood_reset<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.key, w.cls);
             LAUNCHCHK();
             if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK)
                 return r;
@@ -887,8 +891,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         mark("flood_descent");
         if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK) return r;
     }
-    // with a size filter the histogram and the filter read the labels from the packed keys
-    if (packed && (cfg->size_filter <= 0 || h->stop_after == CTWS_STOP_FLOOD))
+    // the histogram, the filter and (pass 1) the final labels read the packed keys directly
+    const bool unpack_final = packed && pl.pass2;
+    if (packed && (h->stop_after == CTWS_STOP_FLOOD || (cfg->size_filter <= 0 && unpack_final)))
         k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     mark("flood");
     if (h->stop_after == CTWS_STOP_FLOOD) {
@@ -900,7 +905,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     if (cfg->size_filter > 0) {
         uint32_t* counts = (uint32_t*)w.A;
         k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
-        dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 1024), nb);
+        dim3 hg((unsigned)std::min<int64_t>((maxN + 8191) / 8192, 2048), nb);
         k_hist<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, packed ? 1 : 0, counts);
         FilterParams fp{(uint32_t)cfg->size_filter, 0, 0, 0, w.act0};
         flood_tile_dims(pl.nd_ws, packed, &fp.tz, &fp.ty, &fp.tx);
@@ -909,14 +914,15 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                                                  w.surv, packed ? 1 : 0);
         LAUNCHCHK();
         if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds2, &fk2)) != CTWS_OK) return r;
-        if (packed) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
+        if (unpack_final) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     }
     mark("size_filter");
+    const int keys_final = (packed && !unpack_final) ? 1 : 0;  // final labels still in the keys
 
     // ---- pass 2: per-slice offsets, takeDict, uncropped inner write --------------------------
     if (pl.pass2) {
         if (pl.nd_ws == 2) {
-            k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.sb, w.slmax);
+            k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, 0, w.sb, w.slmax);
             k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
             k_p2_check<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.soff, w.p2err);
         }
@@ -931,10 +937,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     } else {
     // ---- 2-D offsets / mask -> final uint32 ws ---------------------------------------------
     if (pl.nd_ws == 2) {
-        k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.sb, w.slmax);
+        k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.sb, w.slmax);
         k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
     }
-    k_finalize_ws<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, w.soff, w.lab);
+    k_finalize_ws<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, w.soff, w.key, keys_final, w.lab);
     LAUNCHCHK();
     mark("finalize");
     if (h->stop_after == CTWS_STOP_WS) {
@@ -949,13 +955,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
         k_crop_init<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
         k_crop_union<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
-        k_flatten<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF);
         HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-        k_roots_bitmap<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
+        k_flatten_roots<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
         k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
         k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
         k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
-        k_root_label<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp);
+        k_root_label<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp);
         LAUNCHCHK();
     }
     mark("crop_cc");

@@ -59,14 +59,12 @@ __global__ void k_gauss_row_r(const BlockDesc*, const BlockStat*, GaussParams, H
                               const float*, const uint32_t*, const uint32_t*, float*);
 
 // k_cc.hip
-__global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*);
-__global__ void k_plateau_init(const BlockDesc*, const BlockStat*, const uint8_t*, uint32_t*);
+__global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, uint32_t*);
 __global__ void k_plateau_union(const BlockDesc*, const BlockStat*, const float*, const uint8_t*, uint32_t*);
 __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uint32_t*);
 __global__ void k_seed_init(const BlockDesc*, const BlockStat*, const uint8_t*, const uint32_t*, uint32_t*);
 __global__ void k_seed_union(const BlockDesc*, const BlockStat*, uint32_t*);
-__global__ void k_flatten(const BlockDesc*, const BlockStat*, int, uint32_t*);
-__global__ void k_roots_bitmap(const BlockDesc*, const BlockStat*, int, const uint32_t*, uint64_t*);
+__global__ void k_flatten_roots(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
 __global__ void k_bitmap_csum(const BlockDesc*, const BlockStat*, int, const uint64_t*, uint32_t*);
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
 __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uint64_t*, const uint32_t*, uint32_t*);
@@ -89,17 +87,19 @@ constexpr int kLineWords = 24;
 constexpr int kStatSlots = 64;  // flood statistics: counter[4 + slot * 4 + k]  // per tile: 8 words of line bits for each of x, y, z
 __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
 template <int ND>
-__global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint32_t*);
+__global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
+                               uint32_t*);
 __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
-                               uint64_t*, uint8_t*, uint64_t*, uint64_t*);
+                               const uint32_t*, uint64_t*, uint8_t*, uint64_t*, uint64_t*);
 template <int ND>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>
 __global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint32_t*,
-                               uint32_t*);
-__global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint8_t*);
+                               const uint32_t*, uint32_t*);
+__global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
+                              uint64_t*, uint8_t*);
 
 // k_post.hip
 __global__ void k_slice_seed_base(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
@@ -107,9 +107,11 @@ __global__ void k_hist_zero(const BlockDesc*, const BlockStat*, uint32_t*);
 __global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, uint32_t*);
 __global__ void k_size_filter(const BlockDesc*, const BlockStat*, FilterParams, const uint32_t*, const uint8_t*,
                               const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, int);
-__global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint32_t*);
+__global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
+                            uint32_t*);
 __global__ void k_slice_offsets(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
-__global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint32_t*);
+__global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, const uint64_t*, int,
+                              uint32_t*);
 
 // k_pass2.hip (two-pass watershed, pass 2)
 __global__ void k_p2_zero_dt(const BlockDesc*, const BlockStat*, float*);

@@ -81,7 +81,8 @@ __device__ __forceinline__ void uf_union_scan(uint32_t* P, uint32_t a, uint32_t 
 // cls bit0: a neighbour is strictly greater; bit1: a neighbour is equal (plateau voxel).
 // Neighbourhood: 6 (3-D ws) or 8 in-plane (2-D ws), as localMaxima3D / localMaxima.
 __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ D, BlockStat* S,
-                                                  const float* __restrict__ v, uint8_t* __restrict__ cls) {
+                                                  const float* __restrict__ v, uint8_t* __restrict__ cls,
+                                                  uint32_t* __restrict__ Pp) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int Y = B.Y, X = B.X, Z = B.Z;
@@ -118,6 +119,7 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
             eq |= w[k] == c;
         }
         cl[i] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
+        if (eq) Pp[B.base + i] = (uint32_t)i;  // plateau union-find init
         nplat += eq;
     })
     nplat = wg_reduce_u32(nplat, OpAdd());
@@ -125,15 +127,6 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
 }
 
 // ---- plateau resolution: CC of equal values over plateau voxels (C-order keys) -----------
-__global__ void __launch_bounds__(256) k_plateau_init(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                      const uint8_t* __restrict__ cls, uint32_t* __restrict__ P) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || !S[blockIdx.y].plateau) return;
-    BLOCK_LOOP(i, B) {
-        if (cls[B.base + i] & 2) P[B.base + i] = (uint32_t)i;
-    }
-}
-
 __global__ void __launch_bounds__(256) k_plateau_union(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                        const float* __restrict__ v, const uint8_t* __restrict__ cls,
                                                        uint32_t* __restrict__ Pg) {
@@ -231,21 +224,6 @@ __global__ void __launch_bounds__(256) k_seed_union(const BlockDesc* __restrict_
 // keys per block: n = N (seeds, outer) or NI (crop, inner); words = n/64 + 1, chunks of 256
 // words.  inner != 0 selects NI and the inner-sized parent array offset (ibase).  W must be
 // zeroed beforehand.
-__global__ void __launch_bounds__(256) k_roots_bitmap(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
-                                                      const uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || (inner && !B.crop)) return;
-    const uint32_t* P = PFg + (inner ? B.ibase : B.base);
-    uint64_t* W = Wg + B.wbase;
-    const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
-    ROW_TILES(nz, ny, nx, {
-        if (P[i] == (uint32_t)i) {
-            const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
-            atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
-        }
-    })
-}
-
 // popcount sums of 256-word chunks
 __global__ void __launch_bounds__(256) k_bitmap_csum(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
                                                      const uint64_t* __restrict__ Wg, uint32_t* __restrict__ csum) {
@@ -320,20 +298,40 @@ __global__ void __launch_bounds__(256) k_word_prefix(const BlockDesc* __restrict
     if (w < nw) Wp[B.wbase + w] = csum[B.cbase + blockIdx.x] + woff + x - v;
 }
 
-// roots: slot <- (1 + rank of the root's scan key) | kRootBit (after k_flatten)
+// roots: slot <- (1 + rank of the root's scan key) | kRootBit, walking the set bits of the
+// root bitmap (roots are few: no pass over the voxels)
 __global__ void __launch_bounds__(256) k_root_label(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
                                                     uint32_t* __restrict__ PFg, const uint64_t* __restrict__ Wg,
                                                     const uint32_t* __restrict__ Wpg) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || (inner && !B.crop)) return;
     uint32_t* P = PFg + (inner ? B.ibase : B.base);
+    const int64_t n = inner ? B.NI : B.N;
+    const int64_t nw = n / 64 + 1;
     const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
-    ROW_TILES(nz, ny, nx, {
-        if (P[i] == (uint32_t)i) {
-            const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
-            P[i] = (bitmap_rank(Wg + B.wbase, Wpg + B.wbase, f) + 1u) | kRootBit;
+    const int64_t yx = (int64_t)ny * nx;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t bits = Wg[B.wbase + w];
+        uint32_t rank = Wpg[B.wbase + w];
+        while (bits) {
+            const int b = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            const int64_t f = w * 64 + b;
+            int z, y, x;
+            if (inner || B.nd_ws == 3) {  // f = z + nz * (y + ny * x)
+                z = (int)(f % nz);
+                const int64_t t = f / nz;
+                y = (int)(t % ny);
+                x = (int)(t / ny);
+            } else {  // f = z * Y * X + y + Y * x
+                z = (int)(f / yx);
+                const int64_t rem = f - (int64_t)z * yx;
+                y = (int)(rem % ny);
+                x = (int)(rem / ny);
+            }
+            P[((int64_t)z * ny + y) * nx + x] = (++rank) | kRootBit;
         }
-    })
+    }
 }
 
 // ---- seed labels + flood initialisation --------------------------------------------------
@@ -412,17 +410,24 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
     if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);
 }
 
-// point every element of a union-find forest directly at its root
-__global__ void __launch_bounds__(256) k_flatten(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
-                                                 uint32_t* __restrict__ PFg) {
+// point every element of a union-find forest directly at its root; roots set their scan-key
+// bit in the root bitmap W (zeroed beforehand)
+__global__ void __launch_bounds__(256) k_flatten_roots(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
+                                                       uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || (inner && !B.crop)) return;
-    const int64_t n = inner ? B.NI : B.N;
     uint32_t* P = PFg + (inner ? B.ibase : B.base);
-    for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n; f += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t p = P[f];
-        if (p != kNoParent && p != (uint32_t)f) P[f] = uf_find(P, p);
-    }
+    uint64_t* W = Wg + B.wbase;
+    const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
+    ROW_TILES(nz, ny, nx, {
+        const uint32_t p = P[i];
+        if (p == (uint32_t)i) {
+            const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
+            atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
+        } else if (p != kNoParent) {
+            P[i] = uf_find(P, p);
+        }
+    })
 }
 
 }  // namespace ctws

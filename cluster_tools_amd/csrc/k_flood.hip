@@ -521,8 +521,7 @@ __global__ void __launch_bounds__(256) k_unpack_labels(const BlockDesc* __restri
     if (!S[blockIdx.y].active) return;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t k = key[B.base + i];
-        const uint32_t l = (k == kPackInf) ? 0u : (uint32_t)(k & kLabelMask);
-        lab[B.base + i] = (lab[B.base + i] & kFixedBit) | l;
+        lab[B.base + i] = (k == kPackInf) ? 0u : (uint32_t)(k & kLabelMask);
     }
 }
 
@@ -551,6 +550,17 @@ namespace ctws {
 // or the first voxel outside it.  exit[q] = that voxel (block C-order index); chains that
 // leave the tile are finished by k_descent_init following exit[] across tiles (a hop per tile
 // crossed).  One pass over the volume instead of a global pointer-jumping pass per doubling.
+// seed test / seed label: from the seed CC parents (pass 1: `cc` = PF after k_root_label) or,
+// when cc is null, from lab (kFixedBit; pass 2 and the fallbacks)
+__device__ __forceinline__ bool is_seed(const uint32_t* lab, const uint32_t* cc, int64_t gi) {
+    return cc ? cc[gi] != kNoParent : (lab[gi] & kFixedBit) != 0;
+}
+__device__ __forceinline__ uint32_t seed_label(const uint32_t* lab, const uint32_t* cc, int64_t base, uint32_t r) {
+    if (cc) return cc_label(cc + base, cc[base + r]);
+    const uint32_t l = lab[base + r];
+    return (l & kFixedBit) ? (l & ~kFixedBit) : 0u;
+}
+
 template <int ND>
 struct DTile;
 template <>
@@ -565,7 +575,7 @@ struct DTile<2> {
 template <int ND>
 __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint32_t* __restrict__ lab,
-                                                      uint32_t* __restrict__ exitp) {
+                                                      const uint32_t* __restrict__ cc, uint32_t* __restrict__ exitp) {
     using T = DTile<ND>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, HZ = T::HZ, HY = TY + 2, HX = TX + 2;
     constexpr int HN = HZ * HY * HX, TN = TZ * TY * TX;
@@ -596,7 +606,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
         int p = c;
-        if (gz < B.Z && gy < B.Y && gx < B.X && !(lab[B.base + gz * YX + (int64_t)gy * B.X + gx] & kFixedBit)) {
+        if (gz < B.Z && gy < B.Y && gx < B.X && !is_seed(lab, cc, B.base + gz * YX + (int64_t)gy * B.X + gx)) {
             const int hc = ((lz + ZOFF) * HY + ly + 1) * HX + lx + 1;
             uint32_t best = sh[hc];
             int bh = -1;
@@ -662,9 +672,9 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     }
 }
 template __global__ void k_descent_tile<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                           uint32_t*);
+                                           const uint32_t*, uint32_t*);
 template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                           uint32_t*);
+                                           const uint32_t*, uint32_t*);
 
 // voxels whose descent ends in a seed get their final key, fixed; the others wait for the
 // flood (INF key).  Bitmaps, one word per 64 voxels of a row (the 64 lanes of a wave cover
@@ -672,6 +682,7 @@ template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, c
 // neighbours form the first frontier).
 __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint32_t* __restrict__ lab,
+                                                      const uint32_t* __restrict__ cc,
                                                       const uint32_t* __restrict__ par, uint64_t* __restrict__ key,
                                                       uint8_t* __restrict__ fixedv, uint64_t* __restrict__ open,
                                                       uint64_t* __restrict__ chg) {
@@ -692,9 +703,9 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
                     if (n == r) break;
                     r = n;
                 }
-                const uint32_t lr = lab[B.base + r];
-                const bool res = (lr & kFixedBit) != 0;
-                key[gi] = res ? (((uint64_t)ordf(h[gi]) << 32) | (uint64_t)(lr & (uint32_t)kLabelMask)) : kPackInf;
+                const uint32_t lr = seed_label(lab, cc, B.base, r);
+                const bool res = lr != 0;
+                key[gi] = res ? (((uint64_t)ordf(h[gi]) << 32) | (uint64_t)lr) : kPackInf;
                 fixedv[gi] = res ? 1 : 0;
                 const uint64_t op = __ballot(!res);
                 const uint64_t fi = __ballot(res);
@@ -911,7 +922,8 @@ __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restr
 template <int ND>
 __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint64_t* __restrict__ key,
-                                                      const uint32_t* __restrict__ lab, uint32_t* __restrict__ flag) {
+                                                      const uint32_t* __restrict__ lab, const uint32_t* __restrict__ cc,
+                                                      uint32_t* __restrict__ flag) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const uint64_t* k = key + B.base;
@@ -936,7 +948,7 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
                 if (x > 0) m = min(m, k[i - 1]);
                 if (x + 1 < B.X) m = min(m, k[i + 1]);
                 const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(h[B.base + i]), m);
-                const bool b1 = !(lab[B.base + i] & kFixedBit) && e != k[i];
+                const bool b1 = !is_seed(lab, cc, B.base + i) && e != k[i];
                 if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
                     const uint32_t slot = atomicAdd(&flag[1], 1u);
                     if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + i);
@@ -947,21 +959,21 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 template __global__ void k_flood_verify<3>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
-                                           const uint32_t*, uint32_t*);
+                                           const uint32_t*, const uint32_t*, uint32_t*);
 template __global__ void k_flood_verify<2>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
-                                           const uint32_t*, uint32_t*);
+                                           const uint32_t*, const uint32_t*, uint32_t*);
 
 // seeds only (fallback after a failed verification)
 __global__ void __launch_bounds__(256) k_flood_reset(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                      const float* __restrict__ h, const uint32_t* __restrict__ lab,
-                                                     uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv) {
+                                                     const uint32_t* __restrict__ cc, uint64_t* __restrict__ key,
+                                                     uint8_t* __restrict__ fixedv) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t l = lab[B.base + i];
-        const bool s = (l & kFixedBit) != 0;
-        key[B.base + i] = s ? (((uint64_t)ordf(h[B.base + i]) << 32) | (uint64_t)(l & (uint32_t)kLabelMask)) : kPackInf;
-        fixedv[B.base + i] = s ? 1 : 0;
+        const uint32_t l = seed_label(lab, cc, B.base, (uint32_t)i);
+        key[B.base + i] = l ? (((uint64_t)ordf(h[B.base + i]) << 32) | (uint64_t)l) : kPackInf;
+        fixedv[B.base + i] = l ? 1 : 0;
     }
 }
 

@@ -66,21 +66,31 @@ __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, c
     const int64_t chunk = ((B.N + gridDim.x - 1) / gridDim.x + 255) & ~(int64_t)255;
     const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = min(B.N, i0 + chunk);
     const int lane = threadIdx.x & 63;
-    for (int64_t ib = i0; ib < i1; ib += 256) {
-        const int64_t i = ib + threadIdx.x;
-        const bool ok = i < i1;
-        const uint32_t l = ok ? flood_label(lab, key, packed, B.base + i) : 0xFFFFFFFFu;
-        const uint32_t l0 = __shfl(l, 0);
-        const uint64_t same = __ballot(ok && l == l0);
-        const uint64_t act = __ballot(ok);
-        if (same == act) {
-            if (lane == 0 && act) {
-                if (use_lds) atomicAdd(&sh[l0], (uint32_t)__popcll(act));
-                else atomicAdd(&c[l0], (uint32_t)__popcll(act));
+    constexpr int U = 8;  // loads in flight per thread
+    for (int64_t ib = i0; ib < i1; ib += 256 * U) {
+        uint32_t lv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = ib + u * 256 + threadIdx.x;
+            lv[u] = i < i1 ? flood_label(lab, key, packed, B.base + i) : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t l = lv[u];
+            const bool ok = l != 0xFFFFFFFFu;
+            // a wave of equal labels (the common case) costs one atomic
+            const uint32_t l0 = __shfl(l, 0);
+            const uint64_t same = __ballot(ok && l == l0);
+            const uint64_t act = __ballot(ok);
+            if (same == act) {
+                if (lane == 0 && act) {
+                    if (use_lds) atomicAdd(&sh[l0], (uint32_t)__popcll(act));
+                    else atomicAdd(&c[l0], (uint32_t)__popcll(act));
+                }
+            } else if (ok) {
+                if (use_lds) atomicAdd(&sh[l], 1u);
+                else atomicAdd(&c[l], 1u);
             }
-        } else if (ok) {
-            if (use_lds) atomicAdd(&sh[l], 1u);
-            else atomicAdd(&c[l], 1u);
         }
     }
     if (!use_lds) return;
@@ -103,13 +113,13 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
         const uint32_t l = flood_label(lab, key, packed, B.base + i);
         bool keep = l != 0 && (counts[B.base + l] >= fp.size_filter || (excl && excl[B.base + l]));
         if (keep) {
-            lab[B.base + i] = l | kFixedBit;
+            if (!packed) lab[B.base + i] = l | kFixedBit;
             key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
             fixedv[B.base + i] = 1;
             const int z = (B.nd_ws == 2) ? (int)(i / YX) : 0;
             if (!survivors[B.sbase + z]) survivors[B.sbase + z] = 1;
         } else {
-            lab[B.base + i] = 0;
+            if (!packed) lab[B.base + i] = 0;
             key[B.base + i] = kInfKey;
             fixedv[B.base + i] = 0;
             // only tiles with a free voxel can change in the regrow flood
@@ -123,7 +133,8 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
 // per-slice max_id (2-D ws): max per-slice label over in-mask voxels (all voxels without a
 // mask).  Equals watershedsNew's maxRegionLabel of the (regrow) flood when unmasked.
 __global__ void __launch_bounds__(256) k_slice_max(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                   const uint32_t* __restrict__ lab, const uint32_t* __restrict__ sb,
+                                                   const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
+                                                   int packed, const uint32_t* __restrict__ sb,
                                                    uint32_t* __restrict__ smax) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || B.nd_ws != 2) return;
@@ -134,7 +145,7 @@ __global__ void __launch_bounds__(256) k_slice_max(const BlockDesc* __restrict__
         int z = -1;
         if (i < B.N) {
             z = (int)(i / YX);
-            const uint32_t l = lab[B.base + i] & ~kFixedBit;
+            const uint32_t l = flood_label(lab, key, packed, B.base + i);
             if (l && (!B.mask || B.mask[i])) v = l - sb[B.sbase + z];
         }
         // one atomic per wave when the wave lies in one slice (the common case)
@@ -164,12 +175,13 @@ __global__ void k_slice_offsets(const BlockDesc* __restrict__ D, const BlockStat
 // 2-D: per-slice label + slice offset, masked -> 0 (:220-237)
 __global__ void __launch_bounds__(256) k_finalize_ws(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                      const uint32_t* __restrict__ sb, const uint32_t* __restrict__ soff,
+                                                     const uint64_t* __restrict__ key, int packed,
                                                      uint32_t* __restrict__ lab) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
     BLOCK_LOOP(i, B) {
-        uint32_t l = lab[B.base + i] & ~kFixedBit;
+        uint32_t l = flood_label(lab, key, packed, B.base + i);
         const bool inm = !B.mask || B.mask[i];
         if (B.nd_ws == 2) {
             const int z = (int)(i / YX);
