@@ -34,6 +34,13 @@ CONFIG2 = dict(shape=(512, 512, 512), block_shape=(64, 256, 256), halo=(0, 0, 0)
 STAGE_BYTES = {'prep_edt_x': 12, 'edt_yz': 20, 'smooth_seeds': 24, 'hmap': 28, 'seeds': 16,
                'flood': 12, 'size_filter': 16}
 INNER_BYTES = 12  # crop / CC / offset / uint64 write, per inner voxel
+# library timing marks (HIP events on the library's stream) -> pipeline stages
+STAGE_PARTS = {'flood': ('descent_tile', 'flood_descent', 'flood_relax', 'flood'),
+               'output': ('finalize', 'crop_cc', 'output')}
+STAGE_KERNELS = {'prep_edt_x': 'k_input_minmax + k_prep_edt_x', 'edt_yz': 'k_edt_col (y, z)',
+                 'smooth_seeds': 'k_gauss_col_r (z, y) + k_gauss_row_r', 'hmap': 'k_gauss_col_r + k_gauss_row_r',
+                 'seeds': 'k_localmax ... k_root_label', 'flood': 'k_descent_tile + k_descent_init + k_frontier',
+                 'size_filter': 'k_hist + k_size_filter + regrow flood', 'output': 'k_finalize_ws + k_output'}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -164,11 +171,18 @@ def main():
     ms_per_step = dt / args.steps * 1e3
 
     # roofline of the dominant kernel (by time, HIP events inside the library)
-    kern = {k: v for k, v in stage_ms.items() if k in STAGE_BYTES}
-    dom = max(kern, key=kern.get)
-    dom_ms = kern[dom]
-    if dom in ('flood', 'size_filter') and stage_ms.get(dom + '_kernel_ms'):
-        dom_ms = stage_ms[dom + '_kernel_ms']
+    stages = {}
+    for k in STAGE_BYTES:
+        stages[k] = sum(stage_ms.get(p, 0.0) for p in STAGE_PARTS.get(k, (k,)))
+    stages['output'] = sum(stage_ms.get(p, 0.0) for p in STAGE_PARTS['output'])
+    stage_bytes = dict(STAGE_BYTES)
+    stage_gbs = {}
+    for k, ms in stages.items():
+        b = stage_bytes[k] * outer_vox if k in stage_bytes else INNER_BYTES * inner_vox
+        stage_gbs[k] = round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
+    # roofline of the dominant stage by time (algorithmic bytes / its HIP-event time)
+    dom = max(STAGE_BYTES, key=lambda k: stages[k])
+    dom_ms = stages[dom]
     achieved = STAGE_BYTES[dom] * outer_vox / (dom_ms * 1e-3) / 1e9
     alg_total = sum(STAGE_BYTES.values()) * outer_vox + INNER_BYTES * inner_vox
     pipe = alg_total / (ms_per_step * 1e-3) / 1e9
@@ -183,13 +197,15 @@ def main():
                                    '3-D DT watershed, size_filter 25',
                        'volume': list(cfg['shape']), 'block_shape': list(cfg['block_shape']),
                        'blocks_per_gpu': len(blocks), 'parallelism': 'blocks sharded, %d GPU(s)' % world},
-            'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+            'roofline': {'bound': 'hbm', 'kernel': '%s (%s)' % (dom, STAGE_KERNELS[dom]),
+                         'ms_per_step': round(dom_ms, 3), 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
                          'alg_bytes_per_outer_voxel': STAGE_BYTES[dom]},
             'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(alg_total / inner_vox, 1),
                                   'achieved': round(pipe, 1), 'unit': 'GB/s',
                                   'frac': round(pipe / HBM_PEAK_GBS, 4)},
             'stage_ms': {k: round(v, 3) for k, v in stage_ms.items()},
+            'stage_gbs': stage_gbs,
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
