@@ -940,7 +940,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.sb, w.slmax);
         k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
     }
-    k_finalize_ws<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, w.soff, w.key, keys_final, w.lab);
+    bool any_crop = false;
+    for (int i = 0; i < nb; ++i) any_crop |= desc[i].crop != 0;
+    // without a crop the final labels are computed by k_output itself
+    const int direct = (!any_crop && h->stop_after != CTWS_STOP_WS) ? 1 : 0;
+    if (!direct) k_finalize_ws<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, w.soff, w.key, keys_final, w.lab);
     LAUNCHCHK();
     mark("finalize");
     if (h->stop_after == CTWS_STOP_WS) {
@@ -949,8 +953,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
 
     // ---- halo crop CC + uint64 output -------------------------------------------------------
-    bool any_crop = false;
-    for (int i = 0; i < nb; ++i) any_crop |= desc[i].crop != 0;
     if (any_crop) {
         const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
         k_crop_init<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
@@ -964,7 +966,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         LAUNCHCHK();
     }
     mark("crop_cc");
-    k_output<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
+    k_output<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF, direct, w.key, direct ? keys_final : 0, w.sb,
+                                         w.soff);
     LAUNCHCHK();
     mark("output");
     }

@@ -163,6 +163,15 @@ __device__ __forceinline__ void staged_loop(int begin, int end, int step, LoadF 
     for (; p < end; p += step) st(p, ld(p));
 }
 
+// label of voxel i after the flood: from the packed key (packed flood), else from lab
+__device__ __forceinline__ uint32_t flood_label(const uint32_t* lab, const uint64_t* key, int packed, int64_t i) {
+    if (packed) {
+        const uint64_t k = key[i];
+        return k == kInfKey ? 0u : (uint32_t)(k & ((1ull << 20) - 1ull));
+    }
+    return lab[i] & ~kFixedBit;
+}
+
 // rank of key f among set bits of a per-block bitmap with per-word exclusive prefix
 __device__ __forceinline__ uint32_t bitmap_rank(const uint64_t* W, const uint32_t* Wp, uint32_t f) {
     uint32_t w = f >> 6;

@@ -73,7 +73,8 @@ __global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*
                              uint8_t*, int);
 __global__ void k_crop_init(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_crop_union(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
-__global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*);
+__global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*, int, const uint64_t*, int,
+                         const uint32_t*, const uint32_t*);
 
 // k_flood.hip
 template <int ND>

@@ -387,8 +387,13 @@ __global__ void __launch_bounds__(256) k_crop_union(const BlockDesc* __restrict_
 }
 
 // ---- uint64 output: (crop CC label | ws) + id offset on in-mask voxels ---------------------
+// direct != 0 (no block of the batch is cropped): the final ws label is computed here from the
+// flood result as k_finalize_ws would (3-D: masked -> 0; 2-D: per-slice label + slice offset),
+// saving that pass
 __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D, BlockStat* S,
-                                                const uint32_t* __restrict__ ws, const uint32_t* __restrict__ PFg) {
+                                                const uint32_t* __restrict__ ws, const uint32_t* __restrict__ PFg,
+                                                int direct, const uint64_t* __restrict__ key, int packed,
+                                                const uint32_t* __restrict__ sb, const uint32_t* __restrict__ soff) {
     const BlockDesc& B = D[blockIdx.y];
     const bool active = S[blockIdx.y].active;
     const uint32_t* P = PFg + B.ibase;
@@ -399,8 +404,15 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
         const bool inm = !B.mask || B.mask[o];
         uint64_t v = 0;  // empty block: constant offset (watershed.py:310-321)
         if (active) {
-            uint32_t l = ws[B.base + o];
-            if (B.crop && l) l = cc_label(P, P[i]);
+            uint32_t l;
+            if (direct) {
+                l = flood_label(ws, key, packed, B.base + o);
+                if (!inm) l = 0;
+                else if (B.nd_ws == 2) l = (l - sb[B.sbase + z + B.iz0]) + soff[B.sbase + z + B.iz0];
+            } else {
+                l = ws[B.base + o];
+                if (B.crop && l) l = cc_label(P, P[i]);
+            }
             mx = max(mx, l);
             v = l;
         }

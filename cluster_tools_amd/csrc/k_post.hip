@@ -42,15 +42,6 @@ __global__ void __launch_bounds__(256) k_hist_zero(const BlockDesc* __restrict__
 // Each workgroup counts a contiguous range in an LDS histogram (labels <= n_seeds fit in
 // 16K bins) and flushes its non-zero bins with one global atomic each.
 constexpr int kHistBins = 16384;
-// label of voxel i after the flood: from the packed key (packed flood), else from lab
-__device__ __forceinline__ uint32_t flood_label(const uint32_t* lab, const uint64_t* key, int packed, int64_t i) {
-    if (packed) {
-        const uint64_t k = key[i];
-        return k == kInfKey ? 0u : (uint32_t)(k & ((1ull << 20) - 1ull));
-    }
-    return lab[i] & ~kFixedBit;
-}
-
 __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, const BlockStat* S,
                                               const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
                                               int packed, uint32_t* __restrict__ counts) {
