@@ -27,8 +27,26 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-CONFIG2 = dict(shape=(512, 512, 512), block_shape=(64, 256, 256), halo=(0, 0, 0),
-               task=dict(apply_dt_2d=False, apply_ws_2d=False))
+# BASELINE.json configs; the driver's line is config 2 (configs[1]).  The
+# others run with --config N as single-GPU shares (config 5: the central z-slab of 8).
+D3 = dict(apply_dt_2d=False, apply_ws_2d=False)
+CONFIGS = {
+    2: dict(shape=(512, 512, 512), block_shape=(64, 256, 256), halo=(0, 0, 0), task=dict(D3),
+            workload='config2: synthetic 512^3 f32 boundary map, 64x256x256 blocks, halo 0, 3-D DT watershed, '
+                     'size_filter 25'),
+    3: dict(shape=(256, 2048, 2048), block_shape=(64, 512, 512), halo=(0, 32, 32), pitch=(3, 24, 24),
+            task=dict(apply_dt_2d=True, apply_ws_2d=True),
+            workload='config3: synthetic anisotropic 256x2048x2048 f32, 64x512x512 blocks, halo [0,32,32], '
+                     'apply_dt_2d + apply_ws_2d'),
+    4: dict(shape=(1024, 1024, 1024), block_shape=(64, 256, 256), halo=(8, 32, 32), task=dict(D3),
+            workload='config4 (1 GPU): synthetic 1024^3 f32, 64x256x256 blocks, halo [8,32,32], 3-D'),
+    5: dict(shape=(256, 2048, 2048), full_shape=(2048, 2048, 2048), slab=3, block_shape=(64, 256, 256),
+            halo=(8, 32, 32), dtype='uint8', mask=True, two_pass=True,
+            task=dict(D3, size_filter=25, non_maximum_suppression=False),
+            workload='config5 (1 GPU share): z-slab 3 of 8 (256x2048x2048) of a synthetic 2048^3 uint8 map '
+                     'with ellipsoid mask, 64x256x256 blocks, halo [8,32,32], 3-D two-pass'),
+}
+CONFIG2 = CONFIGS[2]
 
 # Algorithmic HBM bytes per OUTER voxel of each pipeline stage, 3-D f32:
 STAGE_BYTES = {'prep_edt_x': 12, 'edt_yz': 20, 'smooth_seeds': 24, 'hmap': 28, 'seeds': 16,
@@ -60,7 +78,7 @@ def cpu_baseline(cfg, n_jobs=16):
     from oracle import oracle as O
     O.build()
     bz, by, bx = cfg['block_shape']
-    blocks = [boundary_map((bz, by, bx), seed=s) for s in (11, 12)]
+    blocks = [boundary_map((bz, by, bx), seed=s, dtype=cfg.get('dtype', 'float32')) for s in (11, 12)]
     cores = min(n_jobs, len(os.sched_getaffinity(0)))
     jobs = [(blocks[i % 2], cfg['task'], cfg['block_shape']) for i in range(n_jobs)]
     t0 = time.time()
@@ -88,11 +106,25 @@ def blocking(shape, block_shape, halo):
     return out
 
 
+def alg_bytes(cfg, outer_vox, inner_vox, pass2_outer):
+    """Algorithmic HBM bytes of one step."""
+    two_d = cfg['task'].get('apply_ws_2d', True)
+    per_outer = 104 if two_d else 128
+    if cfg.get('dtype', 'float32') == 'uint8':
+        per_outer -= 9
+    per_inner = INNER_BYTES
+    if cfg.get('mask'):
+        per_outer += 1
+        per_inner += 1
+    return per_outer * outer_vox + 8 * pass2_outer + per_inner * inner_vox
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--config', type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-jobs', type=int, default=16)
     args = ap.parse_args()
@@ -100,7 +132,8 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    cfg = CONFIG2
+    cfg = CONFIGS[args.config]
+    two_pass = cfg.get('two_pass', False)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -109,53 +142,94 @@ def main():
     import torch
     import torch.distributed as dist
     from cluster_tools_amd import ctws
-    from cluster_tools_amd.synthetic import boundary_map_torch
+    from cluster_tools_amd.synthetic import boundary_map_torch, ellipsoid_mask_torch
 
     torch.cuda.set_device(local_rank)
     dev = torch.device('cuda', local_rank)
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
 
-    vol = boundary_map_torch(cfg['shape'], seed=rank, device=dev)
-    blist = blocking(cfg['shape'], cfg['block_shape'], cfg['halo'])
-    blocks = []
-    inner_vox = 0
-    outer_vox = 0
+    shape = tuple(cfg['shape'])
+    origin = (0, 0, 0)
+    full = cfg.get('full_shape', shape)
+    if 'slab' in cfg:
+        origin = (((cfg['slab'] + rank) % (full[0] // shape[0])) * shape[0], 0, 0)
+    gen = dict(seed=rank if 'full_shape' not in cfg else 0, device=dev, dtype=cfg.get('dtype', 'float32'),
+               pitch=cfg.get('pitch', (24, 24, 24)), origin=origin, full_shape=full)
+    vol = boundary_map_torch(shape, **gen)
+    mvol = ellipsoid_mask_torch(shape, origin, full, device=dev) if cfg.get('mask') else None
+    blist = blocking(shape, cfg['block_shape'], cfg['halo'])
+    out_vol = torch.zeros(shape, dtype=torch.int64, device=dev) if two_pass else None
+
+    def sl(beg, end):
+        return tuple(slice(a, b) for a, b in zip(beg, end))
+
+    blocks = {}
+    inner_vox = outer_vox = pass2_outer = 0
     for b in blist:
         ob, oe = b['obeg'], b['oend']
-        inp = vol[ob[0]:oe[0], ob[1]:oe[1], ob[2]:oe[2]].contiguous()
+        isl = sl(b['beg'], b['end'])
+        if mvol is not None and not bool(mvol[isl].any()):
+            continue  # empty inner mask: nothing to do, nothing written (watershed.py:295-297)
+        inp = vol[sl(ob, oe)].contiguous()
         ishape = [e - s for s, e in zip(b['beg'], b['end'])]
         ibeg = [s - o for s, o in zip(b['beg'], ob)]
-        out = torch.empty(ishape, dtype=torch.int64, device=dev)
-        crop = ob != b['beg'] or oe != b['end']
-        blocks.append(dict(input=inp, output=out, inner_begin=ibeg, crop_relabel=crop, block_id=b['block_id']))
+        d = dict(input=inp, output=torch.empty(ishape, dtype=torch.int64, device=dev), inner_begin=ibeg,
+                 crop_relabel=list(ob) != list(b['beg']) or list(oe) != list(b['end']), block_id=b['block_id'],
+                 isl=isl, osl=sl(ob, oe))
+        if mvol is not None:
+            d['mask'] = mvol[sl(ob, oe)].contiguous()
+        blocks[b['block_id']] = d
         inner_vox += int(np.prod(ishape))
         outer_vox += int(inp.numel())
     del vol
+    if two_pass:
+        from cluster_tools_amd.utils.blocking import Blocking
+        from cluster_tools_amd.utils import volume_utils as vu
+        lists = vu.make_checkerboard_block_lists(Blocking([0, 0, 0], list(shape), list(cfg['block_shape'])))
+        passes = [[blocks[i] for i in lst if i in blocks] for lst in lists]
+        for b in passes[1]:
+            b['crop_relabel'] = False
+            b['initial_seeds'] = torch.empty(tuple(b['input'].shape[-3:]), dtype=torch.int64, device=dev)
+            pass2_outer += int(b['input'].numel())
+    else:
+        passes = [list(blocks.values())]
     torch.cuda.synchronize()
 
     h = ctws.Handle(local_rank)
-    counts = torch.zeros(len(blocks), dtype=torch.int64, device=dev)
-    gathered = torch.zeros(len(blocks) * world, dtype=torch.int64, device=dev)
+    nblocks = len(blocks)
+    counts = torch.zeros(nblocks, dtype=torch.int64, device=dev)
+    gathered = torch.zeros(nblocks * world, dtype=torch.int64, device=dev)
+    stage_ms = {}
 
-    def step():
-        res = h.ws_blocks_device(cfg['task'], cfg['block_shape'], blocks)
+    def step(record):
+        res = []
+        for pid, pblocks in enumerate(passes):
+            if pid == 1:
+                for b in pblocks:  # initial_seeds = ds_out[input_bb] (two_pass_watershed.py:228)
+                    b['initial_seeds'].copy_(out_vol[b['osl']])
+            r = h.ws_blocks_device(cfg['task'], cfg['block_shape'], pblocks, pass_id=pid)
+            if record:
+                for k, v in h.timings().items():
+                    stage_ms[k] = stage_ms.get(k, 0.0) + v
+            if two_pass:
+                for b, (st, _) in zip(pblocks, r):
+                    if st in (0, 2):
+                        out_vol[b['isl']] = b['output']
+            res += r
         if world > 1:
             counts.copy_(torch.tensor([m for _, m in res], dtype=torch.int64))
             dist.all_gather_into_tensor(gathered, counts)
         return res
 
     for _ in range(args.warmup):
-        step()
+        step(False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stage_ms = {}
     for _ in range(args.steps):
-        step()
-        for k, v in h.timings().items():
-            stage_ms[k] = stage_ms.get(k, 0.0) + v
+        step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -170,36 +244,39 @@ def main():
     value = total_vox / dt / 1e9
     ms_per_step = dt / args.steps * 1e3
 
-    # roofline of the dominant kernel (by time, HIP events inside the library)
     stages = {}
     for k in STAGE_BYTES:
         stages[k] = sum(stage_ms.get(p, 0.0) for p in STAGE_PARTS.get(k, (k,)))
     stages['output'] = sum(stage_ms.get(p, 0.0) for p in STAGE_PARTS['output'])
-    stage_bytes = dict(STAGE_BYTES)
     stage_gbs = {}
     for k, ms in stages.items():
-        b = stage_bytes[k] * outer_vox if k in stage_bytes else INNER_BYTES * inner_vox
+        b = STAGE_BYTES[k] * outer_vox if k in STAGE_BYTES else INNER_BYTES * inner_vox
         stage_gbs[k] = round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
     # roofline of the dominant stage by time (algorithmic bytes / its HIP-event time)
     dom = max(STAGE_BYTES, key=lambda k: stages[k])
     dom_ms = stages[dom]
     achieved = STAGE_BYTES[dom] * outer_vox / (dom_ms * 1e-3) / 1e9
-    alg_total = sum(STAGE_BYTES.values()) * outer_vox + INNER_BYTES * inner_vox
+    alg_total = alg_bytes(cfg, outer_vox, inner_vox, pass2_outer)
     pipe = alg_total / (ms_per_step * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
+    if args.config == 2 and os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get(dom)
 
     if rank == 0:
         line = {
             'metric': 'Gvoxel/s DT-watershed (node, 1/2/4/8 GPU) + % HBM roofline; VI vs ref',
             'value': round(value, 4), 'unit': 'Gvoxel/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
-            'config': {'workload': 'config2: synthetic 512^3 f32 boundary map, 64x256x256 blocks, halo 0, '
-                                   '3-D DT watershed, size_filter 25',
-                       'volume': list(cfg['shape']), 'block_shape': list(cfg['block_shape']),
-                       'blocks_per_gpu': len(blocks), 'parallelism': 'blocks sharded, %d GPU(s)' % world},
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': cfg.get('dtype', 'float32').replace('float', 'f'),
+            'data': 'synthetic',
+            'config': {'workload': cfg['workload'], 'volume': list(shape), 'block_shape': list(cfg['block_shape']),
+                       'halo': list(cfg['halo']), 'blocks_per_gpu': nblocks, 'passes': len(passes),
+                       'parallelism': 'blocks sharded, %d GPU(s)' % world},
             'roofline': {'bound': 'hbm', 'kernel': '%s (%s)' % (dom, STAGE_KERNELS[dom]),
                          'ms_per_step': round(dom_ms, 3), 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
                          'alg_bytes_per_outer_voxel': STAGE_BYTES[dom]},
             'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(alg_total / inner_vox, 1),
                                   'achieved': round(pipe, 1), 'unit': 'GB/s',

@@ -483,6 +483,16 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 int64_t words_of(int64_t n) { return n / 64 + 1; }
 int64_t chunks_of(int64_t n) { return (words_of(n) + 255) / 256; }
 
+// timings of one ctws_ws_blocks call: summed over its batches (counts too)
+void add_timing(ctws_handle* h, const char* name, float v) {
+    for (auto& t : h->timings)
+        if (std::strcmp(t.first, name) == 0) {
+            t.second += v;
+            return;
+        }
+    h->timings.push_back({name, v});
+}
+
 // ---- one batch, all pointers on the device ------------------------------------------------
 int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* blocks, const BlockIO* io, int nb) {
     Workspace& w = h->ws;
@@ -648,7 +658,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     const dim3 rg((unsigned)std::min<int64_t>((maxRows + kRows - 1) / kRows, 16384), nb);
     const dim3 rig((unsigned)std::min<int64_t>((maxIRows + kRows - 1) / kRows, 16384), nb);
     size_t ev = 0;
-    h->timings.clear();
     std::vector<const char*> names;
     auto mark = [&](const char* name) {
         record(h, ev++);
@@ -1000,18 +1009,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     for (size_t i = 1; i < ev; ++i) {
         float ms = 0.f;
         hipEventElapsedTime(&ms, h->events[i - 1], h->events[i]);
-        h->timings.push_back({names[i], ms});
+        add_timing(h, names[i], ms);
     }
-    h->timings.push_back({"flood_rounds", (float)rounds1});
-    h->timings.push_back({"frontier_iters", (float)fiters});
-    h->timings.push_back({"flood_fallback", (float)fallback});
-    h->timings.push_back({"regrow_rounds", (float)rounds2});
-    h->timings.push_back({"flood_kernel_ms", fk1});
-    h->timings.push_back({"flood_packed", packed ? 1.f : 0.f});
-    h->timings.push_back({"flood_tiles_solved", (float)h->flood_tiles});
-    h->timings.push_back({"flood_local_iters", (float)h->flood_iters});
-    h->timings.push_back({"flood_lines_swept", (float)h->flood_lines});
-    h->timings.push_back({"size_filter_kernel_ms", fk2});
+    add_timing(h, "flood_rounds", (float)rounds1);
+    add_timing(h, "frontier_iters", (float)fiters);
+    add_timing(h, "flood_fallback", (float)fallback);
+    add_timing(h, "regrow_rounds", (float)rounds2);
+    add_timing(h, "flood_kernel_ms", fk1);
+    add_timing(h, "flood_packed", packed ? 1.f : 0.f);
+    add_timing(h, "flood_tiles_solved", (float)h->flood_tiles);
+    add_timing(h, "flood_local_iters", (float)h->flood_iters);
+    add_timing(h, "flood_lines_swept", (float)h->flood_lines);
+    add_timing(h, "size_filter_kernel_ms", fk2);
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : (pl.pass2 ? CTWS_BLOCK_EMPTY_PASS2 : CTWS_BLOCK_EMPTY);
         blocks[i].max_label = st[i].active ? st[i].max_label : 0;
@@ -1053,6 +1062,7 @@ int64_t batch_voxels_budget() {
 int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, bool device_ptrs) {
     if (!h || !cfg || (!blocks && n > 0) || n < 0) return CTWS_EINVAL;
     h->err.clear();
+    h->timings.clear();
     HIPCHK(hipSetDevice(h->device));
     Plan pl;
     int r = make_plan(h, cfg, pl);

@@ -84,12 +84,17 @@ def ellipsoid_mask(shape):
     return (r <= 1.0).astype(np.uint8)
 
 
-def boundary_map_torch(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='float32', device='cuda', z_chunk=32):
-    """Same map as `boundary_map`, generated with torch (float64 arithmetic) on `device`."""
+def boundary_map_torch(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='float32', device='cuda', z_chunk=32,
+                       origin=(0, 0, 0), full_shape=None):
+    """Same map as `boundary_map`, generated with torch (float64 arithmetic) on `device`.
+
+    With `full_shape`, the sub-volume [origin, origin + shape) of the map of `full_shape`."""
     import torch
     shape = tuple(int(s) for s in shape)
+    full = tuple(int(s) for s in (full_shape or shape))
+    gz0, gy0, gx0 = (int(o) for o in origin)
     pz, py, px = (float(p) for p in pitch)
-    ncz, ncy, ncx = (int(np.ceil(s / p)) + 2 for s, p in zip(shape, (pz, py, px)))
+    ncz, ncy, ncx = (int(np.ceil(s / p)) + 2 for s, p in zip(full, (pz, py, px)))
     cz, cy, cx = np.meshgrid(np.arange(ncz), np.arange(ncy), np.arange(ncx), indexing='ij')
     cell = ((cz * ncy + cy) * ncx + cx).astype(np.uint64)
     pts = []
@@ -98,9 +103,10 @@ def boundary_map_torch(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='flo
         pts.append(torch.from_numpy(((c - 1) + 0.1 + 0.8 * j) * p).to(device))
     ptz, pty, ptx = pts
     Z, Y, X = shape
+    FY, FX = full[1], full[2]
     out = torch.empty(shape, dtype=getattr(torch, dtype), device=device)
-    yy = torch.arange(Y, dtype=torch.float64, device=device)[:, None].expand(Y, X)
-    xx = torch.arange(X, dtype=torch.float64, device=device)[None, :].expand(Y, X)
+    yy = (gy0 + torch.arange(Y, dtype=torch.float64, device=device))[:, None].expand(Y, X)
+    xx = (gx0 + torch.arange(X, dtype=torch.float64, device=device))[None, :].expand(Y, X)
     icy = torch.div(yy, py, rounding_mode='floor').long() + 1
     icx = torch.div(xx, px, rounding_mode='floor').long() + 1
     # per-voxel noise hash: splitmix64 in int64 arithmetic (wrapping)
@@ -119,7 +125,7 @@ def boundary_map_torch(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='flo
 
     for z0 in range(0, Z, z_chunk):
         z1 = min(Z, z0 + z_chunk)
-        zz = torch.arange(z0, z1, dtype=torch.float64, device=device)[:, None, None]
+        zz = torch.arange(gz0 + z0, gz0 + z1, dtype=torch.float64, device=device)[:, None, None]
         icz = torch.div(zz, pz, rounding_mode='floor').long() + 1
         d1 = torch.full((z1 - z0, Y, X), float('inf'), dtype=torch.float64, device=device)
         d2 = torch.full_like(d1, float('inf'))
@@ -135,7 +141,10 @@ def boundary_map_torch(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='flo
                     d2 = torch.where(closer, d1, torch.minimum(d2, d))
                     d1 = torch.where(closer, d, d1)
         b = torch.clamp(1.0 - (d2 - d1) / 2.5, 0.0, 1.0)
-        vidx = torch.arange(z0 * Y * X, z1 * Y * X, dtype=torch.int64, device=device).view(z1 - z0, Y, X)
+        gz = torch.arange(gz0 + z0, gz0 + z1, dtype=torch.int64, device=device)[:, None, None]
+        gy = torch.arange(gy0, gy0 + Y, dtype=torch.int64, device=device)[None, :, None]
+        gx = torch.arange(gx0, gx0 + X, dtype=torch.int64, device=device)[None, None, :]
+        vidx = (gz * FY + gy) * FX + gx
         h = smix(vidx ^ to_i64(s0))
         u = ((h >> 40) & ((1 << 24) - 1)).to(torch.float64) * (1.0 / (1 << 24))
         b = torch.clamp(b + noise * (2.0 * u - 1.0), 0.0, 1.0)
@@ -144,3 +153,16 @@ def boundary_map_torch(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='flo
         else:
             out[z0:z1] = b.to(out.dtype)
     return out
+
+
+def ellipsoid_mask_torch(shape, origin=(0, 0, 0), full_shape=None, device='cuda'):
+    """`ellipsoid_mask(full_shape)[origin:origin + shape]` as a uint8 torch tensor on `device`."""
+    import torch
+    full = tuple(int(s) for s in (full_shape or shape))
+    ax = []
+    for s, o, f in zip(shape, origin, full):
+        c = torch.arange(o, o + s, dtype=torch.float64, device=device)
+        ax.append(((c + 0.5) / f - 0.5) / 0.5)
+    zz, yy, xx = ax
+    r = zz[:, None, None] ** 2 + yy[None, :, None] ** 2 + xx[None, None, :] ** 2
+    return (r <= 1.0).to(torch.uint8)
