@@ -771,12 +771,15 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
     // packed flood keys need labels < 2^20 in every block of the batch
     bool packed = true;
+    uint32_t max_seeds = 0;  // sizes the LDS histogram of the size filter
     {
         std::vector<BlockStat> s2(nb);
         HIPCHK(hipMemcpyAsync(s2.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
-        for (auto& s : s2)
+        for (auto& s : s2) {
             if (s.n_seeds >= (1u << 20) - 1u) packed = false;
+            max_seeds = std::max(max_seeds, s.n_seeds);
+        }
         if (!packed) {
             set_tiles(false);
             HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
@@ -826,7 +829,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         int TZ, TY, TX;
         flood_tile_dims(pl.nd_ws, true, &TZ, &TY, &TX);
         HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-        k_descent_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P, w.key, w.cls, w.fopen,
+        k_descent_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
                                                   w.front0);
         LAUNCHCHK();
         mark("flood_descent");
@@ -914,8 +917,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     if (cfg->size_filter > 0) {
         uint32_t* counts = (uint32_t*)w.A;
         k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
-        dim3 hg((unsigned)std::min<int64_t>((maxN + 8191) / 8192, 2048), nb);
-        k_hist<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, packed ? 1 : 0, counts);
+        // 32K voxels per workgroup: the LDS histogram is cleared and flushed once per 128 voxels
+        dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 2048), nb);
+        const int bins = (int64_t)max_seeds + 1 <= kHistBins ? (int)max_seeds + 1 : 0;
+        k_hist<<<hg, 256, sizeof(uint32_t) * (size_t)bins, h->stream>>>(w.desc, w.stat, w.lab, w.key, packed ? 1 : 0,
+                                                                        counts, bins);
         FilterParams fp{(uint32_t)cfg->size_filter, 0, 0, 0, w.act0};
         flood_tile_dims(pl.nd_ws, packed, &fp.tz, &fp.ty, &fp.tx);
         HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));

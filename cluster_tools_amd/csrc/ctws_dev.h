@@ -17,6 +17,7 @@ constexpr uint32_t kNoParent = 0xFFFFFFFFu;          // union-find: background
 constexpr uint32_t kFixedBit = 0x80000000u;          // flood label: voxel is a seed
 constexpr uint32_t kRootBit = 0x80000000u;           // CC parent slot of a labelled root
 constexpr int kRows = 4;                             // rows per workgroup iteration (row tiles)
+constexpr uint32_t kDescRes = 0x80000000u;           // descent exit entry resolved: | seed label (0: open)
 
 struct BlockDesc {
     int Z, Y, X, nd_ws;     // outer shape; nd_ws = 2 (per-slice ws) or 3
@@ -148,7 +149,9 @@ __device__ __forceinline__ void atomic_min_if(uint32_t* p, uint32_t v) {
 
 // Strided staging loop with U independent loads in flight: for p in [begin, end) step
 // `step`, st(p, ld(p)).  A plain loop issues one load, waits for it and stores it (one
-// memory latency per element); here the U loads of a batch are issued back to back.
+// memory latency per element); here the U loads of a batch are issued back to back.  The
+// tail batch is predicated rather than a scalar loop, so a short range (a 256-voxel row read
+// by one wave: 4 elements per lane) costs one memory latency, not one per element.
 template <int U, class LoadF, class StoreF>
 __device__ __forceinline__ void staged_loop(int begin, int end, int step, LoadF ld, StoreF st) {
     using T = decltype(ld(0));
@@ -160,7 +163,15 @@ __device__ __forceinline__ void staged_loop(int begin, int end, int step, LoadF 
 #pragma unroll
         for (int u = 0; u < U; ++u) st(p + u * step, v[u]);
     }
-    for (; p < end; p += step) st(p, ld(p));
+    if (p < end) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (p + u * step < end) v[u] = ld(p + u * step);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (p + u * step < end) st(p + u * step, v[u]);
+    }
 }
 
 // label of voxel i after the flood: from the packed key (packed flood), else from lab

@@ -90,8 +90,8 @@ __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64
 template <int ND>
 __global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
                                uint32_t*);
-__global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
-                               const uint32_t*, uint64_t*, uint8_t*, uint64_t*, uint64_t*);
+__global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint8_t*,
+                               uint64_t*, uint64_t*);
 template <int ND>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*);
@@ -105,7 +105,8 @@ __global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, 
 // k_post.hip
 __global__ void k_slice_seed_base(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
 __global__ void k_hist_zero(const BlockDesc*, const BlockStat*, uint32_t*);
-__global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, uint32_t*);
+__global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, uint32_t*, int);
+constexpr int kHistBins = 16384;  // largest LDS histogram of k_hist
 __global__ void k_size_filter(const BlockDesc*, const BlockStat*, FilterParams, const uint32_t*, const uint8_t*,
                               const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, int);
 __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,

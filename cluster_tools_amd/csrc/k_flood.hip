@@ -547,9 +547,10 @@ namespace ctws {
 // Descent inside a tile: tile (3-D 16^3, 2-D 1 x 64 x 64) + 1-voxel halo of heights in LDS;
 // every tile voxel gets its steepest-descent parent (itself for seeds, local minima and ties),
 // then pointer jumping in LDS runs each chain to its end inside the tile: a root of the tile
-// or the first voxel outside it.  exit[q] = that voxel (block C-order index); chains that
-// leave the tile are finished by k_descent_init following exit[] across tiles (a hop per tile
-// crossed).  One pass over the volume instead of a global pointer-jumping pass per doubling.
+// or the first voxel outside it.  exit[q] = kDescRes | label for a chain ending at a tile root
+// (the seed's label, 0 for a root without a seed), else the block C-order index of the first
+// voxel outside the tile; k_descent_init follows those across tiles (a hop per tile crossed).
+// One pass over the volume instead of a global pointer-jumping pass per doubling.
 // seed test / seed label: from the seed CC parents (pass 1: `cc` = PF after k_root_label) or,
 // when cc is null, from lab (kFixedBit; pass 2 and the fallbacks)
 __device__ __forceinline__ bool is_seed(const uint32_t* lab, const uint32_t* cc, int64_t gi) {
@@ -591,6 +592,24 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
     const int64_t YX = (int64_t)B.Y * B.X;
     const float* hb = h + B.base;
+    constexpr int PER = TN / 256;  // voxels per thread: c = threadIdx.x + k * 256
+    static_assert(TN % 256 == 0 && PER <= 32, "");
+    // seed flags of the thread's voxels: all loads issued before the first use
+    uint32_t inm = 0, seedm = 0;
+    {
+        bool sd[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = threadIdx.x + k * 256;
+            const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+            const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
+            const bool in = gz < B.Z && gy < B.Y && gx < B.X;
+            inm |= (in ? 1u : 0u) << k;
+            sd[k] = in && is_seed(lab, cc, B.base + gz * YX + (int64_t)gy * B.X + gx);
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) seedm |= (sd[k] ? 1u : 0u) << k;
+    }
     staged_loop<8>(
         (int)threadIdx.x, HN, 256,
         [&](int c) -> uint32_t {
@@ -602,11 +621,12 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
         [&](int c, uint32_t v) { sh[c] = v; });
     __syncthreads();
     // parents
-    for (int c = threadIdx.x; c < TN; c += 256) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int c = threadIdx.x + k * 256;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-        const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
         int p = c;
-        if (gz < B.Z && gy < B.Y && gx < B.X && !is_seed(lab, cc, B.base + gz * YX + (int64_t)gy * B.X + gx)) {
+        if (((inm & ~seedm) >> k) & 1u) {
             const int hc = ((lz + ZOFF) * HY + ly + 1) * HX + lx + 1;
             uint32_t best = sh[hc];
             int bh = -1;
@@ -640,7 +660,9 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     // pointer jumping inside the tile
     for (int it = 0; it < 16; ++it) {
         bool moved = false;
-        for (int c = threadIdx.x; c < TN; c += 256) {
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = threadIdx.x + k * 256;
             const int p = sp[c];
             if (p < TN) {
                 const int pp = sp[p];
@@ -652,23 +674,45 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
         }
         if (!__syncthreads_or(moved)) break;
     }
-    for (int c = threadIdx.x; c < TN; c += 256) {
+    // tile roots: seed label (seeds) or 0 (local minima without a seed, ties), kept in sh[]
+    // (the heights are no longer read)
+    {
+        uint32_t rl[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = threadIdx.x + k * 256;
+            const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+            rl[k] = 0u;
+            if ((seedm >> k) & 1u)
+                rl[k] = seed_label(lab, cc, B.base, (uint32_t)((z0 + lz) * YX + (int64_t)(y0 + ly) * B.X + x0 + lx));
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = threadIdx.x + k * 256;
+            if (sp[c] == c) sh[c] = rl[k];
+        }
+    }
+    __syncthreads();
+    // exit entry: kDescRes | label when the chain ends at a root of this tile, else the block
+    // index of the first voxel outside the tile (k_descent_init follows it)
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int c = threadIdx.x + k * 256;
+        if (!((inm >> k) & 1u)) continue;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
-        if (gz >= B.Z || gy >= B.Y || gx >= B.X) continue;
         const int p = sp[c];
-        int ez, ey, ex;
+        uint32_t e;
         if (p < TN) {
-            ex = x0 + p % TX;
-            ey = y0 + (p / TX) % TY;
-            ez = z0 + p / (TX * TY);
+            e = kDescRes | sh[p];
         } else {
             const int q = p - TN;
-            ex = x0 + q % HX - 1;
-            ey = y0 + (q / HX) % HY - 1;
-            ez = z0 + q / (HX * HY) - ZOFF;
+            const int ex = x0 + q % HX - 1;
+            const int ey = y0 + (q / HX) % HY - 1;
+            const int ez = z0 + q / (HX * HY) - ZOFF;
+            e = (uint32_t)(ez * YX + (int64_t)ey * B.X + ex);
         }
-        exitp[B.base + gz * YX + (int64_t)gy * B.X + gx] = (uint32_t)(ez * YX + (int64_t)ey * B.X + ex);
+        exitp[B.base + gz * YX + (int64_t)gy * B.X + gx] = e;
     }
 }
 template __global__ void k_descent_tile<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
@@ -681,31 +725,43 @@ template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, c
 // exactly one word): open = not final yet, chg = final (the first "changed" set, whose
 // neighbours form the first frontier).
 __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                      const float* __restrict__ h, const uint32_t* __restrict__ lab,
-                                                      const uint32_t* __restrict__ cc,
-                                                      const uint32_t* __restrict__ par, uint64_t* __restrict__ key,
-                                                      uint8_t* __restrict__ fixedv, uint64_t* __restrict__ open,
-                                                      uint64_t* __restrict__ chg) {
+                                                      const float* __restrict__ h, const uint32_t* __restrict__ par,
+                                                      uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
+                                                      uint64_t* __restrict__ open, uint64_t* __restrict__ chg) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t nrows = (int64_t)B.Z * B.Y;
     const int wpr = (B.X + 63) >> 6;
     for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
         for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
+            // the kRows chains advance together, so their loads overlap
+            uint32_t e[kRows];
+            float hv[kRows];
+#pragma unroll
+            for (int rr = 0; rr < kRows; ++rr) {
+                const int64_t gi = B.base + (r0 + rr) * B.X + x;
+                const bool ok = r0 + rr < nrows;
+                e[rr] = ok ? par[gi] : kDescRes;
+                hv[rr] = ok ? h[gi] : 0.0f;
+            }
+            for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
+                bool more = false;
+#pragma unroll
+                for (int rr = 0; rr < kRows; ++rr)
+                    if (!(e[rr] & kDescRes)) {
+                        e[rr] = par[B.base + e[rr]];
+                        more = true;
+                    }
+                if (!more) break;
+            }
 #pragma unroll
             for (int rr = 0; rr < kRows; ++rr) {
                 const int64_t row = r0 + rr;
                 if (row >= nrows) break;
                 const int64_t gi = B.base + row * B.X + x;
-                uint32_t r = par[gi];
-                for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
-                    const uint32_t n = par[B.base + r];
-                    if (n == r) break;
-                    r = n;
-                }
-                const uint32_t lr = seed_label(lab, cc, B.base, r);
+                const uint32_t lr = e[rr] & ~kDescRes;
                 const bool res = lr != 0;
-                key[gi] = res ? (((uint64_t)ordf(h[gi]) << 32) | (uint64_t)lr) : kPackInf;
+                key[gi] = res ? (((uint64_t)ordf(hv[rr]) << 32) | (uint64_t)lr) : kPackInf;
                 fixedv[gi] = res ? 1 : 0;
                 const uint64_t op = __ballot(!res);
                 const uint64_t fi = __ballot(res);

@@ -39,18 +39,19 @@ __global__ void __launch_bounds__(256) k_hist_zero(const BlockDesc* __restrict__
 }
 
 // label counts over the whole outer block (3-D) / slice (2-D: labels are slice-unique).
-// Each workgroup counts a contiguous range in an LDS histogram (labels <= n_seeds fit in
-// 16K bins) and flushes its non-zero bins with one global atomic each.
-constexpr int kHistBins = 16384;
+// Each workgroup counts a contiguous range in an LDS histogram of `bins` entries (dynamic
+// LDS, sized by the host to the batch's largest seed count so that a few thousand labels do
+// not cap the occupancy) and flushes its non-zero bins with one global atomic each; a block
+// with more labels than bins counts with global atomics.
 __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, const BlockStat* S,
                                               const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
-                                              int packed, uint32_t* __restrict__ counts) {
-    __shared__ uint32_t sh[kHistBins];
+                                              int packed, uint32_t* __restrict__ counts, int bins) {
+    extern __shared__ uint32_t sh[];
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     uint32_t* c = counts + B.base;
     const int64_t nb = (int64_t)S[blockIdx.y].n_seeds + 1;
-    const bool use_lds = nb <= kHistBins;
+    const bool use_lds = nb <= bins;
     if (use_lds)
         for (int j = threadIdx.x; j < nb; j += 256) sh[j] = 0;
     __syncthreads();
@@ -90,7 +91,10 @@ __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, c
         if (sh[j]) atomicAdd(&c[j], sh[j]);
 }
 
-// zero small segments; survivors become the regrow seeds (fixed, key (h, 0))
+// zero small segments; survivors become the regrow seeds (fixed, key (h, 0, label)).
+// Packed keys: a voxel that is already fixed (seed or steepest-descent voxel of the first
+// flood) holds exactly that key, so only voxels the relaxation reached (a minority) and
+// removed voxels are written; the heights are read for the former only.
 __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                      FilterParams fp, const uint32_t* __restrict__ counts,
                                                      const uint8_t* __restrict__ excl, const float* __restrict__ h,
@@ -100,23 +104,71 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
+    auto freed = [&](int64_t i) {
+        // only tiles with a free voxel can change in the regrow flood
+        const int x = (int)(i % B.X), y = (int)((i / B.X) % B.Y), z = (int)(i / YX);
+        uint32_t* a = fp.act + B.tbase + ((z / fp.tz) * B.ty + y / fp.ty) * B.tx + x / fp.tx;
+        if (!*a) atomicOr(a, 8u);
+    };
+    auto survive = [&](int64_t i) {
+        const int z = (B.nd_ws == 2) ? (int)(i / YX) : 0;
+        if (!survivors[B.sbase + z]) survivors[B.sbase + z] = 1;
+    };
+    if (packed) {
+        constexpr int U = 4;  // voxels per thread in flight
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < B.N; i0 += stride * U) {
+            uint64_t kv[U];
+            uint8_t fx[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + u * stride;
+                kv[u] = kInfKey;
+                fx[u] = 0;
+                if (i < B.N) {
+                    kv[u] = key[B.base + i];
+                    fx[u] = fixedv[B.base + i];
+                }
+            }
+            bool keep[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t l = kv[u] == kInfKey ? 0u : (uint32_t)(kv[u] & ((1ull << 20) - 1ull));
+                keep[u] = l != 0 && (counts[B.base + l] >= fp.size_filter || (excl && excl[B.base + l]));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + u * stride;
+                if (i >= B.N) continue;
+                if (keep[u]) {
+                    if (!fx[u]) {
+                        const uint32_t l = (uint32_t)(kv[u] & ((1ull << 20) - 1ull));
+                        key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (uint64_t)l;
+                        fixedv[B.base + i] = 1;
+                    }
+                    survive(i);
+                } else {
+                    if (kv[u] != kInfKey) key[B.base + i] = kInfKey;
+                    if (fx[u]) fixedv[B.base + i] = 0;
+                    freed(i);
+                }
+            }
+        }
+        return;
+    }
     BLOCK_LOOP(i, B) {
-        const uint32_t l = flood_label(lab, key, packed, B.base + i);
+        const uint32_t l = lab[B.base + i] & ~kFixedBit;
         bool keep = l != 0 && (counts[B.base + l] >= fp.size_filter || (excl && excl[B.base + l]));
         if (keep) {
-            if (!packed) lab[B.base + i] = l | kFixedBit;
-            key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
+            lab[B.base + i] = l | kFixedBit;
+            key[B.base + i] = (uint64_t)ordf(h[B.base + i]) << 32;
             fixedv[B.base + i] = 1;
-            const int z = (B.nd_ws == 2) ? (int)(i / YX) : 0;
-            if (!survivors[B.sbase + z]) survivors[B.sbase + z] = 1;
+            survive(i);
         } else {
-            if (!packed) lab[B.base + i] = 0;
+            lab[B.base + i] = 0;
             key[B.base + i] = kInfKey;
             fixedv[B.base + i] = 0;
-            // only tiles with a free voxel can change in the regrow flood
-            const int x = (int)(i % B.X), y = (int)((i / B.X) % B.Y), z = (int)(i / YX);
-            uint32_t* a = fp.act + B.tbase + ((z / fp.tz) * B.ty + y / fp.ty) * B.tx + x / fp.tx;
-            if (!*a) atomicOr(a, 8u);
+            freed(i);
         }
     }
 }
