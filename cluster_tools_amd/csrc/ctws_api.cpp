@@ -64,6 +64,8 @@ struct Workspace {
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
     uint32_t* fflags = nullptr;
     uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: changed
+    int64_t cap_fstat = 0;
+    uint32_t* fstat = nullptr;  // CTWS_TRACE statistics: open voxels, frontier visits per block
 };
 
 constexpr int kCounterBytes = 4 * (4 + 4 * kStatSlots);  // flood flag + statistics slots
@@ -91,6 +93,7 @@ struct ctws_handle {
     int no_descent = 0;  // CTWS_NO_DESCENT=1: flood from the seeds alone (test hook)
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     int verify = 0;      // CTWS_VERIFY=1: check the flood fixpoint, =2: fail on a violation (tests)
+    int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
     // RCCL
     ncclComm_t comm = nullptr;
@@ -212,6 +215,10 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         w.cap_front = front;
     }
     if (!w.fflags) ALLOC(fflags, kFrontierBatch);
+    if (blocks > w.cap_fstat) {
+        ALLOC(fstat, 2 * blocks);
+        w.cap_fstat = blocks;
+    }
     if (!w.counter) ALLOC(counter, kCounterBytes / 4);
     if (!w.taps) ALLOC(taps, 6 * 128);
 #undef ALLOC
@@ -819,7 +826,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
         {
             // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
-            const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;
+            const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
             const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
             if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
             else k_descent_tile<2><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
@@ -829,8 +836,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         int TZ, TY, TX;
         flood_tile_dims(pl.nd_ws, true, &TZ, &TY, &TX);
         HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+        // statistics (CTWS_TRACE only): open voxels and frontier visits per block
+        uint32_t* fst = h->trace ? w.fstat : nullptr;
+        if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
         k_descent_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
-                                                  w.front0);
+                                                  w.front0, fst);
         LAUNCHCHK();
         mark("flood_descent");
         // frontier relaxation of the remaining voxels (k_frontier, one voxel per lane)
@@ -841,15 +851,15 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ccur, 1u, (size_t)(TF / 64 + 1), h->stream));
         const dim3 fg((unsigned)std::min<int64_t>((TF / nb + 64 * 4 - 1) / (64 * 4) + 1, 2048), nb);
         bool converged = false;
-        for (fiters = 0; fiters < kFrontierMaxIters && !converged;) {
+        for (fiters = 0; fiters < h->frontier_max_iters && !converged;) {
             HIPCHK(hipMemsetAsync(w.fflags, 0, sizeof(uint32_t) * kFrontierBatch, h->stream));
             for (int k = 0; k < kFrontierBatch; ++k) {
                 if (pl.nd_ws == 3)
                     k_frontier<3><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur,
-                                                             cnext, w.fflags + k);
+                                                             cnext, w.fflags + k, fst ? fst + nb : nullptr);
                 else
                     k_frontier<2><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur,
-                                                             cnext, w.fflags + k);
+                                                             cnext, w.fflags + k, fst ? fst + nb : nullptr);
                 std::swap(fcur, fnext);
                 std::swap(ccur, cnext);
             }
@@ -874,6 +884,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 return r;
         }
         mark("flood_relax");
+        if (fst) {
+            std::vector<uint32_t> hs(2 * (size_t)nb);
+            HIPCHK(hipMemcpyAsync(hs.data(), fst, sizeof(uint32_t) * 2 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            double no = 0, nv = 0;
+            for (int i = 0; i < nb; ++i) {
+                no += hs[i];
+                nv += hs[nb + i];
+            }
+            add_timing(h, "open_voxels", (float)no);
+            add_timing(h, "frontier_visits", (float)nv);
+        }
         // fixpoint check (exact height ties can break the descent argument): else flood again
         if (h->verify) {
         HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
@@ -1199,6 +1221,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_NO_DESCENT")) h->no_descent = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FRONTIER_ITERS")) h->frontier_max_iters = std::atoi(t);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * 128 * sizeof(double), hipHostMallocDefault) != hipSuccess) {

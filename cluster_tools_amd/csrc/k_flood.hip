@@ -727,11 +727,13 @@ template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, c
 __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint32_t* __restrict__ par,
                                                       uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
-                                                      uint64_t* __restrict__ open, uint64_t* __restrict__ chg) {
+                                                      uint64_t* __restrict__ open, uint64_t* __restrict__ chg,
+                                                      uint32_t* __restrict__ nopen) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t nrows = (int64_t)B.Z * B.Y;
     const int wpr = (B.X + 63) >> 6;
+    uint32_t cnt_open = 0;  // statistics (CTWS_TRACE): voxels left to the relaxation
     for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
         for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
             // the kRows chains advance together, so their loads overlap
@@ -768,9 +770,14 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
                 if ((threadIdx.x & 63) == 0) {
                     open[B.fbase + row * wpr + (x >> 6)] = op;
                     chg[B.fbase + row * wpr + (x >> 6)] = fi;
+                    cnt_open += (uint32_t)__popcll(op);
                 }
             }
         }
+    if (nopen) {
+        cnt_open = wg_reduce_u32(cnt_open, OpAdd());
+        if (threadIdx.x == 0 && cnt_open) atomicAdd(&nopen[blockIdx.y], cnt_open);
+    }
 }
 
 // One iteration of the frontier relaxation.  frontier = (neighbours of the voxels changed in
@@ -807,7 +814,8 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                                   const float* __restrict__ h, uint64_t* __restrict__ key,
                                                   const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
                                                   uint64_t* __restrict__ cnext, const uint32_t* __restrict__ fprev,
-                                                  uint32_t* __restrict__ fnext, uint32_t* __restrict__ flag) {
+                                                  uint32_t* __restrict__ fnext, uint32_t* __restrict__ flag,
+                                                  uint32_t* __restrict__ nvisit) {
     __shared__ uint64_t schg[kFrontierWaves][64];
     __shared__ uint64_t sfw[kFrontierWaves][64];
     __shared__ int spre[kFrontierWaves][64];
@@ -875,6 +883,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             if (lane >= o) incl += t;
         }
         const int total = __shfl(incl, 63);
+        if (nvisit && lane == 0 && total) atomicAdd(&nvisit[blockIdx.y], (uint32_t)total);
         schg[wv][lane] = 0ull;
         sfw[wv][lane] = f;
         spre[wv][lane] = incl - cnt;
@@ -946,9 +955,9 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     if (__ballot(any) && lane == 0 && !*(volatile uint32_t*)flag) atomicOr(flag, 1u);
 }
 template __global__ void k_frontier<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*);
+                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 template __global__ void k_frontier<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*);
+                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
