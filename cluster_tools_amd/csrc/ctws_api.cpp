@@ -1239,7 +1239,8 @@ void ctws_close(ctws_handle* h) {
     Workspace& w = h->ws;
     void* ptrs[] = {w.fin, w.dt, w.A, w.Bf, w.sm, w.hm, w.cls, w.P, w.PF, w.lab, w.key, w.W, w.Wp, w.csum,
                     w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.lines0, w.lines1, w.desc, w.stat, w.counter,
-                    w.taps, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p};
+                    w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1,
+                    w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);
