@@ -174,8 +174,9 @@ class Handle:
         cfg = make_cfg(config, block_shape, pass_id)
         n = len(blocks)
         arr = (CtwsBlock * n)()
-        # the library runs on its own stream: make torch's pending writes visible first
-        torch.cuda.synchronize()
+        # the library runs on its own stream: make torch's pending writes visible first (torch's
+        # stream only: other handles' streams on this device keep running)
+        torch.cuda.current_stream(blocks[0]['input'].device if blocks else None).synchronize()
         codes = {'torch.uint8': 1, 'torch.uint16': 2, 'torch.float32': 3, 'torch.float64': 4}
         for i, b in enumerate(blocks):
             inp = b['input']
