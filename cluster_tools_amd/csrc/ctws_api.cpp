@@ -93,6 +93,7 @@ struct ctws_handle {
     int no_descent = 0;  // CTWS_NO_DESCENT=1: flood from the seeds alone (test hook)
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     int verify = 0;      // CTWS_VERIFY=1: check the flood fixpoint, =2: fail on a violation (tests)
+    int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
     // RCCL
@@ -679,7 +680,15 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         LAUNCHCHK();
         PrepParams pp{(float)cfg->threshold, cfg->invert_inputs, cfg->agglomerate_channels, pl.pitch[2] * pl.pitch[2]};
         dim3 gx((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
-        k_prep_edt_x<<<gx, 256, 4 * (size_t)maxX * 4, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+        // rows up to 1024 voxels: lanes own consecutive voxels in registers (k_prep_edt_x_reg)
+        if (maxX <= 256 && !h->prep_lds)
+            k_prep_edt_x_reg<4><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+        else if (maxX <= 512 && !h->prep_lds)
+            k_prep_edt_x_reg<8><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+        else if (maxX <= 1024 && !h->prep_lds)
+            k_prep_edt_x_reg<16><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+        else
+            k_prep_edt_x<<<gx, 256, 4 * (size_t)maxX * 4, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
         LAUNCHCHK();
         k_set_active<<<(nb + 255) / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb);
         LAUNCHCHK();
@@ -1221,6 +1230,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_NO_DESCENT")) h->no_descent = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS")) h->frontier_max_iters = std::atoi(t);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||

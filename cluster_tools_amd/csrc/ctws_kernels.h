@@ -36,6 +36,8 @@ struct FilterParams {
 // k_edt.hip
 __global__ void k_input_minmax(const BlockDesc*, BlockStat*);
 __global__ void k_prep_edt_x(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
+template <int KMAX>
+__global__ void k_prep_edt_x_reg(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
 template <int W>
 __global__ void k_edt_col(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*, uint32_t*,
                           uint32_t*);

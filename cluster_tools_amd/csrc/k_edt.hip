@@ -159,6 +159,139 @@ __global__ void __launch_bounds__(256) k_prep_edt_x(const BlockDesc* __restrict_
     for (int x = lane; x < X; x += 64) g2[B.base + rbase + x] = (uint32_t)sdist[x];
 }
 
+// Register variant (X <= 64 * KMAX): lane l owns the K = ceil(X / 64) consecutive voxels
+// [l K, l K + K) of the row, so the nearest-foreground scans need no LDS: per-lane first/last
+// foreground, then wave-level exclusive max/min scans, then the lane's own K distances.  f32
+// rows of exactly 64 K voxels move as float4 / uint4 (16 B per lane per access).  Same results
+// as k_prep_edt_x.
+template <int KMAX>
+__global__ void __launch_bounds__(256) k_prep_edt_x_reg(const BlockDesc* __restrict__ D, BlockStat* S, PrepParams pp,
+                                                        float* __restrict__ fin, uint32_t* __restrict__ g2) {
+    const BlockDesc& B = D[blockIdx.y];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+    if (row >= (int64_t)B.Z * B.Y) return;
+    const int X = B.X;
+    const int K = (X + 63) >> 6;
+    const float mn = unordf(S[blockIdx.y].in_min);
+    const float den = unordf(S[blockIdx.y].in_max) - mn;  // max(x - min) == max - min (monotone rounding)
+    const int64_t rbase = row * X;
+    const int x0 = lane * K;
+    float v[KMAX];
+    const bool vec = (KMAX % 4 == 0) && K == KMAX && X == 64 * KMAX && B.n_channels == 0 && B.dtype == 3 &&
+                     ((((uintptr_t)B.input) | (uintptr_t)(B.base * 4)) & 15u) == 0u;
+    if (vec) {
+        const float4* src = (const float4*)((const float*)B.input + rbase + x0);
+#pragma unroll
+        for (int q = 0; q < KMAX / 4; ++q) {
+            const float4 t = src[q];
+            v[4 * q] = t.x;
+            v[4 * q + 1] = t.y;
+            v[4 * q + 2] = t.z;
+            v[4 * q + 3] = t.w;
+        }
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            float a = v[k] - mn;
+            if (den > 0.0f) a = a / den;
+            if (pp.invert) a = 1.0f - a;
+            if (B.mask && !B.mask[rbase + x0 + k]) a = 1.0f;
+            v[k] = a;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            v[k] = 0.0f;
+            const int x = x0 + k;
+            if (k < K && x < X) {
+                const int64_t i = rbase + x;
+                float a;
+                if (B.n_channels == 0) {
+                    a = load_raw(B.input, B.dtype, i) - mn;
+                    if (den > 0.0f) a = a / den;
+                } else {
+                    const int64_t cs = B.N;
+                    const int64_t o0 = (int64_t)B.c0 * cs + i;
+                    a = load_raw(B.input, B.dtype, o0) - mn;
+                    if (den > 0.0f) a = a / den;
+                    for (int c = 1; c < B.C; ++c) {
+                        float w = load_raw(B.input, B.dtype, o0 + c * cs) - mn;
+                        if (den > 0.0f) w = w / den;
+                        if (pp.agg == 0) a = a + w;
+                        else if (pp.agg == 1) a = fmaxf(a, w);
+                        else a = fminf(a, w);
+                    }
+                    if (pp.agg == 0) a = a / (float)B.C;
+                }
+                if (pp.invert) a = 1.0f - a;
+                if (B.mask && !B.mask[i]) a = 1.0f;
+                v[k] = a;
+            }
+        }
+    }
+    // foreground bits of the lane's voxels, first / last foreground
+    uint32_t fg = 0u;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+        if (k < K && x0 + k < X && v[k] > pp.threshold) fg |= 1u << k;
+    // any foreground in the block? (_apply_dt: np.sum(threshd) == 0 -> None)
+    if (__ballot(fg != 0u) != 0ull && lane == 0 && !*(volatile uint32_t*)&S[blockIdx.y].fg)
+        atomicOr(&S[blockIdx.y].fg, 1u);
+    int lp = fg ? x0 + 31 - __builtin_clz(fg) : -1;
+    int rn = fg ? x0 + __builtin_ctz(fg) : 0x3FFFFFFF;
+    // exclusive max-scan of `last` from the left, exclusive min-scan of `first` from the right
+    for (int s2 = 1; s2 < 64; s2 <<= 1) {
+        const int a = __shfl_up(lp, s2);
+        if (lane >= s2) lp = max(lp, a);
+        const int b = __shfl_down(rn, s2);
+        if (lane + s2 < 64) rn = min(rn, b);
+    }
+    int left = __shfl_up(lp, 1);
+    if (lane == 0) left = -1;
+    int right = __shfl_down(rn, 1);
+    if (lane == 63) right = 0x3FFFFFFF;
+    uint32_t out[KMAX];
+    {
+        int r = right;
+#pragma unroll
+        for (int k = KMAX - 1; k >= 0; --k) {
+            const int x = x0 + k;
+            if ((fg >> k) & 1u) r = x;
+            out[k] = (uint32_t)((r >= 0x3FFFFFFF) ? 0x3FFFFFFF : r - x);
+        }
+        int l = left;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int x = x0 + k;
+            if ((fg >> k) & 1u) l = x;
+            const int dl = (l < 0) ? 0x3FFFFFFF : x - l;
+            const int d = min((int)out[k], dl);
+            out[k] = (d >= 0x3FFFFFFF) ? kInfD2 : (uint32_t)(pp.px2 * d * d);
+        }
+    }
+    if (vec) {
+        float4* fo = (float4*)(fin + B.base + rbase + x0);
+        uint4* go = (uint4*)(g2 + B.base + rbase + x0);
+#pragma unroll
+        for (int q = 0; q < KMAX / 4; ++q) {
+            fo[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+            go[q] = make_uint4(out[4 * q], out[4 * q + 1], out[4 * q + 2], out[4 * q + 3]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int x = x0 + k;
+            if (k < K && x < X) {
+                fin[B.base + rbase + x] = v[k];
+                g2[B.base + rbase + x] = out[k];
+            }
+        }
+    }
+}
+template __global__ void k_prep_edt_x_reg<4>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
+template __global__ void k_prep_edt_x_reg<8>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
+template __global__ void k_prep_edt_x_reg<16>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
+
 // Correctly rounded sqrtf of an integer n < 2^24 (vigra: sqrt on the float32 dest).  The
 // hardware v_sqrt_f32 is not correctly rounded, so round a double sqrt to float and fix it
 // with exact arithmetic: the float r is correct iff mid(r-,r)^2 < n < mid(r,r+)^2 (midpoints

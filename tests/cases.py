@@ -24,7 +24,15 @@ def make_cases():
     # a slice without any boundary (EDT = sqrt(dmax) there)
     xe = _x(seed=8).copy()
     xe[5] = 0.0
+    # rows wider than 256 voxels: the x pass's register kernel at 8 and 16 voxels per lane, and
+    # the ragged tail of a 1000-voxel row
+    xw512 = _x(seed=10, shape=(8, 16, 512))
+    xw600 = np.stack([_x(seed=s, shape=(3, 16, 600)) for s in (11, 12)])
+    xw1000 = _x(seed=13, shape=(8, 12, 1000))
     return {
+        '3d_wide512_mask': (dict(D3), dict(input=xw512, mask=ellipsoid_mask(xw512.shape))),
+        '2d_wide600_4d': ({}, dict(input=xw600)),
+        '3d_wide1000': (dict(D3), dict(input=xw1000)),
         '3d_default': (dict(D3), dict(input=x)),
         '2d_default': ({}, dict(input=x)),
         '2d_test_cfg_halo': (dict(threshold=.25, sigma_weights=0., halo=[0, 32, 32]),
