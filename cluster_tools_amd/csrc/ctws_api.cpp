@@ -94,6 +94,7 @@ struct ctws_handle {
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     int verify = 0;      // CTWS_VERIFY=1: check the flood fixpoint, =2: fail on a violation (tests)
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
+    int frontier_reps = 4;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
     // RCCL
@@ -865,10 +866,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             for (int k = 0; k < kFrontierBatch; ++k) {
                 if (pl.nd_ws == 3)
                     k_frontier<3><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur,
-                                                             cnext, w.fflags + k, fst ? fst + nb : nullptr);
+                                                             cnext, w.fflags + k, fst ? fst + nb : nullptr,
+                                                             h->frontier_reps);
                 else
                     k_frontier<2><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur,
-                                                             cnext, w.fflags + k, fst ? fst + nb : nullptr);
+                                                             cnext, w.fflags + k, fst ? fst + nb : nullptr,
+                                                             h->frontier_reps);
                 std::swap(fcur, fnext);
                 std::swap(ccur, cnext);
             }
@@ -1232,6 +1235,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS")) h->frontier_max_iters = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * 128 * sizeof(double), hipHostMallocDefault) != hipSuccess) {

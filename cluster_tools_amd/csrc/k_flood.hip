@@ -815,7 +815,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                                   const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
                                                   uint64_t* __restrict__ cnext, const uint32_t* __restrict__ fprev,
                                                   uint32_t* __restrict__ fnext, uint32_t* __restrict__ flag,
-                                                  uint32_t* __restrict__ nvisit) {
+                                                  uint32_t* __restrict__ nvisit, int reps) {
     __shared__ uint64_t schg[kFrontierWaves][64];
     __shared__ uint64_t sfw[kFrontierWaves][64];
     __shared__ int spre[kFrontierWaves][64];
@@ -874,6 +874,10 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             }
             f &= op[wl];  // open voxels only (their x < X)
         }
+        const uint64_t opw = wl < nwords ? op[wl] : 0ull;
+        const int z0 = row / B.Y, y0 = row - z0 * B.Y;
+        uint64_t acc = 0ull;  // changed bits of this word over all local sweeps
+        for (int rep = 0;; ++rep) {
         // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list is
         // bit (e - pre[j]) of word j, the last j with pre[j] <= e
         const int cnt = __popcll(f);
@@ -883,7 +887,8 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             if (lane >= o) incl += t;
         }
         const int total = __shfl(incl, 63);
-        if (nvisit && lane == 0 && total) atomicAdd(&nvisit[blockIdx.y], (uint32_t)total);
+        if (total == 0) break;
+        if (nvisit && lane == 0) atomicAdd(&nvisit[blockIdx.y], (uint32_t)total);
         schg[wv][lane] = 0ull;
         sfw[wv][lane] = f;
         spre[wv][lane] = incl - cnt;
@@ -947,17 +952,32 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const uint64_t c = schg[wv][lane];
-        const bool chunk_changed = __ballot(c != 0ull) != 0ull;
-        if (chunk_changed && wl < nwords) cn[wl] = c;
+        acc |= c;
+        if (__ballot(c != 0ull) == 0ull || rep + 1 >= reps) break;
+        // local sweep: the neighbours of this sweep's changes that lie in the same chunk
+        // (x within the row's words, y within the chunk's rows); changes are also in acc, so
+        // the neighbours outside the chunk see them in the next launch
+        f = (c << 1) | (c >> 1);
+        const uint64_t cxm = __shfl(c, (lane + 63) & 63), cxp = __shfl(c, (lane + 1) & 63);
+        if (xw > 0 && lane > 0) f |= cxm >> 63;
+        if (xw + 1 < wpr && lane < 63) f |= cxp << 63;
+        const uint64_t cym = __shfl(c, lane >= wpr ? lane - wpr : lane);
+        const uint64_t cyp = __shfl(c, lane + wpr < 64 ? lane + wpr : lane);
+        if (y0 > 0 && lane >= wpr) f |= cym;
+        if (y0 + 1 < B.Y && lane + wpr < 64) f |= cyp;
+        f &= opw;
+        }
+        const bool chunk_changed = __ballot(acc != 0ull) != 0ull;
+        if (chunk_changed && wl < nwords) cn[wl] = acc;
         if (lane == 0) fnx[ch0] = chunk_changed ? 1u : 0u;
         any |= chunk_changed;
     }
     if (__ballot(any) && lane == 0 && !*(volatile uint32_t*)flag) atomicOr(flag, 1u);
 }
 template __global__ void k_frontier<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 template __global__ void k_frontier<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
