@@ -128,7 +128,7 @@ def main():
     ap.add_argument('--config', type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-jobs', type=int, default=16)
-    ap.add_argument('--streams', type=int, default=2,
+    ap.add_argument('--streams', type=int, default=3,
                     help='library handles (one HIP stream each) per GPU, driven from host threads; '
                          'the blocks are split between them so their launch-bound phases overlap')
     args = ap.parse_args()
