@@ -208,26 +208,27 @@ def main():
     gathered = torch.zeros(nblocks * world, dtype=torch.int64, device=dev)
     stage_ms = {}
 
-    def step(record):
+    def step(record, ns=None, into=None):
+        ns = nstreams if ns is None else ns
+        into = stage_ms if into is None else into
         res = []
         for pid, pblocks in enumerate(passes):
             if pid == 1:
                 for b in pblocks:  # initial_seeds = ds_out[input_bb] (two_pass_watershed.py:228)
                     b['initial_seeds'].copy_(out_vol[b['osl']])
             # contiguous shares of the pass's blocks, one per handle (stream)
-            parts = [pblocks[len(pblocks) * i // nstreams:len(pblocks) * (i + 1) // nstreams]
-                     for i in range(nstreams)]
+            parts = [pblocks[len(pblocks) * i // ns:len(pblocks) * (i + 1) // ns] for i in range(ns)]
 
             def run(i):
                 return handles[i].ws_blocks_device(cfg['task'], cfg['block_shape'], parts[i], pass_id=pid)
 
-            rs = list(pool.map(run, range(nstreams))) if pool else [run(0)]
+            rs = list(pool.map(run, range(ns))) if ns > 1 else [run(0)]
             r = [x for part in rs for x in part]
             if record:
                 # stage times summed over the handles (overlapping streams: an upper bound)
-                for hh in handles:
+                for hh in handles[:ns]:
                     for k, v in hh.timings().items():
-                        stage_ms[k] = stage_ms.get(k, 0.0) + v
+                        into[k] = into.get(k, 0.0) + v
             if two_pass:
                 for b, (st, _) in zip(pblocks, r):
                     if st in (0, 2):
@@ -255,20 +256,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     stage_ms = {k: v / args.steps for k, v in stage_ms.items()}
+    # roofline durations: one more, untimed step with every block on ONE stream, so that no
+    # other stream's kernels share the chip while a launch runs (with concurrent streams the
+    # HIP-event duration of a launch includes the time it shares)
+    stage_1 = {}
+    if nstreams > 1:
+        step(True, ns=1, into=stage_1)
+        torch.cuda.synchronize()
+    else:
+        stage_1 = stage_ms
 
     total_vox = inner_vox * world * args.steps
     value = total_vox / dt / 1e9
     ms_per_step = dt / args.steps * 1e3
 
-    stages = {}
-    for k in STAGE_BYTES:
-        stages[k] = sum(stage_ms.get(p, 0.0) for p in STAGE_PARTS.get(k, (k,)))
-    stages['output'] = sum(stage_ms.get(p, 0.0) for p in STAGE_PARTS['output'])
+    def per_stage(sm):
+        st = {}
+        for k in STAGE_BYTES:
+            st[k] = sum(sm.get(p, 0.0) for p in STAGE_PARTS.get(k, (k,)))
+        st['output'] = sum(sm.get(p, 0.0) for p in STAGE_PARTS['output'])
+        return st
+
+    stages = per_stage(stage_1)
     stage_gbs = {}
     for k, ms in stages.items():
         b = STAGE_BYTES[k] * outer_vox if k in STAGE_BYTES else INNER_BYTES * inner_vox
         stage_gbs[k] = round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
-    # roofline of the dominant stage by time (algorithmic bytes / its HIP-event time)
+    # roofline of the dominant stage by time (algorithmic bytes / its single-stream HIP-event time)
     dom = max(STAGE_BYTES, key=lambda k: stages[k])
     dom_ms = stages[dom]
     achieved = STAGE_BYTES[dom] * outer_vox / (dom_ms * 1e-3) / 1e9
@@ -294,11 +308,14 @@ def main():
             'roofline': {'bound': 'hbm', 'kernel': '%s (%s)' % (dom, STAGE_KERNELS[dom]),
                          'ms_per_step': round(dom_ms, 3), 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                         'alg_bytes_per_outer_voxel': STAGE_BYTES[dom]},
+                         'alg_bytes_per_outer_voxel': STAGE_BYTES[dom],
+                         'timing': 'HIP events on the library stream, one untimed step with all blocks on 1 stream',
+                         'traffic_unit': 'HBM bytes per step of the stage (profiles/pmc_traffic.json)'},
             'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(alg_total / inner_vox, 1),
                                   'achieved': round(pipe, 1), 'unit': 'GB/s',
                                   'frac': round(pipe / HBM_PEAK_GBS, 4)},
             'stage_ms': {k: round(v, 3) for k, v in stage_ms.items()},
+            'stage_ms_1stream': {k: round(v, 3) for k, v in stage_1.items()},
             'stage_gbs': stage_gbs,
             'cpu_baseline': cpu,
         }
