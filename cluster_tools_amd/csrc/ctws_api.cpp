@@ -94,6 +94,7 @@ struct ctws_handle {
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     int verify = 0;      // CTWS_VERIFY=1: check the flood fixpoint, =2: fail on a violation (tests)
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
+    int frontier_unroll = 1;  // CTWS_FRONTIER_UNROLL (1, 2, 4, 8): list entries per lane in flight
     int frontier_reps = 4;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
@@ -864,14 +865,22 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         for (fiters = 0; fiters < h->frontier_max_iters && !converged;) {
             HIPCHK(hipMemsetAsync(w.fflags, 0, sizeof(uint32_t) * kFrontierBatch, h->stream));
             for (int k = 0; k < kFrontierBatch; ++k) {
-                if (pl.nd_ws == 3)
-                    k_frontier<3><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur,
-                                                             cnext, w.fflags + k, fst ? fst + nb : nullptr,
-                                                             h->frontier_reps);
-                else
-                    k_frontier<2><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur,
-                                                             cnext, w.fflags + k, fst ? fst + nb : nullptr,
-                                                             h->frontier_reps);
+#define CTWS_FRONTIER(ND, U)                                                                                   \
+    k_frontier<ND, U><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur, cnext, \
+                                                 w.fflags + k, fst ? fst + nb : nullptr, h->frontier_reps)
+                const int fu = h->frontier_unroll;
+                if (pl.nd_ws == 3) {
+                    if (fu == 1) CTWS_FRONTIER(3, 1);
+                    else if (fu == 2) CTWS_FRONTIER(3, 2);
+                    else if (fu == 8) CTWS_FRONTIER(3, 8);
+                    else CTWS_FRONTIER(3, 4);
+                } else {
+                    if (fu == 1) CTWS_FRONTIER(2, 1);
+                    else if (fu == 2) CTWS_FRONTIER(2, 2);
+                    else if (fu == 8) CTWS_FRONTIER(2, 8);
+                    else CTWS_FRONTIER(2, 4);
+                }
+#undef CTWS_FRONTIER
                 std::swap(fcur, fnext);
                 std::swap(ccur, cnext);
             }
@@ -1235,6 +1244,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS")) h->frontier_max_iters = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FRONTIER_UNROLL")) h->frontier_unroll = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||

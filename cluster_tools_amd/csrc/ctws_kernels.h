@@ -94,7 +94,7 @@ __global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*,
                                uint32_t*);
 __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint8_t*,
                                uint64_t*, uint64_t*, uint32_t*);
-template <int ND>
+template <int ND, int U>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);

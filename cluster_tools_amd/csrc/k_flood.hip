@@ -789,7 +789,6 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
 // per lane; its changed bits collect in LDS and are stored whole (no memset, no global
 // atomics).
 constexpr int kFrontierWaves = 4;
-constexpr int kFrontierUnroll = 4;  // list entries per lane in flight
 
 // position of the k-th (0-based) set bit of w (k < popcount(w))
 __device__ __forceinline__ int kth_set_bit(uint64_t w, int k) {
@@ -809,7 +808,7 @@ __device__ __forceinline__ int kth_set_bit(uint64_t w, int k) {
     return pos;
 }
 
-template <int ND>
+template <int ND, int kFrontierUnroll>
 __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                   const float* __restrict__ h, uint64_t* __restrict__ key,
                                                   const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
@@ -974,10 +973,30 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     }
     if (__ballot(any) && lane == 0 && !*(volatile uint32_t*)flag) atomicOr(flag, 1u);
 }
-template __global__ void k_frontier<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
-template __global__ void k_frontier<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                                       const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
+template __global__ void k_frontier<3, 1>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
+                                          uint32_t*, uint32_t*, int);
+template __global__ void k_frontier<2, 1>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
+                                          uint32_t*, uint32_t*, int);
+template __global__ void k_frontier<3, 2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
+                                          uint32_t*, uint32_t*, int);
+template __global__ void k_frontier<3, 4>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
+                                          uint32_t*, uint32_t*, int);
+template __global__ void k_frontier<3, 8>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
+                                          uint32_t*, uint32_t*, int);
+template __global__ void k_frontier<2, 2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
+                                          uint32_t*, uint32_t*, int);
+template __global__ void k_frontier<2, 4>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
+                                          uint32_t*, uint32_t*, int);
+template __global__ void k_frontier<2, 8>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
+                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
+                                          uint32_t*, uint32_t*, int);
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
