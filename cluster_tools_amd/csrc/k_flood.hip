@@ -582,7 +582,10 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     constexpr int HN = HZ * HY * HX, TN = TZ * TY * TX;
     constexpr int ZOFF = ND == 3 ? 1 : 0;
     __shared__ uint32_t sh[HN];  // ordered heights (0xFFFFFFFF outside the block)
-    __shared__ int sp[TN];       // pointer: < TN interior voxel, >= TN halo voxel (TN + halo index)
+    // pointer: < TN interior voxel, >= TN halo voxel (TN + halo index); 16 bits (TN + HN < 2^15)
+    // so that 5 tiles fit a CU's LDS
+    __shared__ int16_t sp[TN];
+    static_assert(TN + HN < 32768, "");
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int ntx = (B.X + TX - 1) / TX, nty = (B.Y + TY - 1) / TY, ntz = (B.Z + TZ - 1) / TZ;
@@ -654,7 +657,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
                 p = inside ? ((hz - ZOFF) * TY + (hy - 1)) * TX + (hx - 1) : TN + bh;
             }
         }
-        sp[c] = p;
+        sp[c] = (int16_t)p;
     }
     __syncthreads();
     // pointer jumping inside the tile
@@ -667,7 +670,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
             if (p < TN) {
                 const int pp = sp[p];
                 if (pp != p) {
-                    sp[c] = pp;
+                    sp[c] = (int16_t)pp;
                     moved = true;
                 }
             }
