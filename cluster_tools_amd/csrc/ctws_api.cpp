@@ -94,6 +94,7 @@ struct ctws_handle {
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     int verify = 0;      // CTWS_VERIFY=1: check the flood fixpoint, =2: fail on a violation (tests)
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
+    int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     int frontier_unroll = 1;  // CTWS_FRONTIER_UNROLL (1, 2, 4, 8): list entries per lane in flight
     int frontier_reps = 4;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
@@ -315,6 +316,10 @@ int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
 }
 
 int col_width(int L) { return L <= 512 ? 32 : (L <= 1024 ? 16 : 8); }
+// EDT columns: 16 x positions (64-B row segments) beat 32 — half the LDS per tile, twice the
+// tiles per CU, and the bounded search's per-lane trip counts vary less per wave (r01 sweep:
+// y+z passes 1.60 ms at 32, 1.44 at 16, 1.77 at 8 for config 2)
+int edt_col_width(int L) { return L <= 1024 ? 16 : 8; }
 
 void record(ctws_handle* h, size_t idx) {
     while (h->events.size() <= idx) {
@@ -698,7 +703,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     mark("prep_edt_x");
     {
         // y pass (final for a 2-D dt), then z pass (3-D dt)
-        const int Wy = col_width(maxY);
+        const int Wy = h->edt_w ? h->edt_w : edt_col_width(maxY);
         EdtColParams ep{1, pl.pitch[1] * pl.pitch[1], pl.dt_2d, pl.dt_2d, 0u};
         dim3 gy((unsigned)((int64_t)maxZ * ((maxX + Wy - 1) / Wy)), nb);
         const size_t ldsy = (size_t)maxY * Wy * 4;
@@ -713,7 +718,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         launch_col(Wy, gy, ldsy, ep, (uint32_t*)w.A, (uint32_t*)w.Bf);
         LAUNCHCHK();
         if (!pl.dt_2d) {
-            const int Wz = col_width(maxZ);
+            const int Wz = h->edt_w ? h->edt_w : edt_col_width(maxZ);
             dim3 gz((unsigned)((int64_t)maxY * ((maxX + Wz - 1) / Wz)), nb);
             const size_t ldsz = (size_t)maxZ * Wz * 4;
             EdtColParams ez{2, pl.pitch[0] * pl.pitch[0], 1, 0, 0u};
@@ -1244,6 +1249,10 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS")) h->frontier_max_iters = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_EDT_W")) {
+        const int v = std::atoi(t);
+        h->edt_w = (v == 8 || v == 16 || v == 32) ? v : 0;
+    }
     if (const char* t = std::getenv("CTWS_FRONTIER_UNROLL")) h->frontier_unroll = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
