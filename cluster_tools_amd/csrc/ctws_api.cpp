@@ -94,6 +94,7 @@ struct ctws_handle {
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     int verify = 0;      // CTWS_VERIFY=1: check the flood fixpoint, =2: fail on a violation (tests)
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
+    int gauss_w = 0;  // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     int frontier_unroll = 1;  // CTWS_FRONTIER_UNROLL (1, 2, 4, 8): list entries per lane in flight
     int frontier_reps = 4;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch
@@ -390,7 +391,7 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
             } else {
                 const int Lm = a == 0 ? maxZ : maxY;
                 const int other = a == 0 ? maxY : maxZ;
-                const int W = col_width(Lm);
+                const int W = h->gauss_w ? h->gauss_w : col_width(Lm);
                 dim3 g((unsigned)((int64_t)other * ((maxX + W - 1) / W)), nb);
                 const size_t lds = (size_t)Lm * W * 4;
                 auto kern = W == 32 ? kGaussColR32[r] : (W == 16 ? kGaussColR16[r] : kGaussColR8[r]);
@@ -1249,6 +1250,10 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS")) h->frontier_max_iters = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_GAUSS_W")) {
+        const int v = std::atoi(t);
+        h->gauss_w = (v == 8 || v == 16 || v == 32) ? v : 0;
+    }
     if (const char* t = std::getenv("CTWS_EDT_W")) {
         const int v = std::atoi(t);
         h->edt_w = (v == 8 || v == 16 || v == 32) ? v : 0;
