@@ -1,20 +1,30 @@
 #!/usr/bin/env python
 """Benchmark: blockwise DT watershed throughput (Gvoxel/s) on MI355X.
 
-Workload (BASELINE.json configs[1]): synthetic 512^3 float32
-boundary map, 64x256x256 blocks, no halo, 3-D DT watershed (apply_dt_2d = apply_ws_2d =
-False), reference defaults otherwise (threshold .5, sigma_seeds 2, sigma_weights 2,
-alpha .8, size_filter 25).  One step = the watershed of every block of the volume (the
-`_ws_block` loop of one job), inputs resident in HBM, uint64 outputs written to HBM.
+Default workload (BASELINE.json configs[2], SURVEY.md §8(d) config 3 — the largest single-GPU
+configuration): a synthetic anisotropic 256x2048x2048 float32 boundary map (cells of 3x24x24
+voxels), 64x512x512 blocks with halo [0, 32, 32] (outer blocks 64x576x576), apply_dt_2d +
+apply_ws_2d, reference defaults otherwise (threshold .5, sigma_seeds 2, sigma_weights 2,
+alpha .8, size_filter 25).  One step = the `_ws_block` of every block of the volume: read the
+outer block, EDT, seeds, hmap, flood, size filter + regrow, halo crop +
+labelVolumeWithBackground, uint64 output with the block id offset.  `value` counts inner
+(output) voxels; inputs are resident in HBM when the timed region starts and the uint64
+outputs are written to HBM.  The PCIe-inclusive rate (host numpy input -> host numpy uint64
+output through ctws_ws_blocks) is reported beside it as `host_resident`.
+
+`--config N` runs the other BASELINE configs on one GPU (config 2: 512^3 3-D; config 4: 1024^3
+with halo [8,32,32]; config 5: one z-slab share of the 2048^3 uint8 two-pass run).
 
 Multi-GPU (torchrun, one process per GPU): weak scaling — every rank processes its own
-512^3 volume; after each step the per-block label counts are all-gathered over RCCL (the
-exchange that assigns compact global id offsets).  value = voxels of all
-ranks / max-over-ranks time.
+volume of the config; after each step the per-block label counts are all-gathered over RCCL
+and exclusively scanned into compact global id offsets (the exchange of
+relabel/find_labeling.py:104-116).  value = inner voxels of all ranks / max-over-ranks time.
 
-The CPU baseline (rank 0, N = 1) is the oracle (C++ restatement of the reference path,
-oracle/) on a bounded sample, run like LocalTask: one single-threaded process per block.
-It runs before any GPU initialisation so that no process is forked from a GPU process.
+The CPU baseline (rank 0, N = 1) is the oracle (oracle/, the C++ restatement of the
+reference path) on a bounded sample of the same workload, driven like LocalTask: one
+single-threaded process per block, n_jobs = min(n_blocks, cores).  It runs before any GPU
+initialisation so that no process is forked from a GPU process.  Worker 0's oracle output
+is compared with the GPU output of the same block (VI, adapted Rand).
 """
 import argparse
 import json
@@ -28,69 +38,68 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-# BASELINE.json configs; the driver's line is config 2 (configs[1]).  The
-# others run with --config N as single-GPU shares (config 5: the central z-slab of 8).
+# BASELINE.json configs.  The single-GPU headline is config 3.
 D3 = dict(apply_dt_2d=False, apply_ws_2d=False)
 CONFIGS = {
-    2: dict(shape=(512, 512, 512), block_shape=(64, 256, 256), halo=(0, 0, 0), task=dict(D3),
+    2: dict(shape=(512, 512, 512), block_shape=(64, 256, 256), halo=(0, 0, 0), task=dict(D3), seed=0,
             workload='config2: synthetic 512^3 f32 boundary map, 64x256x256 blocks, halo 0, 3-D DT watershed, '
                      'size_filter 25'),
-    3: dict(shape=(256, 2048, 2048), block_shape=(64, 512, 512), halo=(0, 32, 32), pitch=(3, 24, 24),
-            task=dict(apply_dt_2d=True, apply_ws_2d=True),
-            workload='config3: synthetic anisotropic 256x2048x2048 f32, 64x512x512 blocks, halo [0,32,32], '
-                     'apply_dt_2d + apply_ws_2d'),
-    4: dict(shape=(1024, 1024, 1024), block_shape=(64, 256, 256), halo=(8, 32, 32), task=dict(D3),
+    3: dict(shape=(256, 2048, 2048), block_shape=(64, 512, 512), halo=(0, 32, 32), pitch=(3, 24, 24), seed=1,
+            task=dict(apply_dt_2d=True, apply_ws_2d=True, halo=[0, 32, 32]),
+            workload='config3: synthetic anisotropic 256x2048x2048 f32 EM-like boundary map, 64x512x512 blocks, '
+                     'halo [0,32,32], apply_dt_2d + apply_ws_2d, size_filter 25'),
+    4: dict(shape=(1024, 1024, 1024), block_shape=(64, 256, 256), halo=(8, 32, 32), task=dict(D3, halo=[8, 32, 32]),
+            seed=2,
             workload='config4 (1 GPU): synthetic 1024^3 f32, 64x256x256 blocks, halo [8,32,32], 3-D'),
     5: dict(shape=(256, 2048, 2048), full_shape=(2048, 2048, 2048), slab=3, block_shape=(64, 256, 256),
-            halo=(8, 32, 32), dtype='uint8', mask=True, two_pass=True,
-            task=dict(D3, size_filter=25, non_maximum_suppression=False),
+            halo=(8, 32, 32), dtype='uint8', mask=True, two_pass=True, seed=3,
+            task=dict(D3, size_filter=25, non_maximum_suppression=False, halo=[8, 32, 32]),
             workload='config5 (1 GPU share): z-slab 3 of 8 (256x2048x2048) of a synthetic 2048^3 uint8 map '
                      'with ellipsoid mask, 64x256x256 blocks, halo [8,32,32], 3-D two-pass'),
 }
-CONFIG2 = CONFIGS[2]
+DEFAULT_CONFIG = 3
 
-# Algorithmic HBM bytes per OUTER voxel of each pipeline stage, 3-D f32:
-STAGE_BYTES = {'prep_edt_x': 12, 'edt_yz': 20, 'smooth_seeds': 24, 'hmap': 28, 'seeds': 16,
-               'flood': 12, 'size_filter': 16}
-INNER_BYTES = 12  # crop / CC / offset / uint64 write, per inner voxel
-# library timing marks (HIP events on the library's stream) -> pipeline stages
-STAGE_PARTS = {'flood': ('descent_tile', 'flood_descent', 'flood_relax', 'flood'),
-               'output': ('finalize', 'crop_cc', 'output')}
-STAGE_KERNELS = {'prep_edt_x': 'k_input_minmax + k_prep_edt_x', 'edt_yz': 'k_edt_col (y, z)',
-                 'smooth_seeds': 'k_gauss_col_r (z, y) + k_gauss_row_r', 'hmap': 'k_gauss_col_r + k_gauss_row_r',
-                 'seeds': 'k_localmax ... k_root_label', 'flood': 'k_descent_tile + k_descent_init + k_frontier',
-                 'size_filter': 'k_hist + k_size_filter + regrow flood', 'output': 'k_finalize_ws + k_output'}
+# Algorithmic HBM bytes per OUTER voxel of each stage: the minimal
+# one-read / one-write traffic; iterative kernels count once.
+STAGE_BYTES_3D = {'prep_edt_x': 12, 'edt_yz': 20, 'smooth_seeds': 24, 'hmap': 28, 'seeds': 16, 'flood': 12,
+                  'size_filter': 16}
+STAGE_BYTES_2D = {'prep_edt_x': 12, 'edt_yz': 12, 'smooth_seeds': 16, 'hmap': 20, 'seeds': 16, 'flood': 12,
+                  'size_filter': 16}
+# per INNER voxel: crop CC (labels read) and the uint64 output write
+INNER_STAGE_BYTES = {'crop_cc': 4, 'output': 8}
+# library timing marks (HIP events on the library's stream) -> stages
+STAGE_PARTS = {'flood': ('descent_tile', 'flood_descent', 'flood_relax', 'flood_verify', 'flood'),
+               'crop_cc': ('finalize', 'crop_cc'), 'output': ('output',)}
+STAGE_KERNELS = {'prep_edt_x': 'k_input_minmax + k_prep_edt_x_reg', 'edt_yz': 'k_edt_col (y[, z])',
+                 'smooth_seeds': 'k_gauss_col_r + k_gauss_row_r', 'hmap': 'k_gauss_col_r + k_gauss_row_r',
+                 'seeds': 'k_localmax + k_tile_cc/k_tile_merge + bitmap rank',
+                 'flood': 'k_descent_tile + k_descent_init + k_frontier + k_flood_verify',
+                 'size_filter': 'k_hist2d/k_hist + k_regrow_init + k_frontier',
+                 'crop_cc': 'k_tile_cc<CROP> + k_tile_merge + k_flatten_roots + bitmap rank',
+                 'output': 'k_output'}
 HBM_PEAK_GBS = 8000.0
 
 
-def _cpu_job(args):
-    block, task, block_shape = args
-    from oracle import oracle as O
-    t0 = time.time()
-    O.ws_blocks(task, block_shape, [dict(input=block, block_id=1)])
-    return time.time() - t0
+def stage_bytes(cfg):
+    """{stage: (bytes per unit, 'outer' | 'inner')} for the config."""
+    two_d = cfg['task'].get('apply_ws_2d', True)
+    sb = {k: [v, 'outer'] for k, v in (STAGE_BYTES_2D if two_d else STAGE_BYTES_3D).items()}
+    if cfg.get('dtype', 'float32') == 'uint8':
+        sb['prep_edt_x'][0] -= 6   # min/max and EDT-x reads of the raw input: 1 B instead of 4
+        sb['hmap'][0] -= 3
+    if cfg.get('mask'):
+        sb['prep_edt_x'][0] += 1
+    for k, v in INNER_STAGE_BYTES.items():
+        sb[k] = [v + (1 if (cfg.get('mask') and k == 'output') else 0), 'inner']
+    return sb
 
 
-def cpu_baseline(cfg, n_jobs=16):
-    """Oracle on a bounded sample: n_jobs blocks, one process each (LocalTask model)."""
-    import multiprocessing as mp
-    from concurrent.futures import ProcessPoolExecutor
-    from cluster_tools_amd.synthetic import boundary_map
-    from oracle import oracle as O
-    O.build()
-    bz, by, bx = cfg['block_shape']
-    blocks = [boundary_map((bz, by, bx), seed=s, dtype=cfg.get('dtype', 'float32')) for s in (11, 12)]
-    cores = min(n_jobs, len(os.sched_getaffinity(0)))
-    jobs = [(blocks[i % 2], cfg['task'], cfg['block_shape']) for i in range(n_jobs)]
-    t0 = time.time()
-    with ProcessPoolExecutor(cores, mp_context=mp.get_context('fork')) as pool:
-        per_job = list(pool.map(_cpu_job, jobs))
-    wall = time.time() - t0
-    vox = n_jobs * bz * by * bx
-    return {'value': vox / wall / 1e9, 'unit': 'Gvoxel/s', 'cores': cores, 'kind': 'port',
-            'sample': '%d oracle jobs (one %dx%dx%d block each, single-threaded, %d processes like '
-                      'LocalTask); %.1f s wall, %.2f s per block' % (n_jobs, bz, by, bx, cores, wall,
-                                                                   float(np.mean(per_job)))}
+def alg_bytes(cfg, outer_vox, inner_vox, pass2_outer):
+    """Algorithmic HBM bytes of one step (SURVEY.md §8(d))."""
+    tot = 0
+    for k, (b, unit) in stage_bytes(cfg).items():
+        tot += b * (outer_vox if unit == 'outer' else inner_vox)
+    return tot + 8 * pass2_outer
 
 
 def blocking(shape, block_shape, halo):
@@ -107,17 +116,87 @@ def blocking(shape, block_shape, halo):
     return out
 
 
-def alg_bytes(cfg, outer_vox, inner_vox, pass2_outer):
-    """Algorithmic HBM bytes of one step (SURVEY.md §8(d))."""
-    two_d = cfg['task'].get('apply_ws_2d', True)
-    per_outer = 104 if two_d else 128
-    if cfg.get('dtype', 'float32') == 'uint8':
-        per_outer -= 9
-    per_inner = INNER_BYTES
+def slab_origin(cfg, rank):
+    if 'slab' not in cfg:
+        return (0, 0, 0)
+    full = cfg['full_shape']
+    return (((cfg['slab'] + rank) % (full[0] // cfg['shape'][0])) * cfg['shape'][0], 0, 0)
+
+
+# ---- CPU baseline (oracle) -----------------------------------------------------------------
+_BARRIER = None
+
+
+def _cpu_init(barrier):
+    global _BARRIER
+    _BARRIER = barrier
+
+
+def _cpu_job(args):
+    """One LocalTask-like job: generate its block (untimed), wait for all jobs, run the oracle."""
+    cfg_id, b, want_output = args
+    from oracle import oracle as O
+    from cluster_tools_amd.synthetic import boundary_map, ellipsoid_mask_sub
+    cfg = CONFIGS[cfg_id]
+    origin = slab_origin(cfg, 0)
+    full = cfg.get('full_shape', cfg['shape'])
+    ob = [o + a for o, a in zip(b['obeg'], origin)]
+    oshape = [e - s for s, e in zip(b['obeg'], b['oend'])]
+    x = boundary_map(oshape, seed=cfg['seed'] if 'full_shape' not in cfg else 0, pitch=cfg.get('pitch', (24, 24, 24)),
+                     dtype=cfg.get('dtype', 'float32'), origin=ob, full_shape=full)
+    blk = dict(input=x, block_id=b['block_id'], inner_begin=[s - o for s, o in zip(b['beg'], b['obeg'])],
+               inner_shape=[e - s for s, e in zip(b['beg'], b['end'])],
+               crop_relabel=list(b['obeg']) != list(b['beg']) or list(b['oend']) != list(b['end']))
     if cfg.get('mask'):
-        per_outer += 1
-        per_inner += 1
-    return per_outer * outer_vox + 8 * pass2_outer + per_inner * inner_vox
+        blk['mask'] = ellipsoid_mask_sub(oshape, ob, full)
+    _BARRIER.wait()
+    t0 = time.time()
+    res = O.ws_blocks(cfg['task'], cfg['block_shape'], [blk])[0]
+    t1 = time.time()
+    return t0, t1, (res['output'] if want_output else None)
+
+
+def cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def cpu_baseline(cfg_id, max_cores=16):
+    """Oracle over the first n_jobs = min(n_blocks, cores) blocks, one process per block."""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    from oracle import oracle as O
+    O.build()
+    cfg = CONFIGS[cfg_id]
+    blist = blocking(cfg['shape'], cfg['block_shape'], cfg['halo'])
+    if cfg.get('two_pass'):
+        from cluster_tools_amd.utils.blocking import Blocking
+        from cluster_tools_amd.utils import volume_utils as vu
+        first = set(vu.make_checkerboard_block_lists(Blocking([0, 0, 0], list(cfg['shape']),
+                                                              list(cfg['block_shape'])))[0])
+        blist = [b for b in blist if b['block_id'] in first]   # pass-0 blocks (_ws_block)
+    cores = min(max_cores, len(os.sched_getaffinity(0)))
+    n_jobs = min(len(blist), cores)
+    ctx = mp.get_context('fork')
+    barrier = ctx.Barrier(n_jobs)
+    jobs = [(cfg_id, blist[i], i == 0) for i in range(n_jobs)]
+    with ProcessPoolExecutor(n_jobs, mp_context=ctx, initializer=_cpu_init, initargs=(barrier,)) as pool:
+        res = list(pool.map(_cpu_job, jobs))
+    wall = max(r[1] for r in res) - min(r[0] for r in res)
+    inner = sum(int(np.prod([e - s for s, e in zip(b['beg'], b['end'])])) for b in blist[:n_jobs])
+    per = [r[1] - r[0] for r in res]
+    out = {'value': inner / wall / 1e9, 'unit': 'Gvoxel/s', 'cores': n_jobs, 'kind': 'port',
+           'cpu': cpu_model(),
+           'sample': '%d of the config\'s %d blocks, one single-threaded oracle process per block (LocalTask '
+                     'model, n_jobs = min(n_blocks, %d cores)); %.1f s wall, %.1f s mean per block'
+                     % (n_jobs, len(blist), cores, wall, float(np.mean(per)))}
+    return out, (blist[0]['block_id'], res[0][2])
 
 
 def main():
@@ -125,9 +204,10 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--config', type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument('--config', type=int, default=DEFAULT_CONFIG, choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-jobs', type=int, default=16)
+    ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe-inclusive) pass')
+    ap.add_argument('--cpu-cores', type=int, default=16)
     ap.add_argument('--streams', type=int, default=3,
                     help='library handles (one HIP stream each) per GPU, driven from host threads; '
                          'the blocks are split between them so their launch-bound phases overlap')
@@ -139,9 +219,9 @@ def main():
     cfg = CONFIGS[args.config]
     two_pass = cfg.get('two_pass', False)
 
-    cpu = None
+    cpu, ref_block = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, args.cpu_jobs)
+        cpu, ref_block = cpu_baseline(args.config, args.cpu_cores)
 
     import torch
     import torch.distributed as dist
@@ -154,12 +234,11 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
 
     shape = tuple(cfg['shape'])
-    origin = (0, 0, 0)
     full = cfg.get('full_shape', shape)
-    if 'slab' in cfg:
-        origin = (((cfg['slab'] + rank) % (full[0] // shape[0])) * shape[0], 0, 0)
-    gen = dict(seed=rank if 'full_shape' not in cfg else 0, device=dev, dtype=cfg.get('dtype', 'float32'),
-               pitch=cfg.get('pitch', (24, 24, 24)), origin=origin, full_shape=full)
+    origin = slab_origin(cfg, rank)
+    seed = (cfg['seed'] + 1000 * rank) if 'full_shape' not in cfg else 0
+    gen = dict(seed=seed, device=dev, dtype=cfg.get('dtype', 'float32'), pitch=cfg.get('pitch', (24, 24, 24)),
+               origin=origin, full_shape=full)
     vol = boundary_map_torch(shape, **gen)
     mvol = ellipsoid_mask_torch(shape, origin, full, device=dev) if cfg.get('mask') else None
     blist = blocking(shape, cfg['block_shape'], cfg['halo'])
@@ -207,6 +286,7 @@ def main():
     counts = torch.zeros(nblocks, dtype=torch.int64, device=dev)
     gathered = torch.zeros(nblocks * world, dtype=torch.int64, device=dev)
     stage_ms = {}
+    offsets = {}
 
     def step(record, ns=None, into=None):
         ns = nstreams if ns is None else ns
@@ -234,9 +314,14 @@ def main():
                     if st in (0, 2):
                         out_vol[b['isl']] = b['output']
             res += r
+        # compact global id offsets: exclusive scan of the per-block label counts of all ranks
+        # (relabel/find_labeling.py:104-116 over RCCL instead of .npy files)
+        counts.copy_(torch.tensor([m for _, m in res], dtype=torch.int64))
         if world > 1:
-            counts.copy_(torch.tensor([m for _, m in res], dtype=torch.int64))
             dist.all_gather_into_tensor(gathered, counts)
+        else:
+            gathered.copy_(counts)
+        offsets['scan'] = torch.cumsum(gathered, 0) - gathered
         return res
 
     for _ in range(args.warmup):
@@ -270,27 +355,62 @@ def main():
     value = total_vox / dt / 1e9
     ms_per_step = dt / args.steps * 1e3
 
-    def per_stage(sm):
-        st = {}
-        for k in STAGE_BYTES:
-            st[k] = sum(sm.get(p, 0.0) for p in STAGE_PARTS.get(k, (k,)))
-        st['output'] = sum(sm.get(p, 0.0) for p in STAGE_PARTS['output'])
-        return st
+    # ---- host-resident pass (PCIe-inclusive): numpy in, numpy uint64 out --------------------
+    host = None
+    if rank == 0 and not args.no_host and not two_pass:
+        hb = []
+        for b in passes[0]:
+            hb.append(dict(input=b['input'].cpu().numpy(), inner_begin=b['inner_begin'],
+                           inner_shape=list(b['output'].shape), crop_relabel=b['crop_relabel'],
+                           block_id=b['block_id'],
+                           mask=b['mask'].cpu().numpy() if b.get('mask') is not None else None,
+                           out=np.empty(tuple(b['output'].shape), dtype=np.uint64)))
+        handles[0].ws_blocks(cfg['task'], cfg['block_shape'], hb)  # warm the staging buffers
+        t0 = time.perf_counter()
+        handles[0].ws_blocks(cfg['task'], cfg['block_shape'], hb)
+        th = time.perf_counter() - t0
+        same = all(np.array_equal(h_['out'], b['output'].cpu().numpy().view(np.uint64))
+                   for h_, b in zip(hb[:2], passes[0][:2]))
+        host = {'value': round(inner_vox / th / 1e9, 4), 'unit': 'Gvoxel/s', 'ms_per_step': round(th * 1e3, 3),
+                'path': 'ctws_ws_blocks: host numpy input -> HBM -> host numpy uint64 output, one handle',
+                'h2d_bytes': int(sum(x['input'].nbytes for x in hb)), 'd2h_bytes': int(inner_vox * 8),
+                'matches_device_path': bool(same)}
+        del hb
 
+    # ---- VI of the GPU output vs the oracle on the CPU baseline's first block ---------------
+    vi = None
+    if ref_block is not None and ref_block[1] is not None and ref_block[0] in blocks:
+        from cluster_tools_amd.metrics import vi_scores, rand_scores
+        gpu_out = blocks[ref_block[0]]['output'].cpu().numpy().view(np.uint64)
+        ref = ref_block[1]
+        vs, vm = vi_scores(gpu_out, ref)
+        are, _ = rand_scores(gpu_out, ref)
+        vi = {'block_id': ref_block[0], 'vi_split': round(vs, 6), 'vi_merge': round(vm, 6),
+              'vi': round(vs + vm, 6), 'adapted_rand_error': round(are, 8),
+              'bit_exact': bool(np.array_equal(gpu_out, ref)),
+              'bar': 'VI <= 0.01, ARand <= 1e-3 (BASELINE.json north_star)'}
+
+    def per_stage(sm):
+        return {k: sum(sm.get(p, 0.0) for p in STAGE_PARTS.get(k, (k,))) for k in stage_bytes(cfg)}
+
+    sbytes = stage_bytes(cfg)
     stages = per_stage(stage_1)
     stage_gbs = {}
     for k, ms in stages.items():
-        b = STAGE_BYTES[k] * outer_vox if k in STAGE_BYTES else INNER_BYTES * inner_vox
-        stage_gbs[k] = round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
+        b, unit = sbytes[k]
+        nbytes = b * (outer_vox if unit == 'outer' else inner_vox)
+        stage_gbs[k] = round(nbytes / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
     # roofline of the dominant stage by time (algorithmic bytes / its single-stream HIP-event time)
-    dom = max(STAGE_BYTES, key=lambda k: stages[k])
+    dom = max(stages, key=lambda k: stages[k])
     dom_ms = stages[dom]
-    achieved = STAGE_BYTES[dom] * outer_vox / (dom_ms * 1e-3) / 1e9
+    b_unit, unit = sbytes[dom]
+    dom_bytes = b_unit * (outer_vox if unit == 'outer' else inner_vox)
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     alg_total = alg_bytes(cfg, outer_vox, inner_vox, pass2_outer)
     pipe = alg_total / (ms_per_step * 1e-3) / 1e9
     traffic = None
-    pmc = os.path.join(HERE, 'profiles', 'pmc_traffic.json')
-    if args.config == 2 and os.path.exists(pmc):
+    pmc = os.path.join(HERE, 'profiles', 'pmc_traffic_c%d.json' % args.config)
+    if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get(dom)
 
@@ -303,20 +423,24 @@ def main():
             'data': 'synthetic',
             'config': {'workload': cfg['workload'], 'volume': list(shape), 'block_shape': list(cfg['block_shape']),
                        'halo': list(cfg['halo']), 'blocks_per_gpu': nblocks, 'passes': len(passes),
-                       'streams_per_gpu': nstreams,
-                       'parallelism': 'blocks sharded, %d GPU(s)' % world},
+                       'inner_voxels_per_gpu': inner_vox, 'outer_voxels_per_gpu': outer_vox,
+                       'streams_per_gpu': nstreams, 'parallelism': 'blocks sharded, %d GPU(s)' % world},
             'roofline': {'bound': 'hbm', 'kernel': '%s (%s)' % (dom, STAGE_KERNELS[dom]),
                          'ms_per_step': round(dom_ms, 3), 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                         'alg_bytes_per_outer_voxel': STAGE_BYTES[dom],
+                         'alg_bytes': dom_bytes, 'alg_bytes_per_voxel': b_unit, 'voxels': unit,
                          'timing': 'HIP events on the library stream, one untimed step with all blocks on 1 stream',
-                         'traffic_unit': 'HBM bytes per step of the stage (profiles/pmc_traffic.json)'},
+                         'traffic_unit': 'HBM bytes per step of the stage (profiles/pmc_traffic_c%d.json)'
+                                         % args.config},
             'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(alg_total / inner_vox, 1),
                                   'achieved': round(pipe, 1), 'unit': 'GB/s',
                                   'frac': round(pipe / HBM_PEAK_GBS, 4)},
+            'host_resident': host,
+            'vi_vs_oracle': vi,
             'stage_ms': {k: round(v, 3) for k, v in stage_ms.items()},
             'stage_ms_1stream': {k: round(v, 3) for k, v in stage_1.items()},
             'stage_gbs': stage_gbs,
+            'global_ids': int(offsets['scan'][-1].item() + gathered[-1].item()) if 'scan' in offsets else None,
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

@@ -11,7 +11,7 @@ import numpy as np
 CTWS_OK = 0
 CTWS_U8, CTWS_U16, CTWS_F32, CTWS_F64 = 1, 2, 3, 4
 CTWS_AGG = {'mean': 0, 'max': 1, 'min': 2}
-CTWS_BLOCK_WRITTEN, CTWS_BLOCK_SKIPPED_MASK, CTWS_BLOCK_EMPTY, CTWS_BLOCK_EMPTY_PASS2 = 0, 1, 2, 3
+CTWS_BLOCK_WRITTEN, CTWS_BLOCK_SKIPPED_MASK, CTWS_BLOCK_EMPTY, CTWS_BLOCK_EMPTY_PASS2, CTWS_BLOCK_FAILED = 0, 1, 2, 3, 4
 
 _DTYPE_CODES = {np.dtype('uint8'): CTWS_U8, np.dtype('uint16'): CTWS_U16,
                 np.dtype('float32'): CTWS_F32, np.dtype('float64'): CTWS_F64}

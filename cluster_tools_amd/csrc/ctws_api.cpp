@@ -87,12 +87,15 @@ struct ctws_handle {
     uint64_t flood_tiles = 0, flood_iters = 0, flood_lines = 0;
     // host-pointer staging
     DevBuf st_in, st_mask, st_init, st_out;
+    // relabel (k_relabel.hip)
+    DevBuf rl_lab, rl_bits, rl_cnt, rl_offs, rl_out, rl_keys, rl_vals, rl_red;
+    int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
     // test hooks
     int stop_after = 0;
     int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
     int no_descent = 0;  // CTWS_NO_DESCENT=1: flood from the seeds alone (test hook)
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
-    int verify = 0;      // CTWS_VERIFY=1: check the flood fixpoint, =2: fail on a violation (tests)
+    int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int gauss_w = 0;  // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
@@ -496,6 +499,76 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
     return CTWS_OK;
 }
 
+// Frontier relaxation (k_frontier) from the open / changed bitmaps in w.fopen / w.front0 (written
+// by k_descent_init for the first flood, by k_regrow_init for the size-filter regrow) until no
+// key changes.  Batches of kFrontierBatch launches run between host checks of their flags; if
+// it has not converged after frontier_max_iters iterations (very long equal-height paths) the
+// tile flood finishes from the current keys.
+int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
+                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
+    Workspace& w = h->ws;
+    uint64_t* fcur = w.front0;
+    uint64_t* fnext = w.front1;
+    uint32_t* ccur = w.fchunk0;
+    uint32_t* cnext = w.fchunk1;
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ccur, 1u, (size_t)(TF / 64 + 1), h->stream));
+    const dim3 fg((unsigned)std::min<int64_t>((TF / nb + 64 * 4 - 1) / (64 * 4) + 1, 2048), nb);
+    bool converged = false;
+    int fiters = 0;
+    for (fiters = 0; fiters < h->frontier_max_iters && !converged;) {
+        HIPCHK(hipMemsetAsync(w.fflags, 0, sizeof(uint32_t) * kFrontierBatch, h->stream));
+        for (int k = 0; k < kFrontierBatch; ++k) {
+#define CTWS_FRONTIER(ND, U)                                                                                   \
+    k_frontier<ND, U><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur, cnext, \
+                                                 w.fflags + k, fst ? fst + nb : nullptr, h->frontier_reps)
+            const int fu = h->frontier_unroll;
+            if (pl.nd_ws == 3) {
+                if (fu == 1) CTWS_FRONTIER(3, 1);
+                else if (fu == 2) CTWS_FRONTIER(3, 2);
+                else if (fu == 8) CTWS_FRONTIER(3, 8);
+                else CTWS_FRONTIER(3, 4);
+            } else {
+                if (fu == 1) CTWS_FRONTIER(2, 1);
+                else if (fu == 2) CTWS_FRONTIER(2, 2);
+                else if (fu == 8) CTWS_FRONTIER(2, 8);
+                else CTWS_FRONTIER(2, 4);
+            }
+#undef CTWS_FRONTIER
+            std::swap(fcur, fnext);
+            std::swap(ccur, cnext);
+        }
+        LAUNCHCHK();
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.fflags, sizeof(uint32_t) * kFrontierBatch, hipMemcpyDeviceToHost,
+                              h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        for (int k = 0; k < kFrontierBatch; ++k) {
+            ++fiters;
+            if (!h->h_counter[k]) {
+                converged = true;
+                break;
+            }
+        }
+    }
+    *iters_out += fiters;
+    if (!converged) {
+        int TZ, TY, TX;
+        flood_tile_dims(pl.nd_ws, packed, &TZ, &TY, &TX);
+        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+        k_frontier_tiles<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0,
+                           h->stream>>>(w.desc, w.stat, w.fopen, w.act0, TZ, TY, TX);
+        LAUNCHCHK();
+        int rounds = 0;
+        float kms = 0.f;
+        int r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds, &kms);
+        if (r != CTWS_OK) return r;
+        *rounds_out += rounds;
+        *kms_out += kms;
+    }
+    return CTWS_OK;
+}
+
+int cdiv(int a, int b) { return (a + b - 1) / b; }
+
 int64_t words_of(int64_t n) { return n / 64 + 1; }
 int64_t chunks_of(int64_t n) { return (words_of(n) + 255) / 256; }
 
@@ -517,6 +590,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int64_t maxH = 0, maxRows = 0, maxIRows = 0;
     int maxZ = 0, maxY = 0, maxX = 0, max_tiles = 0;
     int64_t maxN = 0, maxNI = 0;
+    int maxIZ = 0, maxIY = 0, maxIX = 0;
     const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
     for (int i = 0; i < nb; ++i) {
         const ctws_block& b = blocks[i];
@@ -588,6 +662,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         maxX = std::max(maxX, d.X);
         maxN = std::max(maxN, d.N);
         maxNI = std::max(maxNI, d.NI);
+        maxIZ = std::max(maxIZ, d.IZ);
+        maxIY = std::max(maxIY, d.IY);
+        maxIX = std::max(maxIX, d.IX);
         maxH = std::max(maxH, d.hcap);
         maxRows = std::max(maxRows, (int64_t)d.Z * d.Y);
         maxIRows = std::max(maxIRows, (int64_t)d.IZ * d.IY);
@@ -764,12 +841,31 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     mark("hmap");
 
     // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
-    k_localmax<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
-    LAUNCHCHK();
-    k_plateau_union<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
-    k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
-    k_seed_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF);
-    k_seed_union<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF);
+    {
+        k_localmax<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
+        LAUNCHCHK();
+        // plateaus (equal-valued maxima candidates) and the seed CC: LDS tile union-find
+        // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
+        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0};
+        if (pl.nd_ws == 3) {
+            using T = CcTile<3>;
+            const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
+            k_tile_cc<3, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
+            k_tile_merge<3, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
+            k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
+            k_tile_cc<3, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            k_tile_merge<3, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+        } else {
+            using T = CcTile<2>;
+            const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
+            k_tile_cc<2, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
+            k_tile_merge<2, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
+            k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
+            k_tile_cc<2, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            k_tile_merge<2, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+        }
+        LAUNCHCHK();
+    }
     HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
     k_flatten_roots<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
     k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
@@ -782,9 +878,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
         HIPCHK(hipMemsetAsync(w.hkey, 0xFF, sizeof(uint64_t) * (size_t)TH, h->stream));
         HIPCHK(hipMemsetAsync(w.hpos, 0xFF, sizeof(uint32_t) * (size_t)TH, h->stream));
-        HIPCHK(hipMemsetAsync(w.p2err, 0, sizeof(uint32_t) * 4, h->stream));
         k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.sb, w.key);
-        k_p2_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.hkey, w.hpos, w.p2err);
+        k_p2_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.hkey, w.hpos);
         HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
         const dim3 hg((unsigned)std::min<int64_t>((maxH + 255) / 256, 4096), nb);
         k_p2_roots<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W);
@@ -796,8 +891,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     // packed flood keys need labels < 2^20 in every block of the batch
     bool packed = true;
     uint32_t max_seeds = 0;  // sizes the LDS histogram of the size filter
+    std::vector<BlockStat> s2(nb);
     {
-        std::vector<BlockStat> s2(nb);
         HIPCHK(hipMemcpyAsync(s2.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
         for (auto& s : s2) {
@@ -838,7 +933,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int rounds1 = 0, rounds2 = 0;
     h->flood_tiles = h->flood_iters = h->flood_lines = 0;
     float fk1 = 0.f, fk2 = 0.f;
-    int fallback = 0, fiters = 0;
+    int fallback = 0, fiters = 0, fiters2 = 0;
+    // statistics (CTWS_TRACE only): open voxels and frontier visits per block
+    uint32_t* fst = h->trace ? w.fstat : nullptr;
     if (descent) {
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
         {
@@ -850,66 +947,14 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             LAUNCHCHK();
         }
         mark("descent_tile");
-        int TZ, TY, TX;
-        flood_tile_dims(pl.nd_ws, true, &TZ, &TY, &TX);
-        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-        // statistics (CTWS_TRACE only): open voxels and frontier visits per block
-        uint32_t* fst = h->trace ? w.fstat : nullptr;
         if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
         k_descent_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
                                                   w.front0, fst);
         LAUNCHCHK();
         mark("flood_descent");
         // frontier relaxation of the remaining voxels (k_frontier, one voxel per lane)
-        uint64_t* fcur = w.front0;
-        uint64_t* fnext = w.front1;
-        uint32_t* ccur = w.fchunk0;
-        uint32_t* cnext = w.fchunk1;
-        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ccur, 1u, (size_t)(TF / 64 + 1), h->stream));
-        const dim3 fg((unsigned)std::min<int64_t>((TF / nb + 64 * 4 - 1) / (64 * 4) + 1, 2048), nb);
-        bool converged = false;
-        for (fiters = 0; fiters < h->frontier_max_iters && !converged;) {
-            HIPCHK(hipMemsetAsync(w.fflags, 0, sizeof(uint32_t) * kFrontierBatch, h->stream));
-            for (int k = 0; k < kFrontierBatch; ++k) {
-#define CTWS_FRONTIER(ND, U)                                                                                   \
-    k_frontier<ND, U><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur, cnext, \
-                                                 w.fflags + k, fst ? fst + nb : nullptr, h->frontier_reps)
-                const int fu = h->frontier_unroll;
-                if (pl.nd_ws == 3) {
-                    if (fu == 1) CTWS_FRONTIER(3, 1);
-                    else if (fu == 2) CTWS_FRONTIER(3, 2);
-                    else if (fu == 8) CTWS_FRONTIER(3, 8);
-                    else CTWS_FRONTIER(3, 4);
-                } else {
-                    if (fu == 1) CTWS_FRONTIER(2, 1);
-                    else if (fu == 2) CTWS_FRONTIER(2, 2);
-                    else if (fu == 8) CTWS_FRONTIER(2, 8);
-                    else CTWS_FRONTIER(2, 4);
-                }
-#undef CTWS_FRONTIER
-                std::swap(fcur, fnext);
-                std::swap(ccur, cnext);
-            }
-            LAUNCHCHK();
-            HIPCHK(hipMemcpyAsync(h->h_counter, w.fflags, sizeof(uint32_t) * kFrontierBatch, hipMemcpyDeviceToHost,
-                                  h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
-            for (int k = 0; k < kFrontierBatch; ++k) {
-                ++fiters;
-                if (!h->h_counter[k]) {
-                    converged = true;
-                    break;
-                }
-            }
-        }
-        if (!converged) {
-            // long paths (e.g. large exact plateaus): finish with the tile flood from here
-            HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-            k_frontier_tiles<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, w.act0, TZ, TY, TX);
-            LAUNCHCHK();
-            if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds1, &fk1)) != CTWS_OK)
-                return r;
-        }
+        if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
+            return r;
         mark("flood_relax");
         if (fst) {
             std::vector<uint32_t> hs(2 * (size_t)nb);
@@ -924,30 +969,34 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             add_timing(h, "frontier_visits", (float)nv);
         }
         // fixpoint check (exact height ties can break the descent argument): else flood again
+        // from the seeds alone.  On by default; CTWS_VERIFY=0 turns it off.
         if (h->verify) {
-        HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
-        if (pl.nd_ws == 3) k_flood_verify<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
-        else k_flood_verify<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
-        LAUNCHCHK();
-        HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-        if (h->trace && h->h_counter[0]) {
-            fprintf(stderr, "[ctws] flood verify: violations at");
-            for (uint32_t k = 0; k < std::min(8u, h->h_counter[1]); ++k) fprintf(stderr, " %u", h->h_counter[2 + k]);
-            fprintf(stderr, "\n");
-        }
-        if (h->h_counter[0] && h->verify >= 2) {
-            h->err = "flood fixpoint check failed (CTWS_VERIFY=2)";
-            return CTWS_EHIP;
-        }
-        if (h->h_counter[0] && !h->no_fallback) {
-            fallback = 1;
-            k_flood_reset<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.key, w.cls);
+            HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
+            if (pl.nd_ws == 3)
+                k_flood_verify<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
+            else
+                k_flood_verify<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
             LAUNCHCHK();
-            if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK)
-                return r;
+            HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            if (h->trace && h->h_counter[0]) {
+                fprintf(stderr, "[ctws] flood verify: violations at");
+                for (uint32_t k = 0; k < std::min(8u, h->h_counter[1]); ++k) fprintf(stderr, " %u", h->h_counter[2 + k]);
+                fprintf(stderr, "\n");
+            }
+            if (h->h_counter[0] && h->verify >= 2) {
+                h->err = "flood fixpoint check failed (CTWS_VERIFY=2)";
+                return CTWS_EHIP;
+            }
+            if (h->h_counter[0] && !h->no_fallback) {
+                fallback = 1;
+                k_flood_reset<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.key, w.cls);
+                LAUNCHCHK();
+                if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK)
+                    return r;
+            }
         }
-        }
+        mark("flood_verify");
     } else {
         mark("flood_descent");
         if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK) return r;
@@ -963,32 +1012,81 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
 
     // ---- size filter + regrow ---------------------------------------------------------------
+    std::vector<uint32_t> surv(TS, 1u);
+    int n_auto_blocks = 0;
     if (cfg->size_filter > 0) {
         uint32_t* counts = (uint32_t*)w.A;
         k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
-        // 32K voxels per workgroup: the LDS histogram is cleared and flushed once per 128 voxels
-        dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 2048), nb);
-        const int bins = (int64_t)max_seeds + 1 <= kHistBins ? (int)max_seeds + 1 : 0;
-        k_hist<<<hg, 256, sizeof(uint32_t) * (size_t)bins, h->stream>>>(w.desc, w.stat, w.lab, w.key, packed ? 1 : 0,
-                                                                        counts, bins);
-        FilterParams fp{(uint32_t)cfg->size_filter, 0, 0, 0, w.act0};
-        flood_tile_dims(pl.nd_ws, packed, &fp.tz, &fp.ty, &fp.tx);
-        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-        k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, excl, w.hm, w.lab, w.key, w.cls,
-                                                 w.surv, packed ? 1 : 0);
+        if (pl.nd_ws == 2) {
+            // one LDS histogram per slice quarter over the slice's label range
+            k_hist2d<<<dim3((unsigned)maxZ * 4, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key,
+                                                                          packed ? 1 : 0, w.sb, counts, 4);
+        } else {
+            // 32K voxels per workgroup: the LDS histogram is cleared and flushed once per 128 voxels
+            dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 2048), nb);
+            const int bins = (int64_t)max_seeds + 1 <= kHistBins ? (int)max_seeds + 1 : 0;
+            k_hist<<<hg, 256, sizeof(uint32_t) * (size_t)bins, h->stream>>>(w.desc, w.stat, w.lab, w.key,
+                                                                            packed ? 1 : 0, counts, bins);
+        }
         LAUNCHCHK();
-        if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds2, &fk2)) != CTWS_OK) return r;
+        if (packed) {
+            // survivors -> regrow seeds, removed voxels -> open; then the frontier relaxation
+            HIPCHK(hipMemsetAsync(w.surv, 0, sizeof(uint32_t) * TS, h->stream));
+            k_regrow_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts, excl, w.hm,
+                                                     w.key, w.cls, w.fopen, w.front0, w.surv);
+            LAUNCHCHK();
+            std::vector<BlockStat> s3(nb);
+            HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipMemcpyAsync(s3.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            for (int i = 0; i < nb; ++i) {
+                if (!s3[i].active) continue;
+                const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
+                bool need = false;
+                for (int z = 0; z < ns; ++z) need |= !surv[desc[i].sbase + z];
+                n_auto_blocks += need;
+            }
+            if (n_auto_blocks) {
+                // every segment of a slice / block removed: vigra seeds the regrow from the strict
+                // local minima of the hmap (watershedsNew with an all-zero seed image)
+                HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+                const dim3 ag((unsigned)std::min<int64_t>(maxRows, 65535), nb);
+                k_auto_minima<<<ag, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.surv, w.W);
+                k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
+                k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 2);
+                k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
+                k_auto_seed_set<<<ag, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.surv, w.W, w.Wp, w.sb, w.key,
+                                                           w.cls, w.fopen, w.front0);
+                LAUNCHCHK();
+            }
+            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2)) !=
+                CTWS_OK)
+                return r;
+        } else {
+            FilterParams fp{(uint32_t)cfg->size_filter, 0, 0, 0, w.act0};
+            flood_tile_dims(pl.nd_ws, packed, &fp.tz, &fp.ty, &fp.tx);
+            HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+            HIPCHK(hipMemsetAsync(w.surv, 0, sizeof(uint32_t) * TS, h->stream));
+            k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, excl, w.hm, w.lab, w.key, w.cls,
+                                                     w.surv, packed ? 1 : 0);
+            LAUNCHCHK();
+            if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds2, &fk2)) != CTWS_OK)
+                return r;
+            HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+        }
         if (unpack_final) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     }
     mark("size_filter");
     const int keys_final = (packed && !unpack_final) ? 1 : 0;  // final labels still in the keys
 
     // ---- pass 2: per-slice offsets, takeDict, uncropped inner write --------------------------
+    const int ssplit = 4;  // workgroups per slice of the per-slice reductions
     if (pl.pass2) {
         if (pl.nd_ws == 2) {
-            k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, 0, w.sb, w.slmax);
+            k_slice_max<<<dim3((unsigned)maxZ * ssplit, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, 0,
+                                                                                  w.sb, w.slmax, ssplit, 1);
             k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
-            k_p2_check<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.soff, w.p2err);
+            k_p2_check<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.soff);
         }
         HIPCHK(hipMemsetAsync(w.smin, 0, sizeof(uint32_t) * TS, h->stream));  // free after the hmap
         k_slice_inmask<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.smin);
@@ -999,68 +1097,66 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         LAUNCHCHK();
         mark("output");
     } else {
-    // ---- 2-D offsets / mask -> final uint32 ws ---------------------------------------------
-    if (pl.nd_ws == 2) {
-        k_slice_max<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.sb, w.slmax);
-        k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
-    }
-    bool any_crop = false;
-    for (int i = 0; i < nb; ++i) any_crop |= desc[i].crop != 0;
-    // without a crop the final labels are computed by k_output itself
-    const int direct = (!any_crop && h->stop_after != CTWS_STOP_WS) ? 1 : 0;
-    if (!direct) k_finalize_ws<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, w.soff, w.key, keys_final, w.lab);
-    LAUNCHCHK();
-    mark("finalize");
-    if (h->stop_after == CTWS_STOP_WS) {
-        HIPCHK(hipStreamSynchronize(h->stream));
-        return CTWS_OK;
-    }
-
-    // ---- halo crop CC + uint64 output -------------------------------------------------------
-    if (any_crop) {
-        const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
-        k_crop_init<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
-        k_crop_union<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF);
-        HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-        k_flatten_roots<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
-        k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
-        k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
-        k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
-        k_root_label<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp);
+        // ---- 2-D offsets (uncropped blocks only: a cropped block is renumbered by its CC) ----
+        bool any_crop = false, any_plain2d = false;
+        for (int i = 0; i < nb; ++i) {
+            any_crop |= desc[i].crop != 0;
+            any_plain2d |= desc[i].crop == 0 && pl.nd_ws == 2;
+        }
+        const bool stop_ws = h->stop_after == CTWS_STOP_WS;
+        if (pl.nd_ws == 2 && (any_plain2d || stop_ws)) {
+            k_slice_max<<<dim3((unsigned)maxZ * ssplit, nb), 256, 0, h->stream>>>(
+                w.desc, w.stat, w.lab, w.key, keys_final, w.sb, w.slmax, ssplit, stop_ws ? 1 : 0);
+            k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
+        }
+        if (stop_ws) {
+            // test hook: the final uint32 ws of the outer block in `lab`
+            k_finalize_ws<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, w.soff, w.key, keys_final, w.lab);
+            LAUNCHCHK();
+            HIPCHK(hipStreamSynchronize(h->stream));
+            return CTWS_OK;
+        }
         LAUNCHCHK();
-    }
-    mark("crop_cc");
-    k_output<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.PF, direct, w.key, direct ? keys_final : 0, w.sb,
-                                         w.soff);
-    LAUNCHCHK();
-    mark("output");
+        mark("finalize");
+
+        // ---- halo crop CC (labelVolumeWithBackground) + uint64 output --------------------------
+        if (any_crop) {
+            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final};
+            const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
+            if (pl.nd_ws == 3) {
+                using T = CcTile<3>;
+                const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
+                k_tile_cc<3, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+                k_tile_merge<3, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            } else {
+                using T = CcTile<2>;
+                const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
+                k_tile_cc<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+                k_tile_merge<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            }
+            HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+            k_flatten_roots<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
+            k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
+            k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
+            k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
+            k_root_label<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp);
+            LAUNCHCHK();
+        }
+        mark("crop_cc");
+        k_output<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff);
+        LAUNCHCHK();
+        mark("output");
     }
 
     HIPCHK(hipMemcpyAsync(st.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
-    std::vector<uint32_t> surv;
-    if (cfg->size_filter > 0) {
-        surv.resize(TS);
-        HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
-    }
     std::vector<uint32_t> sbh, inmask;
-    uint32_t p2err = 0;
     if (pl.pass2) {
         sbh.resize(TS);
         inmask.resize(TS);
         HIPCHK(hipMemcpyAsync(sbh.data(), w.sb, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipMemcpyAsync(inmask.data(), w.smin, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(hipMemcpyAsync(&p2err, w.p2err, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
     }
     HIPCHK(hipStreamSynchronize(h->stream));
-    if (p2err & 1u) {
-        h->err = "pass 2: relabel hash table full";
-        return CTWS_EUNSUPPORTED;
-    }
-    if (p2err & 2u) {
-        h->err = "pass 2 (2-D): a shifted new seed id equals an initial seed id of its slice after the uint32 "
-                 "wrap-around (two_pass_watershed.py:146-153); relabelConsecutive would merge them: not implemented";
-        return CTWS_EUNSUPPORTED;
-    }
     for (size_t i = 1; i < ev; ++i) {
         float ms = 0.f;
         hipEventElapsedTime(&ms, h->events[i - 1], h->events[i]);
@@ -1068,8 +1164,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
     add_timing(h, "flood_rounds", (float)rounds1);
     add_timing(h, "frontier_iters", (float)fiters);
+    add_timing(h, "regrow_iters", (float)fiters2);
     add_timing(h, "flood_fallback", (float)fallback);
     add_timing(h, "regrow_rounds", (float)rounds2);
+    add_timing(h, "auto_seeded_blocks", (float)n_auto_blocks);
     add_timing(h, "flood_kernel_ms", fk1);
     add_timing(h, "flood_packed", packed ? 1.f : 0.f);
     add_timing(h, "flood_tiles_solved", (float)h->flood_tiles);
@@ -1079,30 +1177,32 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : (pl.pass2 ? CTWS_BLOCK_EMPTY_PASS2 : CTWS_BLOCK_EMPTY);
         blocks[i].max_label = st[i].active ? st[i].max_label : 0;
+        if (!st[i].active) continue;
+        uint32_t err = st[i].err;
         const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
-        if (st[i].active && pl.pass2) {
-            // a slice/block without any seed: vigra generates seeds from the hmap's local minima
-            // (watershedsNew with labels.any() == false).  Irrelevant where nothing lies inside
-            // the mask (the result is zeroed, max_id 0); otherwise not implemented.
+        if (pl.pass2) {
+            // a slice/block without any seed: watershedsNew seeds from the hmap minima and the
+            // result has no new_to_old entry (takeDict, two_pass_watershed.py:173/204) where it
+            // is not masked before the lookup (2-D: in-mask voxels; 3-D: every voxel)
             for (int z = 0; z < ns; ++z) {
                 const int64_t s0 = desc[i].sbase + z;
                 const uint32_t nl = pl.nd_ws == 2 ? ((z + 1 < ns ? sbh[s0 + 1] : st[i].n_seeds) - sbh[s0]) : st[i].n_seeds;
-                if (!nl && inmask[s0]) {
-                    h->err = "pass 2: a slice/block without seeds inside the mask (auto-seeded watershed) is not "
-                             "implemented";
-                    return CTWS_EUNSUPPORTED;
-                }
+                if (!nl && (pl.nd_ws == 3 || inmask[s0])) err |= kErrTakeDict;
             }
         }
-        if (st[i].active && cfg->size_filter > 0) {
-            // every segment of a slice/block below size_filter: vigra then seeds the regrow
-            // from the local minima of the hmap (watershedsGraph with labels.any() == false)
+        if (cfg->size_filter > 0 && !packed)
             for (int z = 0; z < ns; ++z)
-                if (!surv[desc[i].sbase + z] && (!pl.pass2 || inmask[desc[i].sbase + z])) {
-                    h->err = "size filter removed every segment of a block/slice (auto-seeded regrow) "
-                             "is not implemented";
-                    return CTWS_EUNSUPPORTED;
-                }
+                if (!surv[desc[i].sbase + z]) err |= kErrUnsupported;
+        if (err) {
+            blocks[i].status = CTWS_BLOCK_FAILED;
+            char msg[256];
+            std::snprintf(msg, sizeof msg, "block %lld failed (%s%s%s%s%s); ", (long long)blocks[i].block_id,
+                          (err & kErrHashFull) ? "pass-2 relabel hash table full " : "",
+                          (err & kErrCollision) ? "pass-2 2-D wrapped id collision not resolved " : "",
+                          (err & kErrLabelBits) ? "auto-seed labels beyond 2^20 " : "",
+                          (err & kErrTakeDict) ? "takeDict: no new_to_old entry, as in the reference " : "",
+                          (err & kErrUnsupported) ? "auto-seeded regrow with >= 2^20 seeds " : "");
+            h->err += msg;
         }
     }
     return CTWS_OK;
@@ -1278,7 +1378,8 @@ void ctws_close(ctws_handle* h) {
     void* ptrs[] = {w.fin, w.dt, w.A, w.Bf, w.sm, w.hm, w.cls, w.P, w.PF, w.lab, w.key, w.W, w.Wp, w.csum,
                     w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.lines0, w.lines1, w.desc, w.stat, w.counter,
                     w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1,
-                    w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p};
+                    w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
+                    h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);
@@ -1337,6 +1438,140 @@ int ctws_debug_read(ctws_handle* h, const char* array, int block, void* dst, int
     }
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipMemcpy(dst, (const char*)src + d.base * es, (size_t)nbytes, hipMemcpyDeviceToHost));
+    return CTWS_OK;
+}
+
+// ---- RelabelWorkflow kernels (k_relabel.hip) ----------------------------------------------
+int ctws_unique_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_device, uint64_t* out, int64_t cap,
+                    int64_t* n_unique) {
+    if (!h || (!labels && n > 0) || n < 0 || !n_unique || cap < 0 || (!out && cap > 0)) return CTWS_EINVAL;
+    h->err.clear();
+    HIPCHK(hipSetDevice(h->device));
+    *n_unique = 0;
+    if (n == 0) return CTWS_OK;
+    int r;
+    const uint64_t* dl = labels;
+    if (!on_device) {
+        if ((r = grow(h, h->rl_lab, sizeof(uint64_t) * (size_t)n)) != CTWS_OK) return r;
+        HIPCHK(hipMemcpyAsync(h->rl_lab.p, labels, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice, h->stream));
+        dl = (const uint64_t*)h->rl_lab.p;
+    }
+    if ((r = grow(h, h->rl_red, 4 * sizeof(uint64_t))) != CTWS_OK) return r;
+    unsigned long long* red = (unsigned long long*)h->rl_red.p;
+    const unsigned long long init[3] = {~0ull, 0ull, 0ull};
+    HIPCHK(hipMemcpyAsync(red, init, sizeof(init), hipMemcpyHostToDevice, h->stream));
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+    k_u64_range<<<g, 256, 0, h->stream>>>(dl, n, red);
+    LAUNCHCHK();
+    unsigned long long hr[3];
+    HIPCHK(hipMemcpyAsync(hr, red, sizeof(hr), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const bool has_nz = hr[0] != ~0ull;
+    const int64_t first = hr[2] ? 1 : 0;
+    int64_t total = first;
+    if (has_nz) {
+        const uint64_t lo = hr[0], span = hr[1] - hr[0] + 1;
+        if (span > (1ull << 35)) {
+            h->err = "ctws_unique_u64: nonzero labels span more than 2^35 values";
+            return CTWS_EUNSUPPORTED;
+        }
+        const int64_t nw = (int64_t)((span + 63) / 64), nc = (nw + 255) / 256;
+        if ((r = grow(h, h->rl_bits, sizeof(uint64_t) * (size_t)nw)) != CTWS_OK) return r;
+        if ((r = grow(h, h->rl_cnt, sizeof(uint32_t) * (size_t)nc)) != CTWS_OK) return r;
+        if ((r = grow(h, h->rl_offs, sizeof(uint64_t) * (size_t)(nc + 1))) != CTWS_OK) return r;
+        HIPCHK(hipMemsetAsync(h->rl_bits.p, 0, sizeof(uint64_t) * (size_t)nw, h->stream));
+        k_u64_bits<<<g, 256, 0, h->stream>>>(dl, n, lo, (unsigned long long*)h->rl_bits.p);
+        k_bits_chunk_count<<<(unsigned)nc, 256, 0, h->stream>>>((const uint64_t*)h->rl_bits.p, nw,
+                                                               (uint32_t*)h->rl_cnt.p);
+        k_scan_chunks<<<1, 256, 0, h->stream>>>((const uint32_t*)h->rl_cnt.p, nc, (uint64_t*)h->rl_offs.p);
+        LAUNCHCHK();
+        uint64_t cnt = 0;
+        HIPCHK(hipMemcpyAsync(&cnt, (uint64_t*)h->rl_offs.p + nc, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        total += (int64_t)cnt;
+        *n_unique = total;
+        if (total > cap) {
+            h->err = "ctws_unique_u64: output capacity too small";
+            return CTWS_EINVAL;
+        }
+        uint64_t* dout = out;
+        if (!on_device) {
+            if ((r = grow(h, h->rl_out, sizeof(uint64_t) * (size_t)total)) != CTWS_OK) return r;
+            dout = (uint64_t*)h->rl_out.p;
+        }
+        k_bits_compact<<<(unsigned)nc, 256, 0, h->stream>>>((const uint64_t*)h->rl_bits.p, nw,
+                                                           (const uint64_t*)h->rl_offs.p, lo, (uint64_t)first, dout);
+        LAUNCHCHK();
+        if (first) HIPCHK(hipMemsetAsync(dout, 0, sizeof(uint64_t), h->stream));
+        if (!on_device)
+            HIPCHK(hipMemcpyAsync(out, dout, sizeof(uint64_t) * (size_t)total, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        return CTWS_OK;
+    }
+    *n_unique = total;  // only zeros
+    if (total > cap) {
+        h->err = "ctws_unique_u64: output capacity too small";
+        return CTWS_EINVAL;
+    }
+    if (on_device) HIPCHK(hipMemsetAsync(out, 0, sizeof(uint64_t), h->stream));
+    else out[0] = 0;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return CTWS_OK;
+}
+
+int ctws_set_table_u64(ctws_handle* h, const uint64_t* keys, const uint64_t* values, int64_t n_table) {
+    if (!h || n_table < 0 || ((!keys || !values) && n_table > 0)) return CTWS_EINVAL;
+    h->err.clear();
+    HIPCHK(hipSetDevice(h->device));
+    int r;
+    if ((r = grow(h, h->rl_keys, sizeof(uint64_t) * (size_t)std::max<int64_t>(1, n_table))) != CTWS_OK) return r;
+    if ((r = grow(h, h->rl_vals, sizeof(uint64_t) * (size_t)std::max<int64_t>(1, n_table))) != CTWS_OK) return r;
+    if (n_table) {
+        HIPCHK(hipMemcpyAsync(h->rl_keys.p, keys, sizeof(uint64_t) * (size_t)n_table, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(h->rl_vals.p, values, sizeof(uint64_t) * (size_t)n_table, hipMemcpyHostToDevice,
+                              h->stream));
+    }
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->rl_ntable = n_table;
+    return CTWS_OK;
+}
+
+int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, const uint64_t* keys,
+                    const uint64_t* values, int64_t n_table, int64_t* n_missing) {
+    if (!h || (!labels && n > 0) || n < 0) return CTWS_EINVAL;
+    const bool resident = !keys && !values;
+    if (!resident && (n_table < 0 || ((!keys || !values) && n_table > 0))) return CTWS_EINVAL;
+    h->err.clear();
+    HIPCHK(hipSetDevice(h->device));
+    if (n_missing) *n_missing = 0;
+    if (n == 0) return CTWS_OK;
+    int r;
+    if (resident) {
+        n_table = h->rl_ntable;
+    } else if (!on_device) {
+        // host table: upload it as the resident one
+        if ((r = ctws_set_table_u64(h, keys, values, n_table)) != CTWS_OK) return r;
+    }
+    const uint64_t* dk = (resident || !on_device) ? (const uint64_t*)h->rl_keys.p : keys;
+    const uint64_t* dv = (resident || !on_device) ? (const uint64_t*)h->rl_vals.p : values;
+    uint64_t* dl = labels;
+    if (!on_device) {
+        if ((r = grow(h, h->rl_lab, sizeof(uint64_t) * (size_t)n)) != CTWS_OK) return r;
+        dl = (uint64_t*)h->rl_lab.p;
+        HIPCHK(hipMemcpyAsync(dl, labels, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice, h->stream));
+    }
+    if ((r = grow(h, h->rl_red, 4 * sizeof(uint64_t))) != CTWS_OK) return r;
+    unsigned long long* miss = (unsigned long long*)h->rl_red.p + 3;
+    HIPCHK(hipMemsetAsync(miss, 0, sizeof(uint64_t), h->stream));
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+    k_u64_lookup<<<g, 256, 0, h->stream>>>(dl, n, dk, dv, n_table, miss);
+    LAUNCHCHK();
+    unsigned long long hm = 0;
+    HIPCHK(hipMemcpyAsync(&hm, miss, sizeof(hm), hipMemcpyDeviceToHost, h->stream));
+    if (!on_device) HIPCHK(hipMemcpyAsync(labels, dl, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (n_missing) *n_missing = (int64_t)hm;
     return CTWS_OK;
 }
 

@@ -53,8 +53,17 @@ struct BlockStat {
     uint32_t max_label;       // local max label (before the id offset)
     uint32_t active;          // block takes part in the remaining pipeline
     uint32_t n_cc;            // crop CC components
-    uint32_t _p[6];
+    uint32_t err;             // kErr* bits: the block cannot be finished (per-block failure)
+    uint32_t n_auto;          // auto-seeded regrow: strict hmap minima of the seedless slices
+    uint32_t _p[4];
 };
+
+// BlockStat::err bits (a failed block does not fail its batch; the caller sees the status)
+constexpr uint32_t kErrHashFull = 1u;    // pass 2: relabel hash table full
+constexpr uint32_t kErrCollision = 2u;   // pass 2 (2-D): wrapped new id == initial id (unresolved)
+constexpr uint32_t kErrLabelBits = 4u;   // auto-seeded regrow: labels beyond the 20-bit key field
+constexpr uint32_t kErrTakeDict = 8u;    // pass 2: auto-seed label without a new_to_old entry
+constexpr uint32_t kErrUnsupported = 16u; // auto-seeded regrow in a block with >= 2^20 seeds (wide keys)
 
 // order-preserving float <-> uint32 mapping (total order for non-NaN floats)
 __device__ __forceinline__ uint32_t ordf(float f) {
@@ -103,6 +112,41 @@ __device__ __forceinline__ void uf_union(uint32_t* P, uint32_t a, uint32_t b) {
             b = t;
         }
         uint32_t old = atomicCAS(&P[b], b, a);
+        if (old == b) return;
+        b = old;
+    }
+}
+
+// vigra scan key (F order, axis 0 fastest; per slice and slice-major in 2-D ws mode)
+__device__ __forceinline__ uint32_t scan_key_of(const BlockDesc& B, int z, int y, int x) {
+    return (B.nd_ws == 3) ? (uint32_t)(z + B.Z * (y + B.Y * x))
+                          : (uint32_t)((int64_t)z * B.Y * B.X + y + (int64_t)B.Y * x);
+}
+// scan key of a C-order index (outer block, or the inner block when inner != 0: 3-D F order)
+__device__ __forceinline__ uint32_t scan_key_idx(const BlockDesc& B, int inner, uint32_t c) {
+    const int Y = inner ? B.IY : B.Y, X = inner ? B.IX : B.X;
+    const uint32_t yx = (uint32_t)Y * (uint32_t)X;
+    const int z = (int)(c / yx);
+    const uint32_t rem = c - (uint32_t)z * yx;
+    const int y = (int)(rem / (uint32_t)X);
+    const int x = (int)(rem - (uint32_t)y * (uint32_t)X);
+    if (inner) return (uint32_t)(z + B.IZ * (y + B.IY * x));
+    return scan_key_of(B, z, y, x);
+}
+
+// union by scan key: the root with the smaller key becomes the parent, so every root is its
+// component's first voxel in vigra scan order
+__device__ __forceinline__ void uf_union_scan(uint32_t* P, uint32_t a, uint32_t b, const BlockDesc& B, int inner) {
+    while (true) {
+        a = uf_find(P, a);
+        b = uf_find(P, b);
+        if (a == b) return;
+        if (scan_key_idx(B, inner, a) > scan_key_idx(B, inner, b)) {
+            const uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        const uint32_t old = atomicCAS(&P[b], b, a);
         if (old == b) return;
         b = old;
     }

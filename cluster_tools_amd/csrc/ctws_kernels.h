@@ -62,10 +62,7 @@ __global__ void k_gauss_row_r(const BlockDesc*, const BlockStat*, GaussParams, H
 
 // k_cc.hip
 __global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, uint32_t*);
-__global__ void k_plateau_union(const BlockDesc*, const BlockStat*, const float*, const uint8_t*, uint32_t*);
 __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uint32_t*);
-__global__ void k_seed_init(const BlockDesc*, const BlockStat*, const uint8_t*, const uint32_t*, uint32_t*);
-__global__ void k_seed_union(const BlockDesc*, const BlockStat*, uint32_t*);
 __global__ void k_flatten_roots(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
 __global__ void k_bitmap_csum(const BlockDesc*, const BlockStat*, int, const uint64_t*, uint32_t*);
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
@@ -73,10 +70,33 @@ __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uin
 __global__ void k_root_label(const BlockDesc*, const BlockStat*, int, uint32_t*, const uint64_t*, const uint32_t*);
 __global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const float*, uint32_t*, uint64_t*,
                              uint8_t*, int);
-__global__ void k_crop_init(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
-__global__ void k_crop_union(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
-__global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*, int, const uint64_t*, int,
+__global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
                          const uint32_t*, const uint32_t*);
+
+// k_tilecc.hip: LDS block-based union-find (plateaus, seed CC, halo-crop CC)
+enum CcMode { CC_PLATEAU = 0, CC_SEED = 1, CC_CROP = 2 };
+struct CcArgs {
+    const float* v;        // PLATEAU: seed map
+    const uint8_t* cls;    // PLATEAU / SEED: local-max classes (k_localmax)
+    const uint32_t* Pp;    // SEED: plateau parents (is_max)
+    const uint32_t* lab;   // CROP: flood labels (non-packed)
+    const uint64_t* key;   // CROP: packed keys
+    int packed;            // CROP
+};
+template <int ND>
+struct CcTile;
+template <>
+struct CcTile<3> {
+    static constexpr int TZ = 4, TY = 16, TX = 32;
+};
+template <>
+struct CcTile<2> {
+    static constexpr int TZ = 1, TY = 32, TX = 64;
+};
+template <int ND, int MODE>
+__global__ void k_tile_cc(const BlockDesc*, const BlockStat*, CcArgs, uint32_t*);
+template <int ND, int MODE>
+__global__ void k_tile_merge(const BlockDesc*, const BlockStat*, CcArgs, uint32_t*);
 
 // k_flood.hip
 template <int ND>
@@ -112,7 +132,14 @@ constexpr int kHistBins = 16384;  // largest LDS histogram of k_hist
 __global__ void k_size_filter(const BlockDesc*, const BlockStat*, FilterParams, const uint32_t*, const uint8_t*,
                               const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, int);
 __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
-                            uint32_t*);
+                            uint32_t*, int, int);
+__global__ void k_hist2d(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
+                         uint32_t*, int);
+__global__ void k_regrow_init(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*, const uint8_t*,
+                              const float*, uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*);
+__global__ void k_auto_minima(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*);
+__global__ void k_auto_seed_set(const BlockDesc*, BlockStat*, const float*, const uint32_t*, const uint64_t*,
+                                const uint32_t*, const uint32_t*, uint64_t*, uint8_t*, uint64_t*, uint64_t*);
 __global__ void k_slice_offsets(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, const uint64_t*, int,
                               uint32_t*);
@@ -120,15 +147,23 @@ __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t
 // k_pass2.hip (two-pass watershed, pass 2)
 __global__ void k_p2_zero_dt(const BlockDesc*, const BlockStat*, float*);
 __global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint64_t*);
-__global__ void k_p2_insert(const BlockDesc*, const BlockStat*, const uint64_t*, uint64_t*, uint32_t*, uint32_t*);
+__global__ void k_p2_insert(const BlockDesc*, BlockStat*, const uint64_t*, uint64_t*, uint32_t*);
 __global__ void k_p2_roots(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint64_t*);
 __global__ void k_p2_label(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, const uint64_t*,
                            const uint32_t*, const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, uint32_t*, int);
 __global__ void k_p2_excl_zero(const BlockDesc*, const BlockStat*, uint8_t*);
 __global__ void k_p2_excl(const BlockDesc*, const BlockStat*, const uint32_t*, uint8_t*);
-__global__ void k_p2_check(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
+__global__ void k_p2_check(const BlockDesc*, BlockStat*, const uint64_t*, const uint32_t*);
 __global__ void k_p2_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*, const uint32_t*,
                             const uint32_t*);
 __global__ void k_slice_inmask(const BlockDesc*, const BlockStat*, uint32_t*);
+
+// k_relabel.hip (RelabelWorkflow: sorted uniques, assignment-table lookup)
+__global__ void k_u64_range(const uint64_t*, int64_t, unsigned long long*);
+__global__ void k_u64_bits(const uint64_t*, int64_t, uint64_t, unsigned long long*);
+__global__ void k_bits_chunk_count(const uint64_t*, int64_t, uint32_t*);
+__global__ void k_scan_chunks(const uint32_t*, int64_t, uint64_t*);
+__global__ void k_bits_compact(const uint64_t*, int64_t, const uint64_t*, uint64_t, uint64_t, uint64_t*);
+__global__ void k_u64_lookup(uint64_t*, int64_t, const uint64_t*, const uint64_t*, int64_t, unsigned long long*);
 
 }  // namespace ctws

@@ -44,39 +44,6 @@ namespace ctws {
             }                                                                                 \
     }
 
-__device__ __forceinline__ uint32_t scan_key_of(const BlockDesc& B, int z, int y, int x) {
-    return (B.nd_ws == 3) ? (uint32_t)(z + B.Z * (y + B.Y * x))
-                          : (uint32_t)((int64_t)z * B.Y * B.X + y + (int64_t)B.Y * x);
-}
-// scan key of a C-order index (outer block, or the inner block when inner != 0)
-__device__ __forceinline__ uint32_t scan_key_idx(const BlockDesc& B, int inner, uint32_t c) {
-    const int Y = inner ? B.IY : B.Y, X = inner ? B.IX : B.X;
-    const uint32_t yx = (uint32_t)Y * (uint32_t)X;
-    const int z = (int)(c / yx);
-    const uint32_t rem = c - (uint32_t)z * yx;
-    const int y = (int)(rem / (uint32_t)X);
-    const int x = (int)(rem - (uint32_t)y * (uint32_t)X);
-    if (inner) return (uint32_t)(z + B.IZ * (y + B.IY * x));
-    return scan_key_of(B, z, y, x);
-}
-
-// union by scan key: the root with the smaller key becomes the parent
-__device__ __forceinline__ void uf_union_scan(uint32_t* P, uint32_t a, uint32_t b, const BlockDesc& B, int inner) {
-    while (true) {
-        a = uf_find(P, a);
-        b = uf_find(P, b);
-        if (a == b) return;
-        if (scan_key_idx(B, inner, a) > scan_key_idx(B, inner, b)) {
-            const uint32_t t = a;
-            a = b;
-            b = t;
-        }
-        const uint32_t old = atomicCAS(&P[b], b, a);
-        if (old == b) return;
-        b = old;
-    }
-}
-
 // ---- local maxima classification ---------------------------------------------------------
 // cls bit0: a neighbour is strictly greater; bit1: a neighbour is equal (plateau voxel).
 // Neighbourhood: 6 (3-D ws) or 8 in-plane (2-D ws), as localMaxima3D / localMaxima.
@@ -119,46 +86,10 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
             eq |= w[k] == c;
         }
         cl[i] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
-        if (eq) Pp[B.base + i] = (uint32_t)i;  // plateau union-find init
-        nplat += eq;
+        nplat += eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
     })
     nplat = wg_reduce_u32(nplat, OpAdd());
     if (threadIdx.x == 0 && nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
-}
-
-// ---- plateau resolution: CC of equal values over plateau voxels (C-order keys) -----------
-__global__ void __launch_bounds__(256) k_plateau_union(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                       const float* __restrict__ v, const uint8_t* __restrict__ cls,
-                                                       uint32_t* __restrict__ Pg) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || !S[blockIdx.y].plateau) return;
-    const int Y = B.Y, X = B.X;
-    const int64_t YX = (int64_t)Y * X;
-    const float* p = v + B.base;
-    const uint8_t* cl = cls + B.base;
-    uint32_t* P = Pg + B.base;
-    BLOCK_LOOP(i, B) {
-        if (!(cl[i] & 2)) continue;
-        const int z = (int)(i / YX);
-        const int rem = (int)(i - z * YX);
-        const int y = rem / X, x = rem - (rem / X) * X;
-        const float c = p[i];
-        auto un = [&](int64_t j) {
-            if (p[j] == c) uf_union(P, (uint32_t)i, (uint32_t)j);
-        };
-        if (B.nd_ws == 3) {
-            if (z > 0) un(i - YX);
-            if (y > 0) un(i - X);
-            if (x > 0) un(i - 1);
-        } else {
-            if (y > 0) {
-                if (x > 0) un(i - X - 1);
-                un(i - X);
-                if (x + 1 < X) un(i - X + 1);
-            }
-            if (x > 0) un(i - 1);
-        }
-    }
 }
 
 // mark roots of plateaus that touch a strictly greater value (cls bit2 on the root)
@@ -175,49 +106,6 @@ __global__ void __launch_bounds__(256) k_plateau_flag(const BlockDesc* __restric
             cl[r] |= 4;  // benign race: every writer sets the same bit
         }
     }
-}
-
-// is voxel i a local maximum?
-__device__ __forceinline__ bool is_max(const uint8_t* cl, const uint32_t* P, int64_t i) {
-    const uint8_t c = cl[i];
-    if (c & 1) return false;
-    if (!(c & 2)) return true;
-    return !(cl[uf_find(P, (uint32_t)i)] & 4);
-}
-
-// ---- seed CC: init / union over maxima voxels (direct nbhd; in-plane in 2-D) -------------
-// PF (C-order index) = self for maxima voxels, kNoParent for the background.
-__global__ void __launch_bounds__(256) k_seed_init(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                   const uint8_t* __restrict__ cls, const uint32_t* __restrict__ Pp,
-                                                   uint32_t* __restrict__ PF) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
-    const uint8_t* cl = cls + B.base;
-    const uint32_t* P = Pp + B.base;
-    uint32_t* F = PF + B.base;
-    const bool plat = S[blockIdx.y].plateau != 0;
-    ROW_TILES(B.Z, B.Y, B.X, {
-        const uint8_t c = cl[i];
-        bool m = !(c & 1);
-        if (m && (c & 2) && plat) m = is_max(cl, P, i);
-        F[i] = m ? (uint32_t)i : kNoParent;
-    })
-}
-
-__global__ void __launch_bounds__(256) k_seed_union(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                    uint32_t* __restrict__ PFg) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
-    const int64_t YX = (int64_t)B.Y * B.X;
-    uint32_t* P = PFg + B.base;
-    ROW_TILES(B.Z, B.Y, B.X, {
-        if (P[i] != kNoParent) {
-            const uint32_t u = (uint32_t)i;
-            if (B.nd_ws == 3 && z > 0 && P[i - YX] != kNoParent) uf_union_scan(P, u, (uint32_t)(i - YX), B, 0);
-            if (y > 0 && P[i - B.X] != kNoParent) uf_union_scan(P, u, (uint32_t)(i - B.X), B, 0);
-            if (x > 0 && P[i - 1] != kNoParent) uf_union_scan(P, u, u - 1, B, 0);
-        }
-    })
 }
 
 // ---- root bitmap + exclusive prefix -----------------------------------------------------
@@ -269,7 +157,8 @@ __global__ void __launch_bounds__(256) k_chunk_scan(const BlockDesc* __restrict_
     }
     if (threadIdx.x == 0) {
         if (which_counter == 0) S[blockIdx.x].n_seeds = carry;
-        else S[blockIdx.x].n_cc = carry;
+        else if (which_counter == 1) S[blockIdx.x].n_cc = carry;
+        else S[blockIdx.x].n_auto = carry;
     }
 }
 
@@ -359,40 +248,14 @@ __device__ __forceinline__ int64_t outer_of_inner(const BlockDesc& B, int z, int
     return ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0);
 }
 
-__global__ void __launch_bounds__(256) k_crop_init(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                   const uint32_t* __restrict__ ws, uint32_t* __restrict__ PFg) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || !B.crop) return;
-    uint32_t* P = PFg + B.ibase;
-    ROW_TILES(B.IZ, B.IY, B.IX, { P[i] = ws[B.base + outer_of_inner(B, z, y, x)] ? (uint32_t)i : kNoParent; })
-}
-
-__global__ void __launch_bounds__(256) k_crop_union(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                    const uint32_t* __restrict__ ws, uint32_t* __restrict__ PFg) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || !B.crop) return;
-    uint32_t* P = PFg + B.ibase;
-    const uint32_t* w = ws + B.base;
-    const int64_t oyx = (int64_t)B.Y * B.X, iyx = (int64_t)B.IY * B.IX;
-    ROW_TILES(B.IZ, B.IY, B.IX, {
-        const int64_t o = outer_of_inner(B, z, y, x);
-        const uint32_t v = w[o];
-        if (v) {
-            const uint32_t u = (uint32_t)i;
-            if (z > 0 && w[o - oyx] == v) uf_union_scan(P, u, (uint32_t)(i - iyx), B, 1);
-            if (y > 0 && w[o - B.X] == v) uf_union_scan(P, u, (uint32_t)(i - B.IX), B, 1);
-            if (x > 0 && w[o - 1] == v) uf_union_scan(P, u, u - 1, B, 1);
-        }
-    })
-}
-
-// ---- uint64 output: (crop CC label | ws) + id offset on in-mask voxels ---------------------
-// direct != 0 (no block of the batch is cropped): the final ws label is computed here from the
-// flood result as k_finalize_ws would (3-D: masked -> 0; 2-D: per-slice label + slice offset),
-// saving that pass
+// ---- uint64 output: crop CC label (cropped blocks) or final ws label, + id offset ----------
+// Cropped blocks (watershed.py:327-330): the label is the labelVolumeWithBackground number of
+// the voxel's component (k_tile_cc<.., CC_CROP> + k_root_label; kNoParent = background).
+// Otherwise the final ws label is computed from the flood result as _apply_watershed leaves
+// it: 3-D: masked -> 0 (:245-248); 2-D: per-slice label + slice offset, masked -> 0 (:220-237).
 __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D, BlockStat* S,
-                                                const uint32_t* __restrict__ ws, const uint32_t* __restrict__ PFg,
-                                                int direct, const uint64_t* __restrict__ key, int packed,
+                                                const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
+                                                int packed, const uint32_t* __restrict__ PFg,
                                                 const uint32_t* __restrict__ sb, const uint32_t* __restrict__ soff) {
     const BlockDesc& B = D[blockIdx.y];
     const bool active = S[blockIdx.y].active;
@@ -405,13 +268,13 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
         uint64_t v = 0;  // empty block: constant offset (watershed.py:310-321)
         if (active) {
             uint32_t l;
-            if (direct) {
-                l = flood_label(ws, key, packed, B.base + o);
+            if (B.crop) {
+                const uint32_t p = P[i];
+                l = p == kNoParent ? 0u : cc_label(P, p);
+            } else {
+                l = flood_label(lab, key, packed, B.base + o);
                 if (!inm) l = 0;
                 else if (B.nd_ws == 2) l = (l - sb[B.sbase + z + B.iz0]) + soff[B.sbase + z + B.iz0];
-            } else {
-                l = ws[B.base + o];
-                if (B.crop && l) l = cc_label(P, P[i]);
             }
             mx = max(mx, l);
             v = l;

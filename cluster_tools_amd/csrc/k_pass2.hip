@@ -111,9 +111,9 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
 
 // insert keys whose scan-order predecessor holds a different key (only those can be the
 // first appearance); the table keeps the smallest scan key per value
-__global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__ D, const BlockStat* S,
+__global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__ D, BlockStat* S,
                                                    const uint64_t* __restrict__ vkey, uint64_t* __restrict__ hkey,
-                                                   uint32_t* __restrict__ hpos, uint32_t* __restrict__ err) {
+                                                   uint32_t* __restrict__ hpos) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__
             }
             s = (s + 1) & (cap - 1);
         }
-        if (!done) atomicOr(err, 1u);  // table full
+        if (!done) atomicOr(&S[blockIdx.y].err, kErrHashFull);  // table full: this block fails
     }
 }
 
@@ -227,9 +227,9 @@ __global__ void __launch_bounds__(256) k_p2_excl_zero(const BlockDesc* __restric
 
 // 2-D: with the slice offsets known, no shifted new seed may equal an initial value of its
 // slice (else relabelConsecutive would have merged them: unsupported, err bit 1)
-__global__ void __launch_bounds__(256) k_p2_check(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                  const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ soff,
-                                                  uint32_t* __restrict__ err) {
+__global__ void __launch_bounds__(256) k_p2_check(const BlockDesc* __restrict__ D, BlockStat* S,
+                                                  const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ soff) {
+    uint32_t* err = &S[blockIdx.y].err;
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || B.nd_ws != 2) return;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -239,12 +239,12 @@ __global__ void __launch_bounds__(256) k_p2_check(const BlockDesc* __restrict__ 
         if (i == (int64_t)z * YX) {
             // a shifted new seed that wraps to 0 would have become background
             const uint32_t t0 = 0u - (uint32_t)B.id_offset - soff[B.sbase + z];
-            if (t0 && hash_find(hkey + B.hbase, B.hcap, ((uint64_t)z << 33) | t0) >= 0) atomicOr(err, 2u);
+            if (t0 && hash_find(hkey + B.hbase, B.hcap, ((uint64_t)z << 33) | t0) >= 0) atomicOr(err, kErrCollision);
         }
         if (u == 0 || (uint32_t)u == 0) continue;
         const uint32_t t = (uint32_t)u - (uint32_t)B.id_offset - soff[B.sbase + z];
         if (t == 0) continue;
-        if (hash_find(hkey + B.hbase, B.hcap, ((uint64_t)z << 33) | t) >= 0) atomicOr(err, 2u);
+        if (hash_find(hkey + B.hbase, B.hcap, ((uint64_t)z << 33) | t) >= 0) atomicOr(err, kErrCollision);
     }
 }
 

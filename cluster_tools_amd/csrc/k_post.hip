@@ -91,6 +91,209 @@ __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, c
         if (sh[j]) atomicAdd(&c[j], sh[j]);
 }
 
+// 2-D ws: the labels of slice z are the block labels (sb[z], sb[z + 1]] (seeds are numbered
+// slice-major), so each workgroup counts a quarter of one slice into a small LDS histogram of
+// that range — no contention on a block-wide table of tens of thousands of labels.
+constexpr int kHist2dBins = 8192;
+__global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
+                                                int packed, const uint32_t* __restrict__ sb,
+                                                uint32_t* __restrict__ counts, int splits) {
+    __shared__ uint32_t sh[kHist2dBins];
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int z = blockIdx.x / splits, s = blockIdx.x % splits;
+    if (z >= B.Z) return;
+    const uint32_t b0 = sb[B.sbase + z];
+    const uint32_t b1 = z + 1 < B.Z ? sb[B.sbase + z + 1] : S[blockIdx.y].n_seeds;
+    const uint32_t nb = b1 - b0;  // labels b0 + 1 .. b1 -> bins 0 .. nb - 1
+    const bool use_lds = nb <= (uint32_t)kHist2dBins;
+    if (use_lds)
+        for (uint32_t j = threadIdx.x; j < nb; j += 256) sh[j] = 0;
+    __syncthreads();
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const int64_t i0 = (int64_t)z * YX + YX * s / splits, i1 = (int64_t)z * YX + YX * (s + 1) / splits;
+    uint32_t* c = counts + B.base + b0 + 1;
+    const int lane = threadIdx.x & 63;
+    constexpr int U = 8;
+    for (int64_t ib = i0; ib < i1; ib += 256 * U) {
+        uint32_t lv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = ib + u * 256 + threadIdx.x;
+            lv[u] = i < i1 ? flood_label(lab, key, packed, B.base + i) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t l = lv[u];
+            const bool ok = l > b0 && l <= b1;  // 0 (unreached) is not counted
+            const uint32_t l0 = __shfl(l, 0);
+            const uint64_t same = __ballot(ok && l == l0);
+            const uint64_t act = __ballot(ok);
+            if (same == act) {
+                if (lane == 0 && act) {
+                    if (use_lds) atomicAdd(&sh[l0 - b0 - 1], (uint32_t)__popcll(act));
+                    else atomicAdd(&c[l0 - b0 - 1], (uint32_t)__popcll(act));
+                }
+            } else if (ok) {
+                if (use_lds) atomicAdd(&sh[l - b0 - 1], 1u);
+                else atomicAdd(&c[l - b0 - 1], 1u);
+            }
+        }
+    }
+    if (!use_lds) return;
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nb; j += 256)
+        if (sh[j]) atomicAdd(&c[j], sh[j]);
+}
+
+// Size filter + regrow initialisation for the frontier relaxation (packed keys).  The regrow
+// is watershedsNew(hmap, seeds=seg) on the filtered labels (volume_utils.py:131-139): every
+// surviving voxel is a seed pushed with priority h (key (h, 0, label)), every removed voxel is
+// reset.  The open bitmap gets the removed voxels and the changed bitmap the survivors, so
+// the first frontier is exactly the removed voxels next to a survivor (k_frontier, k_flood.hip).
+// survivors[slice (2-D) / 0 (3-D)] = 1 if any label survives there.
+__global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     uint32_t size_filter, const uint32_t* __restrict__ counts,
+                                                     const uint8_t* __restrict__ excl, const float* __restrict__ h,
+                                                     uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
+                                                     uint64_t* __restrict__ open, uint64_t* __restrict__ chg,
+                                                     uint32_t* __restrict__ survivors) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t nrows = (int64_t)B.Z * B.Y;
+    const int wpr = (B.X + 63) >> 6;
+    constexpr uint64_t kLab = (1ull << 20) - 1ull;
+    for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
+        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
+            uint64_t kv[kRows];
+            uint8_t fx[kRows];
+#pragma unroll
+            for (int rr = 0; rr < kRows; ++rr) {
+                const int64_t gi = B.base + (r0 + rr) * B.X + x;
+                const bool ok = r0 + rr < nrows;
+                kv[rr] = ok ? key[gi] : kInfKey;
+                fx[rr] = ok ? fixedv[gi] : 0;
+            }
+#pragma unroll
+            for (int rr = 0; rr < kRows; ++rr) {
+                const int64_t row = r0 + rr;
+                if (row >= nrows) break;
+                const int64_t gi = B.base + row * B.X + x;
+                const uint32_t l = kv[rr] == kInfKey ? 0u : (uint32_t)(kv[rr] & kLab);
+                const bool keep = l != 0 && (counts[B.base + l] >= size_filter || (excl && excl[B.base + l]));
+                if (keep) {
+                    if (!fx[rr]) {
+                        key[gi] = ((uint64_t)ordf(h[gi]) << 32) | (uint64_t)l;
+                        fixedv[gi] = 1;
+                    }
+                } else {
+                    if (kv[rr] != kInfKey) key[gi] = kInfKey;
+                    if (fx[rr]) fixedv[gi] = 0;
+                }
+                const uint64_t op = __ballot(!keep);
+                const uint64_t kp = __ballot(keep);
+                if ((threadIdx.x & 63) == 0) {
+                    open[B.fbase + row * wpr + (x >> 6)] = op;
+                    chg[B.fbase + row * wpr + (x >> 6)] = kp;
+                    if (kp) {
+                        uint32_t* sv = survivors + B.sbase + (B.nd_ws == 2 ? (int)(row / B.Y) : 0);
+                        if (!*sv) *sv = 1;
+                    }
+                }
+            }
+        }
+}
+
+// Auto-seeded regrow: a slice (2-D) / block (3-D) whose every segment was removed leaves
+// watershedsNew an all-zero seed image, and vigra then seeds from the strict local minima of
+// the hmap (direct nbhd, labelled in scan order; oracle/ctws_oracle.cpp:local_minima_strict).
+// Strict minima are never adjacent, so each one is its own seed: its bit is set at its scan
+// key in W, and its label is 1 + its rank among the slice's / block's minima.
+__global__ void __launch_bounds__(256) k_auto_minima(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     const float* __restrict__ h,
+                                                     const uint32_t* __restrict__ survivors,
+                                                     uint64_t* __restrict__ W) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const float* p = h + B.base;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const int64_t nrows = (int64_t)B.Z * B.Y;
+    for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
+        const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
+        if (survivors[B.sbase + (B.nd_ws == 2 ? z : 0)]) continue;
+        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
+            const int64_t i = row * B.X + x;
+            const float c = p[i];
+            bool mn = c < 3.402823466e+38f;
+            if (B.nd_ws == 3) {
+                if (z > 0) mn &= c < p[i - YX];
+                if (z + 1 < B.Z) mn &= c < p[i + YX];
+            }
+            if (y > 0) mn &= c < p[i - B.X];
+            if (y + 1 < B.Y) mn &= c < p[i + B.X];
+            if (x > 0) mn &= c < p[i - 1];
+            if (x + 1 < B.X) mn &= c < p[i + 1];
+            if (mn) {
+                const uint32_t f = scan_key_of(B, z, y, x);
+                atomicOr((unsigned long long*)&W[B.wbase + (f >> 6)], 1ull << (f & 63));
+            }
+        }
+    }
+}
+
+// the minima become fixed seeds of the regrow (after k_bitmap_csum / k_chunk_scan /
+// k_word_prefix over W).  2-D: label = sb[z] + per-slice rank (the slice's own labels are all
+// gone; label ranges of different slices may overlap, which is harmless because slices never
+// meet in 2-D).  Pass 2: the reference maps the result through new_to_old (takeDict,
+// two_pass_watershed.py:173/204), which has no entry beyond the slice's / block's relabelled
+// seed count: such a block fails like the reference (kErrTakeDict).
+__global__ void __launch_bounds__(256) k_auto_seed_set(const BlockDesc* __restrict__ D, BlockStat* S,
+                                                       const float* __restrict__ h,
+                                                       const uint32_t* __restrict__ survivors,
+                                                       const uint64_t* __restrict__ W, const uint32_t* __restrict__ Wp,
+                                                       const uint32_t* __restrict__ sb, uint64_t* __restrict__ key,
+                                                       uint8_t* __restrict__ fixedv, uint64_t* __restrict__ open,
+                                                       uint64_t* __restrict__ chg) {
+    const BlockDesc& B = D[blockIdx.y];
+    BlockStat& st = S[blockIdx.y];
+    if (!st.active) return;
+    const int64_t nrows = (int64_t)B.Z * B.Y;
+    const int wpr = (B.X + 63) >> 6;
+    const uint64_t* Wb = W + B.wbase;
+    const uint32_t* Wpb = Wp + B.wbase;
+    uint32_t err = 0;
+    for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
+        const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
+        if (survivors[B.sbase + (B.nd_ws == 2 ? z : 0)]) continue;
+        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
+            const uint32_t f = scan_key_of(B, z, y, x);
+            if (!((Wb[f >> 6] >> (f & 63)) & 1ull)) continue;
+            uint32_t l = bitmap_rank(Wb, Wpb, f) + 1u;
+            if (B.nd_ws == 2) {
+                const uint32_t ls = l - bitmap_rank(Wb, Wpb, (uint32_t)((int64_t)z * B.Y * B.X));
+                const uint32_t m = (z + 1 < B.Z ? sb[B.sbase + z + 1] : st.n_seeds) - sb[B.sbase + z];
+                if (B.pass2 && ls > m) err |= kErrTakeDict;
+                l = sb[B.sbase + z] + ls;
+            } else if (B.pass2 && l > st.n_seeds) {
+                err |= kErrTakeDict;
+            }
+            if (l >= (1u << 20) - 1u) {
+                err |= kErrLabelBits;
+                continue;
+            }
+            const int64_t gi = B.base + row * B.X + x;
+            key[gi] = ((uint64_t)ordf(h[gi]) << 32) | (uint64_t)l;
+            fixedv[gi] = 1;
+            const int64_t wi = B.fbase + row * wpr + (x >> 6);
+            const uint64_t bit = 1ull << (x & 63);
+            atomicAnd((unsigned long long*)&open[wi], ~bit);
+            atomicOr((unsigned long long*)&chg[wi], bit);
+        }
+    }
+    if (err) atomicOr(&st.err, err);
+}
+
 // zero small segments; survivors become the regrow seeds (fixed, key (h, 0, label)).
 // Packed keys: a voxel that is already fixed (seed or steepest-descent voxel of the first
 // flood) holds exactly that key, so only voxels the relaxation reached (a minority) and
@@ -175,31 +378,36 @@ __global__ void __launch_bounds__(256) k_size_filter(const BlockDesc* __restrict
 
 // per-slice max_id (2-D ws): max per-slice label over in-mask voxels (all voxels without a
 // mask).  Equals watershedsNew's maxRegionLabel of the (regrow) flood when unmasked.
+// Grid (Z * splits, blocks): a workgroup reduces a quarter of one slice and issues one atomic.
+// all == 0 skips cropped blocks (their output is the crop CC numbering, which needs no offsets).
 __global__ void __launch_bounds__(256) k_slice_max(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                    const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
                                                    int packed, const uint32_t* __restrict__ sb,
-                                                   uint32_t* __restrict__ smax) {
+                                                   uint32_t* __restrict__ smax, int splits, int all) {
     const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || B.nd_ws != 2) return;
+    if (!S[blockIdx.y].active || B.nd_ws != 2 || (B.crop && !all)) return;
+    const int z = blockIdx.x / splits, s = blockIdx.x % splits;
+    if (z >= B.Z) return;
     const int64_t YX = (int64_t)B.Y * B.X;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < B.N; i0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = i0 + threadIdx.x;
-        uint32_t v = 0;
-        int z = -1;
-        if (i < B.N) {
-            z = (int)(i / YX);
-            const uint32_t l = flood_label(lab, key, packed, B.base + i);
-            if (l && (!B.mask || B.mask[i])) v = l - sb[B.sbase + z];
+    const int64_t i0 = (int64_t)z * YX + YX * s / splits, i1 = (int64_t)z * YX + YX * (s + 1) / splits;
+    const uint32_t base = sb[B.sbase + z];
+    uint32_t v = 0;
+    constexpr int U = 8;
+    for (int64_t ib = i0; ib < i1; ib += 256 * U) {
+        uint32_t lv[U];
+        bool in[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = ib + u * 256 + threadIdx.x;
+            lv[u] = i < i1 ? flood_label(lab, key, packed, B.base + i) : 0u;
+            in[u] = i < i1 && (!B.mask || B.mask[i]);
         }
-        // one atomic per wave when the wave lies in one slice (the common case)
-        const int z0 = __shfl(z, 0);
-        if (__all(z == z0 || z < 0)) {
-            for (int s = 32; s > 0; s >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, s));
-            if ((threadIdx.x & 63) == 0 && v && z0 >= 0) atomic_max_if(&smax[B.sbase + z0], v);
-        } else if (v) {
-            atomic_max_if(&smax[B.sbase + z], v);
-        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (lv[u] && in[u]) v = max(v, lv[u] - base);
     }
+    v = wg_reduce_u32(v, OpMax());
+    if (threadIdx.x == 0 && v) atomicMax(&smax[B.sbase + z], v);
 }
 
 // exclusive scan over slices of max_id (uint32 arithmetic, as `wsz += offset` on uint32)

@@ -10,7 +10,7 @@ import threading
 
 import numpy as np
 
-from ._abi import CtwsBlock, make_cfg, dtype_code, CTWS_OK
+from ._abi import CtwsBlock, make_cfg, dtype_code, CTWS_OK, CTWS_BLOCK_FAILED  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libctws.so')
@@ -49,6 +49,11 @@ def lib():
             L.ctws_comm_unique_id.argtypes = [C.c_void_p, C.c_void_p]
             L.ctws_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
             L.ctws_allgather_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
+            L.ctws_unique_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
+                                          C.POINTER(C.c_int64)]
+            L.ctws_lookup_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
+                                          C.c_int64, C.POINTER(C.c_int64)]
+            L.ctws_set_table_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
             L.ctws_debug_set_stop.argtypes = [C.c_void_p, C.c_int]
             L.ctws_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_int64]
             _lib = L
@@ -57,7 +62,8 @@ def lib():
 
 EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
                     'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_comm_unique_id', 'ctws_comm_init',
-                    'ctws_allgather_counts', 'ctws_debug_set_stop', 'ctws_debug_read')
+                    'ctws_allgather_counts', 'ctws_unique_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
+                    'ctws_debug_set_stop', 'ctws_debug_read')
 
 
 class CtwsError(RuntimeError):
@@ -95,6 +101,11 @@ class Handle:
         if ret != CTWS_OK:
             msg = lib().ctws_last_error(self._h)
             raise CtwsError("%s failed (%i): %s" % (what, ret, msg.decode() if msg else ''))
+
+    def last_error(self):
+        """Message of the last call (also set, with status CTWS_BLOCK_FAILED, for failed blocks)."""
+        msg = lib().ctws_last_error(self._h)
+        return msg.decode() if msg else ''
 
     def timings(self):
         n = lib().ctws_last_timings(self._h, None, None, 0)
@@ -206,6 +217,45 @@ class Handle:
             c.output = out.data_ptr()
         self._check(lib().ctws_ws_blocks_device(self._h, C.byref(cfg), arr, n), 'ctws_ws_blocks_device')
         return [(int(arr[i].status), int(arr[i].max_label)) for i in range(n)]
+
+    # ---- RelabelWorkflow kernels ---------------------------------------------------------
+    def unique_u64(self, labels):
+        """np.unique of a uint64 label array on the GPU (sorted).  numpy in, numpy out."""
+        lab = np.ascontiguousarray(labels, dtype=np.uint64).ravel()
+        n = C.c_int64(0)
+        cap = 1024
+        while True:
+            out = np.empty(cap, dtype=np.uint64)
+            ret = lib().ctws_unique_u64(self._h, lab.ctypes.data, lab.size, 0, out.ctypes.data, cap, C.byref(n))
+            if ret == -1 and n.value > cap:
+                cap = n.value
+                continue
+            self._check(ret, 'ctws_unique_u64')
+            return out[:n.value]
+
+    def set_table_u64(self, keys, values):
+        """Upload an assignment table (keys ascending) and keep it resident on the GPU."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        values = np.ascontiguousarray(values, dtype=np.uint64)
+        assert keys.shape == values.shape and keys.ndim == 1
+        self._check(lib().ctws_set_table_u64(self._h, keys.ctypes.data, values.ctypes.data, keys.size),
+                    'ctws_set_table_u64')
+
+    def lookup_u64(self, labels, keys=None, values=None):
+        """takeDict: labels (uint64 ndarray, modified in place) through the table keys -> values
+        (keys ascending; None: the resident table).  Returns the number of labels absent from
+        the table (they are left unchanged)."""
+        assert labels.dtype == np.uint64 and labels.flags.c_contiguous
+        kp = vp = None
+        nt = 0
+        if keys is not None:
+            keys = np.ascontiguousarray(keys, dtype=np.uint64)
+            values = np.ascontiguousarray(values, dtype=np.uint64)
+            kp, vp, nt = keys.ctypes.data, values.ctypes.data, keys.size
+        miss = C.c_int64(0)
+        self._check(lib().ctws_lookup_u64(self._h, labels.ctypes.data, labels.size, 0, kp, vp, nt, C.byref(miss)),
+                    'ctws_lookup_u64')
+        return int(miss.value)
 
     # ---- multi-GPU label-count exchange (RCCL) ------------------------------------------
     def comm_unique_id(self):

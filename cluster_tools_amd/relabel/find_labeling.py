@@ -1,7 +1,7 @@
 #! /usr/bin/env python
 """FindLabeling: consecutive new ids for the global uniques, as an (N, 2) uint64 assignment
-table (cluster_tools/relabel/find_labeling.py:20-126): 0 stays 0 if present, else ids start
-at 1."""
+table (cluster_tools/relabel/find_labeling.py:20-126; task surface unchanged), merged on the
+GPU: 0 stays 0 if present, else ids start at 1."""
 import json
 import os
 import sys
@@ -56,30 +56,38 @@ class FindLabelingLSF(FindLabelingBase, LSFTask):
 
 
 def find_labeling(job_id, config_path):
+    """Job entry (find_labeling.py:84-126): the global sorted uniques and their new ids.
+
+    The jobs' unique arrays are merged by a GPU unique (ctws_unique_u64); new ids are
+    consecutive in the order of the old ones, starting at 0 when 0 is present (it keeps id 0),
+    else at 1.  The (N, 2) uint64 table [old, new] is written to assignment_path/key.
+    """
+    from cluster_tools_amd import ctws
     fu.log("start processing job %i" % job_id)
     fu.log("reading config from %s" % config_path)
     with open(config_path) as f:
         config = json.load(f)
     tmp = config['tmp_folder']
     fu.log("read uniques")
-    uniques = np.concatenate([np.load(os.path.join(tmp, 'find_uniques_job_%i.npy' % j))
-                              for j in range(config['n_jobs'])])
+    parts = [np.load(os.path.join(tmp, 'find_uniques_job_%i.npy' % j)) for j in range(config['n_jobs'])]
     fu.log("compute uniques")
-    uniques = np.unique(uniques)
-    start, stop = (0, len(uniques)) if uniques[0] == 0 else (1, len(uniques) + 1)
-    fu.log("relabel to new max-id %i" % stop)
-    new_ids = np.arange(start, stop, dtype='uint64')
-    assignments = np.concatenate([uniques[:, None].astype('uint64'), new_ids[:, None]], axis=1)
+    with ctws.Handle(int(os.environ.get('CTWS_DEVICE', '0'))) as h:
+        old_ids = h.unique_u64(np.concatenate(parts))
+    first = 0 if (len(old_ids) and old_ids[0] == 0) else 1
+    n_ids = first + len(old_ids)
+    fu.log("relabel to new max-id %i" % n_ids)
+    table = np.empty((len(old_ids), 2), dtype='uint64')
+    table[:, 0] = old_ids
+    table[:, 1] = np.arange(first, n_ids, dtype='uint64')
     fu.log("saving results to %s/%s" % (config['assignment_path'], config['assignment_key']))
     with vu.file_reader(config['assignment_path']) as f:
-        chunks = (min(int(1e6), len(assignments)), 2)
         if config['assignment_key'] in f:
             import shutil
             shutil.rmtree(os.path.join(config['assignment_path'], config['assignment_key']))
-        ds = f.create_dataset(config['assignment_key'], shape=assignments.shape, dtype='uint64',
-                              compression='gzip', chunks=chunks)
+        ds = f.create_dataset(config['assignment_key'], shape=table.shape, dtype='uint64', compression='gzip',
+                              chunks=(max(1, min(1000000, len(table))), 2))
         ds.n_threads = config.get('threads_per_job', 1)
-        ds[:] = assignments
+        ds[:] = table
     fu.log_job_success(job_id)
 
 

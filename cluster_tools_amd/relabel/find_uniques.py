@@ -1,10 +1,10 @@
 #! /usr/bin/env python
-"""FindUniques: per-job unique labels of the watershed output
-(cluster_tools/relabel/find_uniques.py:20-159).  numpy implementation; the GPU version of the
-relabel stage is the next row of SURVEY.md §8(f)."""
+"""FindUniques: per-job unique labels of the watershed output on the GPU
+(cluster_tools/relabel/find_uniques.py:20-159; task surface unchanged)."""
 import json
 import os
 import sys
+from concurrent import futures
 
 import numpy as np
 
@@ -58,39 +58,49 @@ class FindUniquesLSF(FindUniquesBase, LSFTask):
     pass
 
 
-def uniques_in_block(block_id, blocking, ds, return_counts):
-    fu.log("start processing block %i" % block_id)
-    labels = ds[vu.block_to_bb(blocking.getBlock(block_id))]
-    if labels.sum() == 0:
-        if return_counts:
-            return np.array([0], dtype=labels.dtype), np.array([labels.size], dtype='int64')
-        return np.array([0], dtype=labels.dtype)
-    res = np.unique(labels, return_counts=return_counts)
-    fu.log_block_success(block_id)
-    return res
+def _device():
+    return int(os.environ.get('CTWS_DEVICE', os.environ.get('LOCAL_RANK', '0')))
 
 
 def find_uniques(job_id, config_path):
+    """Job entry (find_uniques.py:115-159): the sorted unique ids of the job's blocks.
+
+    Every block goes through the GPU bitmap unique (ctws_unique_u64, k_relabel.hip); the
+    per-block id sets are then merged by one more GPU unique over their concatenation.
+    Blocks are read ahead on a thread while the GPU works.  As in the reference, an all-zero
+    block contributes [0] without logging "processed block" (find_uniques.py:97-101).
+    """
+    from cluster_tools_amd import ctws
     fu.log("start processing job %i" % job_id)
     fu.log("reading config from %s" % config_path)
     with open(config_path) as f:
         config = json.load(f)
-    return_counts = config['return_counts']
-    with vu.file_reader(config['input_path'], 'r') as f:
+    if config['return_counts']:
+        raise NotImplementedError("find_uniques with return_counts (post-processing workflows) is outside "
+                                  "the watershed path; only the relabel mode is implemented")
+    block_list = config['block_list']
+    with vu.file_reader(config['input_path'], 'r') as f, ctws.Handle(_device()) as h, \
+            futures.ThreadPoolExecutor(1) as io:
         ds = f[config['input_key']]
         blocking = Blocking([0, 0, 0], list(ds.shape), list(config['block_shape']))
-        uniques = [uniques_in_block(b, blocking, ds, return_counts) for b in config['block_list']]
-    tmp = config['tmp_folder']
-    if return_counts:
-        unique_values = np.unique(np.concatenate([u[0] for u in uniques]))
-        counts = np.zeros(int(unique_values[-1] + 1), dtype='uint64')
-        for ub, cb in uniques:
-            counts[ub] += cb.astype('uint64')
-        counts = counts[counts != 0]
-        np.save(os.path.join(tmp, 'counts_job_%i.npy' % job_id), counts)
-    else:
-        unique_values = np.unique(np.concatenate(uniques))
-    np.save(os.path.join(tmp, 'find_uniques_job_%i.npy' % job_id), unique_values)
+
+        def read(block_id):
+            return ds[vu.block_to_bb(blocking.getBlock(block_id))]
+
+        per_block = []
+        nxt = io.submit(read, block_list[0]) if block_list else None
+        for k, block_id in enumerate(block_list):
+            fu.log("start processing block %i" % block_id)
+            labels = nxt.result()
+            nxt = io.submit(read, block_list[k + 1]) if k + 1 < len(block_list) else None
+            u = h.unique_u64(labels)
+            per_block.append(u)
+            if not (len(u) == 1 and u[0] == 0):
+                fu.log_block_success(block_id)
+        unique_values = h.unique_u64(np.concatenate(per_block)) if per_block else np.zeros(0, 'uint64')
+    save_path = os.path.join(config['tmp_folder'], 'find_uniques_job_%i.npy' % job_id)
+    fu.log("saving results to %s" % save_path)
+    np.save(save_path, unique_values)
     fu.log_job_success(job_id)
 
 

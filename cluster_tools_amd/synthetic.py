@@ -27,11 +27,15 @@ def _u01(seed, idx):
     return (h >> np.uint64(40)).astype(np.float64) * (1.0 / (1 << 24))
 
 
-def boundary_map(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='float32', z_chunk=16):
-    """Voronoi boundary map of `shape` (Z, Y, X)."""
+def boundary_map(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='float32', z_chunk=16, origin=(0, 0, 0),
+                 full_shape=None):
+    """Voronoi boundary map of `shape` (Z, Y, X); with `full_shape`, the sub-volume
+    [origin, origin + shape) of the map of `full_shape` (as boundary_map_torch)."""
     shape = tuple(int(s) for s in shape)
+    full = tuple(int(s) for s in (full_shape or shape))
+    gz0, gy0, gx0 = (int(o) for o in origin)
     pz, py, px = (float(p) for p in pitch)
-    ncz, ncy, ncx = (int(np.ceil(s / p)) + 2 for s, p in zip(shape, (pz, py, px)))
+    ncz, ncy, ncx = (int(np.ceil(s / p)) + 2 for s, p in zip(full, (pz, py, px)))
     # points for cells -1 .. nc-2 along each axis (one ring of padding cells)
     cz, cy, cx = np.meshgrid(np.arange(ncz), np.arange(ncy), np.arange(ncx), indexing='ij')
     cell = (cz * ncy + cy) * ncx + cx
@@ -44,12 +48,13 @@ def boundary_map(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='float32',
     ptx = ((cx - 1) + 0.1 + 0.8 * jx) * px
     out = np.empty(shape, dtype=np.dtype(dtype))
     Y, X = shape[1], shape[2]
-    yy, xx = np.meshgrid(np.arange(Y, dtype=np.float64), np.arange(X, dtype=np.float64), indexing='ij')
+    FY, FX = full[1], full[2]
+    yy, xx = np.meshgrid(gy0 + np.arange(Y, dtype=np.float64), gx0 + np.arange(X, dtype=np.float64), indexing='ij')
     icy = (yy // py).astype(np.int64) + 1
     icx = (xx // px).astype(np.int64) + 1
     for z0 in range(0, shape[0], z_chunk):
         z1 = min(shape[0], z0 + z_chunk)
-        zz = np.arange(z0, z1, dtype=np.float64)[:, None, None]
+        zz = np.arange(gz0 + z0, gz0 + z1, dtype=np.float64)[:, None, None]
         icz = (zz // pz).astype(np.int64) + 1
         d1 = np.full((z1 - z0, Y, X), np.inf)
         d2 = np.full((z1 - z0, Y, X), np.inf)
@@ -65,9 +70,9 @@ def boundary_map(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='float32',
                     d2 = np.where(closer, d1, np.minimum(d2, d))
                     d1 = np.where(closer, d, d1)
         b = np.clip(1.0 - (d2 - d1) / 2.5, 0.0, 1.0)
-        vidx = (np.arange(z0, z1, dtype=np.uint64)[:, None, None] * np.uint64(Y) +
-                np.arange(Y, dtype=np.uint64)[None, :, None]) * np.uint64(X) + \
-            np.arange(X, dtype=np.uint64)[None, None, :]
+        vidx = (np.arange(gz0 + z0, gz0 + z1, dtype=np.uint64)[:, None, None] * np.uint64(FY) +
+                np.arange(gy0, gy0 + Y, dtype=np.uint64)[None, :, None]) * np.uint64(FX) + \
+            np.arange(gx0, gx0 + X, dtype=np.uint64)[None, None, :]
         b = b + noise * (2.0 * _u01(seed + 7919, vidx) - 1.0)
         b = np.clip(b, 0.0, 1.0)
         if out.dtype == np.uint8:
@@ -75,6 +80,14 @@ def boundary_map(shape, seed=0, pitch=(24, 24, 24), noise=0.05, dtype='float32',
         else:
             out[z0:z1] = b.astype(out.dtype)
     return out
+
+
+def ellipsoid_mask_sub(shape, origin, full_shape):
+    """`ellipsoid_mask(full_shape)[origin:origin + shape]` (numpy)."""
+    ax = [((np.arange(o, o + s, dtype=np.float64) + 0.5) / f - 0.5) / 0.5
+          for s, o, f in zip(shape, origin, full_shape)]
+    r = ax[0][:, None, None] ** 2 + ax[1][None, :, None] ** 2 + ax[2][None, None, :] ** 2
+    return (r <= 1.0).astype(np.uint8)
 
 
 def ellipsoid_mask(shape):

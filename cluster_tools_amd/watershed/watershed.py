@@ -137,8 +137,47 @@ def _device():
     return int(os.environ.get('CTWS_DEVICE', os.environ.get('LOCAL_RANK', '0')))
 
 
+def _overlaps(a, b):
+    return all(sa.start < sb.stop and sb.start < sa.stop for sa, sb in zip(a, b))
+
+
+def make_batches(blocking, block_list, config, pass_id, batch_blocks):
+    """Split the job's block list (in order) into GPU batches.
+
+    Pass 0 reads only ds_in, so any split works.  Pass 1 (`_ws_pass2`) reads ds_out[input_bb]:
+    in the reference's sequential loop (two_pass_watershed.py:296-299) a block sees the writes
+    of the blocks before it, and in the checkerboard a block's halo corners can overlap the
+    inner block of a diagonal neighbour of the same colour.  A batch reads all its blocks
+    before any of them is written, so a block starts a new batch when its input bb overlaps
+    the output bb of a block already in the current batch.
+    """
+    batches, cur, cur_out = [], [], []
+    for bid in block_list:
+        if pass_id == 1:
+            input_bb, _, _ = _get_bbs(blocking, bid, config)
+            if any(_overlaps(input_bb, ob) for ob in cur_out):
+                batches.append(cur)
+                cur, cur_out = [], []
+        if len(cur) >= batch_blocks:
+            batches.append(cur)
+            cur, cur_out = [], []
+        cur.append(bid)
+        if pass_id == 1:
+            cur_out.append(_get_bbs(blocking, bid, config)[2])
+    if cur:
+        batches.append(cur)
+    return batches
+
+
 def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, batch_blocks=None):
-    """Run `_ws_block` (pass 0) or `_ws_pass2` (pass 1) for `block_list` on the GPU."""
+    """Run `_ws_block` (pass 0) or `_ws_pass2` (pass 1) for `block_list` on the GPU.
+
+    Blocks are processed in batches with the same observable behaviour as the reference's
+    sequential loop: outputs are written and "processed block" is logged in block-list order;
+    a block the kernels cannot finish (status CTWS_BLOCK_FAILED, e.g. the reference's own
+    takeDict failure) raises after the blocks before it are written, as the reference job
+    would raise at that block.
+    """
     from cluster_tools_amd import ctws
     block_shape = list(config['block_shape'])
     lib_config = dict(config)
@@ -148,15 +187,17 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
     if config.get('non_maximum_suppression', True if pass_id == 1 else False):
         fu.log("non-maximum suppression was activated, but is not available")
     batch_blocks = batch_blocks or int(config.get('gpu_batch_blocks', 16))
-    batches = [block_list[i:i + batch_blocks] for i in range(0, len(block_list), batch_blocks)]
+    batches = make_batches(blocking, block_list, config, pass_id, batch_blocks)
     n_io = max(1, int(config.get('threads_per_job', 1)))
     ds_in.n_threads = ds_out.n_threads = max(n_io, 4)
 
     def read_batch(ids):
         return [_read_block(blocking, bid, ds_in, ds_out, mask, config, pass_id) for bid in ids]
 
-    def write_batch(blocks, results):
+    def write_batch(blocks, results, error):
         for b, r in zip(blocks, results):
+            if r is not None and r['status'] == ctws.CTWS_BLOCK_FAILED:
+                raise ctws.CtwsError("block %i: %s" % (b['block_id'], error))
             if r is not None and r['status'] in (0, 2):   # written / empty block: constant offset
                 ds_out[b['output_bb']] = r['output']
             fu.log_block_success(b['block_id'])
@@ -166,15 +207,23 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
         pending_write = None
         for bi in range(len(batches)):
             blocks = nxt.result()
-            nxt = io.submit(read_batch, batches[bi + 1]) if bi + 1 < len(batches) else None
+            if pass_id == 0:
+                # inputs never depend on outputs: read the next batch while this one runs
+                nxt = io.submit(read_batch, batches[bi + 1]) if bi + 1 < len(batches) else None
             for b in blocks:
                 fu.log("start processing block %i" % b['block_id'])
             todo = [b for b in blocks if not b.get('skip')]
             res = h.ws_blocks(lib_config, block_shape, todo, pass_id=pass_id) if todo else []
+            error = h.last_error()
             by_id = {b['block_id']: r for b, r in zip(todo, res)}
             if pending_write is not None:
                 pending_write.result()
-            pending_write = io.submit(write_batch, blocks, [by_id.get(b['block_id']) for b in blocks])
+            pending_write = io.submit(write_batch, blocks, [by_id.get(b['block_id']) for b in blocks], error)
+            if pass_id == 1:
+                # the next batch's halos may hold this batch's outputs: read after the write
+                pending_write.result()
+                pending_write = None
+                nxt = io.submit(read_batch, batches[bi + 1]) if bi + 1 < len(batches) else None
         if pending_write is not None:
             pending_write.result()
 

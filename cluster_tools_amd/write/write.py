@@ -1,10 +1,11 @@
 #! /usr/bin/env python
 """Write: apply an assignment table to every block and set attrs['maxId']
-(cluster_tools/write/write.py:28-329).  numpy implementation of takeDict (sorted-table
-lookup); the pickled-dict assignment form is not supported (no unpickling of data)."""
+(cluster_tools/write/write.py:28-329; task surface unchanged).  takeDict runs on the GPU
+(k_u64_lookup); the pickled-dict assignment form is not supported (no unpickling of data)."""
 import json
 import os
 import sys
+from concurrent import futures
 
 import numpy as np
 
@@ -89,21 +90,38 @@ class WriteLSF(WriteBase, LSFTask):
     pass
 
 
-def _apply_table(seg, table, allow_empty):
-    """nt.takeDict with an (N, 2) assignment table sorted by old id."""
-    keys, vals = table[:, 0], table[:, 1]
-    order = np.argsort(keys, kind='stable')
-    keys, vals = keys[order], vals[order]
-    pos = np.clip(np.searchsorted(keys, seg), 0, len(keys) - 1)
-    hit = keys[pos] == seg
-    if not hit.all():
-        if not allow_empty:
-            raise KeyError("labels missing from the assignment table")
-        return np.where(hit, vals[pos], seg)
-    return vals[pos]
+def _load_table(path, key):
+    """The assignment as (keys ascending, values): an (N, 2) / (2, N) table [old, new], or a
+    1-D array mapping index -> value (write.py:229-261; pickled dicts are not loaded)."""
+    with vu.file_reader(path, 'r') as f:
+        node_labels = np.asarray(f[key][:])
+    if node_labels.ndim == 0:
+        node_labels = node_labels.reshape(1)
+    if node_labels.ndim == 1:
+        return np.arange(len(node_labels), dtype='uint64'), node_labels.astype('uint64'), True
+    if node_labels.shape[1] == 2:
+        keys, values = node_labels[:, 0], node_labels[:, 1]
+    elif node_labels.shape[0] == 2:
+        keys, values = node_labels[0], node_labels[1]
+    else:
+        raise ValueError("Invalid shape for 2d node labels")
+    keys = keys.astype('uint64')
+    values = values.astype('uint64')
+    if len(keys) > 1 and not (keys[1:] > keys[:-1]).all():
+        order = np.argsort(keys, kind='stable')   # FindLabeling tables are sorted already
+        keys, values = keys[order], values[order]
+    return keys, values, False
 
 
 def write(job_id, config_path):
+    """Job entry (write.py:264-329): every block through the assignment on the GPU.
+
+    The table is uploaded once per job and stays resident (ctws_set_table_u64); each block is
+    read (next one ahead on a thread), mapped by k_u64_lookup (binary search per voxel) and
+    written back.  All-zero blocks are skipped, labels missing from the table raise unless
+    allow_empty_assignments (then they keep their id), job 0 writes attrs['maxId'].
+    """
+    from cluster_tools_amd import ctws
     fu.log("start processing job %i" % job_id)
     fu.log("loading config from %s" % config_path)
     with open(config_path) as f:
@@ -112,36 +130,42 @@ def write(job_id, config_path):
     output_path = config.get('output_path', input_path)
     output_key = config.get('output_key', input_key)
     allow_empty = config.get('allow_empty_assignments', False)
-    with vu.file_reader(config['assignment_path'], 'r') as f:
-        table = f[config['assignment_key']][:]
-    if table.ndim == 1:
-        table = np.stack([np.arange(len(table), dtype='uint64'), table.astype('uint64')], axis=1)
-    elif table.shape[1] != 2:
-        table = table.T
-    offsets = None
+    keys, values, is_array = _load_table(config['assignment_path'], config['assignment_key'])
+    offsets, skip = None, set()
     if config.get('offset_path'):
+        fu.log("loading offsets from %s" % config['offset_path'])
         with open(config['offset_path']) as f:
             oc = json.load(f)
-        offsets, empty_blocks = oc['offsets'], set(oc['empty_blocks'])
-    with vu.file_reader(input_path) as f_in, vu.file_reader(output_path) as f_out:
+        offsets, skip = oc['offsets'], set(oc['empty_blocks'])
+    block_list = [b for b in config['block_list'] if b not in skip]
+    with vu.file_reader(input_path) as f_in, vu.file_reader(output_path) as f_out, \
+            ctws.Handle(int(os.environ.get('CTWS_DEVICE', '0'))) as h, futures.ThreadPoolExecutor(1) as io:
         ds_in, ds_out = f_in[input_key], f_out[output_key]
         blocking = Blocking([0, 0, 0], list(ds_in.shape), list(config['block_shape']))
-        for block_id in config['block_list']:
-            if offsets is not None and block_id in empty_blocks:
-                continue
-            fu.log("start processing block %i" % block_id)
+        h.set_table_u64(keys, values)
+
+        def read(block_id):
             bb = vu.block_to_bb(blocking.getBlock(block_id))
-            seg = ds_in[bb]
-            mask = seg != 0
-            if mask.sum() == 0:
+            return bb, np.ascontiguousarray(ds_in[bb], dtype='uint64')
+
+        nxt = io.submit(read, block_list[0]) if block_list else None
+        for k, block_id in enumerate(block_list):
+            fu.log("start processing block %i" % block_id)
+            bb, seg = nxt.result()
+            nxt = io.submit(read, block_list[k + 1]) if k + 1 < len(block_list) else None
+            nz = seg != 0
+            if not nz.any():
                 fu.log_block_success(block_id)
                 continue
             if offsets is not None:
-                seg[mask] += np.uint64(offsets[block_id])
-            ds_out[bb] = _apply_table(seg, table, allow_empty)
+                seg[nz] += np.uint64(offsets[block_id])
+            missing = h.lookup_u64(seg)
+            if missing and (is_array or not allow_empty):
+                raise KeyError("block %i: %i labels are not in the assignment table" % (block_id, missing))
+            ds_out[bb] = seg
             fu.log_block_success(block_id)
         if job_id == 0:
-            ds_out.attrs['maxId'] = int(table[:, 1].max())
+            ds_out.attrs['maxId'] = int(values.max()) if len(values) else 0
     fu.log_job_success(job_id)
 
 

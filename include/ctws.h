@@ -68,6 +68,9 @@ extern "C" {
 #define CTWS_BLOCK_SKIPPED_MASK 1  /* inner mask empty: nothing written (:295-297)     */
 #define CTWS_BLOCK_EMPTY        2  /* nothing above threshold: constant offset written */
 #define CTWS_BLOCK_EMPTY_PASS2  3  /* pass 2, nothing above threshold: nothing written */
+#define CTWS_BLOCK_FAILED       4  /* the block cannot be finished: nothing written;    */
+                                   /* the reason is in ctws_last_error (the reference   */
+                                   /* job would raise at this block)                    */
 
 /*
  * Task configuration.  Mirrors the watershed task config keys
@@ -155,6 +158,28 @@ int ctws_comm_unique_id(ctws_handle* h, void* unique_id_128);
 int ctws_comm_init(ctws_handle* h, int nranks, int rank, const void* unique_id_128);
 int ctws_allgather_counts(ctws_handle* h, const int64_t* local_counts, int64_t n_local,
                           int64_t* all_counts /* nranks * n_local */);
+
+/*
+ * RelabelWorkflow (relabel/find_uniques.py:93-159, find_labeling.py:84-126,
+ * write/write.py:153-226) on the GPU.  on_device = 1: labels/out/keys/values are device
+ * pointers on the handle's GPU; 0: host pointers (staged through HBM).
+ *
+ * ctws_unique_u64: the sorted unique values of labels[0..n) (np.unique) into out[0..cap);
+ *   *n_unique = their number (also when cap is too small: then CTWS_EINVAL, retry with a
+ *   larger buffer).  The nonzero values must span < 2^35 (always true for watershed ids of
+ *   volumes below 2^35 voxels), else CTWS_EUNSUPPORTED.
+ * ctws_set_table_u64: upload an assignment table (host keys ascending, values) and keep it
+ *   resident on the handle (one upload per Write job instead of one per block).
+ * ctws_lookup_u64: labels[i] <- values[j] where keys[j] == labels[i] (keys ascending;
+ *   nifty.tools.takeDict); labels absent from the table are left unchanged and counted in
+ *   *n_missing (takeDict would raise: the caller raises).  keys == values == NULL: use the
+ *   resident table; host keys/values (on_device = 0) become the resident table.
+ */
+int ctws_set_table_u64(ctws_handle* h, const uint64_t* keys, const uint64_t* values, int64_t n_table);
+int ctws_unique_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_device, uint64_t* out, int64_t cap,
+                    int64_t* n_unique);
+int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, const uint64_t* keys,
+                    const uint64_t* values, int64_t n_table, int64_t* n_missing);
 
 /*
  * Test hooks (used by the parity tests, not by the task code): stop the pipeline after a

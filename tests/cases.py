@@ -29,7 +29,18 @@ def make_cases():
     xw512 = _x(seed=10, shape=(8, 16, 512))
     xw600 = np.stack([_x(seed=s, shape=(3, 16, 600)) for s in (11, 12)])
     xw1000 = _x(seed=13, shape=(8, 12, 1000))
+    # slices 0-3 of pure noise (only small segments) over a regular map: with size_filter 200
+    # every segment of those slices is removed and vigra auto-seeds their regrow from the hmap
+    # minima, while the other slices keep segments (volume_utils.py:131-139)
+    xn = _x(seed=14).copy()
+    rng = np.random.RandomState(5)
+    xn[:4] = rng.rand(4, SHAPE[1], SHAPE[2]).astype(np.float32)
     return {
+        '3d_sizefilter_all': (dict(D3, size_filter=10 ** 9), dict(input=x)),
+        '2d_sizefilter_all': (dict(size_filter=10 ** 9), dict(input=x)),
+        '2d_sizefilter_noise_slices': (dict(size_filter=200), dict(input=xn)),
+        '2d_sizefilter_noise_halo': (dict(size_filter=200, halo=[0, 16, 16]),
+                                     dict(input=xn, inner_begin=inner[0], inner_shape=inner[1], crop_relabel=True)),
         '3d_wide512_mask': (dict(D3), dict(input=xw512, mask=ellipsoid_mask(xw512.shape))),
         '2d_wide600_4d': ({}, dict(input=xw600)),
         '3d_wide1000': (dict(D3), dict(input=xw1000)),
