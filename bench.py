@@ -116,11 +116,37 @@ def blocking(shape, block_shape, halo):
     return out
 
 
-def slab_origin(cfg, rank):
-    if 'slab' not in cfg:
-        return (0, 0, 0)
-    full = cfg['full_shape']
-    return (((cfg['slab'] + rank) % (full[0] // cfg['shape'][0])) * cfg['shape'][0], 0, 0)
+def volume_geometry(cfg, rank=0, world=1):
+    """The rank's share of the workload (weak scaling: the per-GPU work is fixed).
+
+    Every rank owns a z-slab of cfg['shape'] of one volume: config 5's slabs are those of the
+    2048^3 volume (slab cfg['slab'] on one GPU, slab `rank` on N); the other configs stack N
+    slabs into an (N * Z, Y, X) volume of the same synthetic map.  A rank processes the
+    blocks of the volume's global block grid whose inner block lies in its slab, with their
+    full halos (the input of a halo that reaches into a neighbouring slab is generated from
+    the same map), and global block ids.  Returns full (volume shape), z0 (slab start),
+    g0 / gshape (the generated region: slab + z halos) and the blocks with bounding boxes in
+    region coordinates.
+    """
+    Z, Y, X = cfg['shape']
+    if 'full_shape' in cfg:
+        full = tuple(cfg['full_shape'])
+        slab = cfg['slab'] if world == 1 else rank % (full[0] // Z)
+    else:
+        full = (Z * world, Y, X)
+        slab = rank
+    z0 = slab * Z
+    hz = cfg['halo'][0]
+    g0, g1 = max(0, z0 - hz), min(full[0], z0 + Z + hz)
+    blocks = []
+    for b in blocking(full, cfg['block_shape'], cfg['halo']):
+        if not z0 <= b['beg'][0] < z0 + Z:
+            continue
+        d = dict(b)
+        for k in ('beg', 'end', 'obeg', 'oend'):
+            d[k] = [d[k][0] - g0] + list(d[k][1:])
+        blocks.append(d)
+    return dict(full=full, z0=z0, g0=g0, gshape=(g1 - g0, Y, X), lo=z0 - g0, hi=g1 - (z0 + Z), blocks=blocks)
 
 
 # ---- CPU baseline (oracle) -----------------------------------------------------------------
@@ -138,11 +164,11 @@ def _cpu_job(args):
     from oracle import oracle as O
     from cluster_tools_amd.synthetic import boundary_map, ellipsoid_mask_sub
     cfg = CONFIGS[cfg_id]
-    origin = slab_origin(cfg, 0)
-    full = cfg.get('full_shape', cfg['shape'])
-    ob = [o + a for o, a in zip(b['obeg'], origin)]
+    geo = volume_geometry(cfg)
+    full = geo['full']
+    ob = [b['obeg'][0] + geo['g0']] + list(b['obeg'][1:])
     oshape = [e - s for s, e in zip(b['obeg'], b['oend'])]
-    x = boundary_map(oshape, seed=cfg['seed'] if 'full_shape' not in cfg else 0, pitch=cfg.get('pitch', (24, 24, 24)),
+    x = boundary_map(oshape, seed=cfg['seed'], pitch=cfg.get('pitch', (24, 24, 24)),
                      dtype=cfg.get('dtype', 'float32'), origin=ob, full_shape=full)
     blk = dict(input=x, block_id=b['block_id'], inner_begin=[s - o for s, o in zip(b['beg'], b['obeg'])],
                inner_shape=[e - s for s, e in zip(b['beg'], b['end'])],
@@ -154,6 +180,13 @@ def _cpu_job(args):
     res = O.ws_blocks(cfg['task'], cfg['block_shape'], [blk])[0]
     t1 = time.time()
     return t0, t1, (res['output'] if want_output else None)
+
+
+def block_colour(cfg, geo, b):
+    """Checkerboard colour of a block: 0 for the list of block 0 (make_checkerboard_block_lists,
+    volume_utils.py:142-205: even coordinate sum)."""
+    c = [(bb + (geo['g0'] if k == 0 else 0)) // s for k, (bb, s) in enumerate(zip(b['beg'], cfg['block_shape']))]
+    return sum(c) % 2
 
 
 def cpu_model():
@@ -174,13 +207,10 @@ def cpu_baseline(cfg_id, max_cores=16):
     from oracle import oracle as O
     O.build()
     cfg = CONFIGS[cfg_id]
-    blist = blocking(cfg['shape'], cfg['block_shape'], cfg['halo'])
+    geo = volume_geometry(cfg)
+    blist = geo['blocks']
     if cfg.get('two_pass'):
-        from cluster_tools_amd.utils.blocking import Blocking
-        from cluster_tools_amd.utils import volume_utils as vu
-        first = set(vu.make_checkerboard_block_lists(Blocking([0, 0, 0], list(cfg['shape']),
-                                                              list(cfg['block_shape'])))[0])
-        blist = [b for b in blist if b['block_id'] in first]   # pass-0 blocks (_ws_block)
+        blist = [b for b in blist if block_colour(cfg, geo, b) == 0]   # pass-1 blocks (_ws_block)
     cores = min(max_cores, len(os.sched_getaffinity(0)))
     n_jobs = min(len(blist), cores)
     ctx = mp.get_context('fork')
@@ -227,6 +257,7 @@ def main():
     import torch.distributed as dist
     from cluster_tools_amd import ctws
     from cluster_tools_amd.synthetic import boundary_map_torch, ellipsoid_mask_torch
+    from cluster_tools_amd.watershed import sharded
 
     torch.cuda.set_device(local_rank)
     dev = torch.device('cuda', local_rank)
@@ -234,15 +265,16 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
 
     shape = tuple(cfg['shape'])
-    full = cfg.get('full_shape', shape)
-    origin = slab_origin(cfg, rank)
-    seed = (cfg['seed'] + 1000 * rank) if 'full_shape' not in cfg else 0
-    gen = dict(seed=seed, device=dev, dtype=cfg.get('dtype', 'float32'), pitch=cfg.get('pitch', (24, 24, 24)),
+    geo = volume_geometry(cfg, rank, world)
+    full = geo['full']
+    origin = (geo['g0'], 0, 0)
+    gen = dict(seed=cfg['seed'], device=dev, dtype=cfg.get('dtype', 'float32'), pitch=cfg.get('pitch', (24, 24, 24)),
                origin=origin, full_shape=full)
-    vol = boundary_map_torch(shape, **gen)
-    mvol = ellipsoid_mask_torch(shape, origin, full, device=dev) if cfg.get('mask') else None
-    blist = blocking(shape, cfg['block_shape'], cfg['halo'])
-    out_vol = torch.zeros(shape, dtype=torch.int64, device=dev) if two_pass else None
+    vol = boundary_map_torch(geo['gshape'], **gen)
+    mvol = ellipsoid_mask_torch(geo['gshape'], origin, full, device=dev) if cfg.get('mask') else None
+    blist = geo['blocks']
+    # two-pass: the pass-1 labels of the region (own slab + z halos from the neighbour ranks)
+    out_vol = torch.zeros(geo['gshape'], dtype=torch.int64, device=dev) if two_pass else None
 
     def sl(beg, end):
         return tuple(slice(a, b) for a, b in zip(beg, end))
@@ -267,10 +299,8 @@ def main():
         outer_vox += int(inp.numel())
     del vol
     if two_pass:
-        from cluster_tools_amd.utils.blocking import Blocking
-        from cluster_tools_amd.utils import volume_utils as vu
-        lists = vu.make_checkerboard_block_lists(Blocking([0, 0, 0], list(shape), list(cfg['block_shape'])))
-        passes = [[blocks[i] for i in lst if i in blocks] for lst in lists]
+        colour = {b['block_id']: block_colour(cfg, geo, b) for b in blist}
+        passes = [[blocks[i] for i in sorted(blocks) if colour[i] == c] for c in (0, 1)]
         for b in passes[1]:
             b['crop_relabel'] = False
             b['initial_seeds'] = torch.empty(tuple(b['input'].shape[-3:]), dtype=torch.int64, device=dev)
@@ -294,6 +324,8 @@ def main():
         res = []
         for pid, pblocks in enumerate(passes):
             if pid == 1:
+                # the neighbour slabs' pass-1 labels in the z halos (RCCL point-to-point)
+                sharded.exchange_z_halos(out_vol, geo['lo'], geo['hi'])
                 for b in pblocks:  # initial_seeds = ds_out[input_bb] (two_pass_watershed.py:228)
                     b['initial_seeds'].copy_(out_vol[b['osl']])
             # contiguous shares of the pass's blocks, one per handle (stream)
@@ -310,18 +342,19 @@ def main():
                     for k, v in hh.timings().items():
                         into[k] = into.get(k, 0.0) + v
             if two_pass:
-                for b, (st, _) in zip(pblocks, r):
+                for b, (st, _, _) in zip(pblocks, r):
                     if st in (0, 2):
                         out_vol[b['isl']] = b['output']
             res += r
-        # compact global id offsets: exclusive scan of the per-block label counts of all ranks
-        # (relabel/find_labeling.py:104-116 over RCCL instead of .npy files)
-        counts.copy_(torch.tensor([m for _, m in res], dtype=torch.int64))
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, counts)
-        else:
-            gathered.copy_(counts)
-        offsets['scan'] = torch.cumsum(gathered, 0) - gathered
+        if not two_pass:
+            # compact global id offsets: exclusive scan of the per-block distinct-id counts of
+            # all ranks (relabel/find_labeling.py:104-116 over RCCL instead of .npy files)
+            counts.copy_(torch.tensor([k for _, _, k in res], dtype=torch.int64))
+            if world > 1:
+                dist.all_gather_into_tensor(gathered, counts)
+            else:
+                gathered.copy_(counts)
+            offsets['scan'] = torch.cumsum(gathered, 0) - gathered
         return res
 
     for _ in range(args.warmup):
@@ -421,7 +454,8 @@ def main():
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': cfg.get('dtype', 'float32').replace('float', 'f'),
             'data': 'synthetic',
-            'config': {'workload': cfg['workload'], 'volume': list(shape), 'block_shape': list(cfg['block_shape']),
+            'config': {'workload': cfg['workload'], 'volume': list(shape), 'full_volume': list(full),
+                       'block_shape': list(cfg['block_shape']),
                        'halo': list(cfg['halo']), 'blocks_per_gpu': nblocks, 'passes': len(passes),
                        'inner_voxels_per_gpu': inner_vox, 'outer_voxels_per_gpu': outer_vox,
                        'streams_per_gpu': nstreams, 'parallelism': 'blocks sharded, %d GPU(s)' % world},

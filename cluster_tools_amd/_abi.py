@@ -53,7 +53,7 @@ class CtwsBlock(C.Structure):
                 ('output', C.c_void_p),
                 ('max_label', C.c_uint64),
                 ('status', C.c_int32),
-                ('_pad1', C.c_int32)]
+                ('n_ids', C.c_int32)]
 
 
 def _sigma(value):

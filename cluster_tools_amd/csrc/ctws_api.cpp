@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -63,14 +64,18 @@ struct Workspace {
     int64_t cap_front = 0;
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
     uint32_t* fflags = nullptr;
-    uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: changed
+    uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: generation of its last change
+    uint32_t *wl0 = nullptr, *wl1 = nullptr, *qgen = nullptr;  // chunk worklists, queued generation
+    uint32_t* wlcnt = nullptr;  // worklist length per iteration
     int64_t cap_fstat = 0;
     uint32_t* fstat = nullptr;  // CTWS_TRACE statistics: open voxels, frontier visits per block
 };
 
 constexpr int kCounterBytes = 4 * (4 + 4 * kStatSlots);  // flood flag + statistics slots
 constexpr int kFrontierBatch = 8;        // frontier iterations per host check
+constexpr int kFrontierWavesHost = 4;    // waves per workgroup of k_frontier (kFrontierWaves)
 constexpr int kFrontierMaxIters = 256;   // then the tile flood takes over
+constexpr int kFrontierMaxItersCap = 4096;  // CTWS_FRONTIER_ITERS upper bound (worklist counters)
 
 }  // namespace
 
@@ -220,9 +225,13 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(fopen, front);
         ALLOC(fchunk0, front / 64 + 1);
         ALLOC(fchunk1, front / 64 + 1);
+        ALLOC(wl0, front / 64 + 1);
+        ALLOC(wl1, front / 64 + 1);
+        ALLOC(qgen, front / 64 + 1);
         w.cap_front = front;
     }
     if (!w.fflags) ALLOC(fflags, kFrontierBatch);
+    if (!w.wlcnt) ALLOC(wlcnt, kFrontierMaxItersCap + 2);
     if (blocks > w.cap_fstat) {
         ALLOC(fstat, 2 * blocks);
         w.cap_fstat = blocks;
@@ -507,43 +516,52 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
                  uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
     Workspace& w = h->ws;
-    uint64_t* fcur = w.front0;
-    uint64_t* fnext = w.front1;
-    uint32_t* ccur = w.fchunk0;
-    uint32_t* cnext = w.fchunk1;
-    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ccur, 1u, (size_t)(TF / 64 + 1), h->stream));
-    const dim3 fg((unsigned)std::min<int64_t>((TF / nb + 64 * 4 - 1) / (64 * 4) + 1, 2048), nb);
+    const int64_t nch = TF / 64 + 1;
+    uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
+    uint32_t* gen[2] = {w.fchunk0, w.fchunk1};  // iteration it writes gen[it & 1], reads gen[(it + 1) & 1]
+    uint32_t* wl[2] = {w.wl0, w.wl1};
+    HIPCHK(hipMemsetAsync(w.fchunk0, 0, sizeof(uint32_t) * (size_t)nch, h->stream));
+    HIPCHK(hipMemsetAsync(w.fchunk1, 0, sizeof(uint32_t) * (size_t)nch, h->stream));
+    HIPCHK(hipMemsetAsync(w.qgen, 0, sizeof(uint32_t) * (size_t)nch, h->stream));
+    HIPCHK(hipMemsetAsync(w.wlcnt, 0, sizeof(uint32_t) * (size_t)(h->frontier_max_iters + 2), h->stream));
+    // iteration 0: every chunk with an open voxel
+    const dim3 lg((unsigned)std::min<int64_t>((TF / nb + 64 * 64 * kFrontierWavesHost - 1) / (64 * 64 * kFrontierWavesHost) + 1,
+                                              1024), nb);
+    k_frontier_list0<<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt);
+    LAUNCHCHK();
+    // one wave per list entry; the largest list is every chunk of the batch
+    const unsigned fg = (unsigned)std::min<int64_t>((nch + kFrontierWavesHost - 1) / kFrontierWavesHost, 2048);
     bool converged = false;
     int fiters = 0;
-    for (fiters = 0; fiters < h->frontier_max_iters && !converged;) {
-        HIPCHK(hipMemsetAsync(w.fflags, 0, sizeof(uint32_t) * kFrontierBatch, h->stream));
-        for (int k = 0; k < kFrontierBatch; ++k) {
-#define CTWS_FRONTIER(ND, U)                                                                                   \
-    k_frontier<ND, U><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fcur, fnext, ccur, cnext, \
-                                                 w.fflags + k, fst ? fst + nb : nullptr, h->frontier_reps)
+    while (fiters < h->frontier_max_iters && !converged) {
+        const int it0 = fiters;
+        const int nl = std::min(kFrontierBatch, h->frontier_max_iters - it0);
+        for (int k = 0; k < nl; ++k) {
+            const int it = it0 + k;
+#define CTWS_FRONTIER(ND, U)                                                                                       \
+    k_frontier<ND, U><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], \
+                                                 gen[(it + 1) & 1], gen[it & 1], it, wl[it & 1], w.wlcnt + it,      \
+                                                 wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen,                        \
+                                                 fst ? fst + nb : nullptr, h->frontier_reps)
             const int fu = h->frontier_unroll;
             if (pl.nd_ws == 3) {
-                if (fu == 1) CTWS_FRONTIER(3, 1);
-                else if (fu == 2) CTWS_FRONTIER(3, 2);
-                else if (fu == 8) CTWS_FRONTIER(3, 8);
-                else CTWS_FRONTIER(3, 4);
+                if (fu == 2) CTWS_FRONTIER(3, 2);
+                else if (fu == 4) CTWS_FRONTIER(3, 4);
+                else CTWS_FRONTIER(3, 1);
             } else {
-                if (fu == 1) CTWS_FRONTIER(2, 1);
-                else if (fu == 2) CTWS_FRONTIER(2, 2);
-                else if (fu == 8) CTWS_FRONTIER(2, 8);
-                else CTWS_FRONTIER(2, 4);
+                if (fu == 2) CTWS_FRONTIER(2, 2);
+                else if (fu == 4) CTWS_FRONTIER(2, 4);
+                else CTWS_FRONTIER(2, 1);
             }
 #undef CTWS_FRONTIER
-            std::swap(fcur, fnext);
-            std::swap(ccur, cnext);
         }
         LAUNCHCHK();
-        HIPCHK(hipMemcpyAsync(h->h_counter, w.fflags, sizeof(uint32_t) * kFrontierBatch, hipMemcpyDeviceToHost,
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.wlcnt + it0 + 1, sizeof(uint32_t) * nl, hipMemcpyDeviceToHost,
                               h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
-        for (int k = 0; k < kFrontierBatch; ++k) {
+        for (int k = 0; k < nl; ++k) {
             ++fiters;
-            if (!h->h_counter[k]) {
+            if (!h->h_counter[k]) {  // nothing queued for the next iteration
                 converged = true;
                 break;
             }
@@ -568,6 +586,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
 }
 
 int cdiv(int a, int b) { return (a + b - 1) / b; }
+
 
 int64_t words_of(int64_t n) { return n / 64 + 1; }
 int64_t chunks_of(int64_t n) { return (words_of(n) + 255) / 256; }
@@ -750,6 +769,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     // row-tile kernels: kRows rows (z, y) per workgroup iteration
     const dim3 rg((unsigned)std::min<int64_t>((maxRows + kRows - 1) / kRows, 16384), nb);
     const dim3 rig((unsigned)std::min<int64_t>((maxIRows + kRows - 1) / kRows, 16384), nb);
+    // word-tile kernels: one wave per 64-voxel row word, kWordWaves waves per workgroup
+    const dim3 wtg((unsigned)std::min<int64_t>((maxRows * ((maxX + 63) / 64) + kWordWaves - 1) / kWordWaves, 65535), nb);
     size_t ev = 0;
     std::vector<const char*> names;
     auto mark = [&](const char* name) {
@@ -760,18 +781,49 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- normalize + threshold + EDT ------------------------------------------------------
     {
+        // one raw dtype and 3-D datasets in the batch: the typed kernels (global loads in flight)
+        int dt = desc[0].dtype;
+        bool typed = !h->prep_lds && maxX <= 1024;
+        bool all_exact = true;
+        for (auto& d : desc) {
+            typed &= d.dtype == dt && d.n_channels == 0;
+            all_exact &= d.X == maxX && (d.X == 256 || d.X == 512 || d.X == 1024) && d.n_channels == 0 && d.dtype == 3;
+        }
         dim3 g((unsigned)std::min<int64_t>((maxN + 65535) / 65536, 256), nb);
-        k_input_minmax<<<g, 256, 0, h->stream>>>(w.desc, w.stat);
+        if (typed) {
+            dim3 gm((unsigned)std::min<int64_t>((maxN + 8 * 256 - 1) / (8 * 256), 1024), nb);
+            if (dt == CTWS_U8) k_input_minmax_t<uint8_t><<<gm, 256, 0, h->stream>>>(w.desc, w.stat);
+            else if (dt == CTWS_U16) k_input_minmax_t<uint16_t><<<gm, 256, 0, h->stream>>>(w.desc, w.stat);
+            else if (dt == CTWS_F32) k_input_minmax_t<float><<<gm, 256, 0, h->stream>>>(w.desc, w.stat);
+            else k_input_minmax_t<double><<<gm, 256, 0, h->stream>>>(w.desc, w.stat);
+        } else {
+            k_input_minmax<<<g, 256, 0, h->stream>>>(w.desc, w.stat);
+        }
         LAUNCHCHK();
         PrepParams pp{(float)cfg->threshold, cfg->invert_inputs, cfg->agglomerate_channels, pl.pitch[2] * pl.pitch[2]};
         dim3 gx((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
-        // rows up to 1024 voxels: lanes own consecutive voxels in registers (k_prep_edt_x_reg)
-        if (maxX <= 256 && !h->prep_lds)
+        // rows up to 1024 voxels: one wave per row in registers.  f32 rows of exactly 64 K voxels
+        // move as float4 with lanes owning consecutive voxels (k_prep_edt_x_reg); other rows use
+        // the lane-interleaved coalesced layout (k_prep_edt_x_co)
+        auto launch_co = [&](auto kmax_c) {
+            constexpr int KM = decltype(kmax_c)::value;
+            if (dt == CTWS_U8) k_prep_edt_x_co<KM, uint8_t><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+            else if (dt == CTWS_U16) k_prep_edt_x_co<KM, uint16_t><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+            else if (dt == CTWS_F32) k_prep_edt_x_co<KM, float><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+            else k_prep_edt_x_co<KM, double><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+        };
+        if (typed && all_exact && maxX == 256)
             k_prep_edt_x_reg<4><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
-        else if (maxX <= 512 && !h->prep_lds)
+        else if (typed && all_exact && maxX == 512)
             k_prep_edt_x_reg<8><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
-        else if (maxX <= 1024 && !h->prep_lds)
+        else if (typed && all_exact && maxX == 1024)
             k_prep_edt_x_reg<16><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+        else if (typed && maxX <= 256)
+            launch_co(std::integral_constant<int, 4>());
+        else if (typed && maxX <= 512)
+            launch_co(std::integral_constant<int, 8>());
+        else if (typed && maxX <= 1024)
+            launch_co(std::integral_constant<int, 16>());
         else
             k_prep_edt_x<<<gx, 256, 4 * (size_t)maxX * 4, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
         LAUNCHCHK();
@@ -948,7 +1000,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         mark("descent_tile");
         if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
-        k_descent_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
+        k_descent_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
                                                   w.front0, fst);
         LAUNCHCHK();
         mark("flood_descent");
@@ -968,14 +1020,15 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             add_timing(h, "open_voxels", (float)no);
             add_timing(h, "frontier_visits", (float)nv);
         }
-        // fixpoint check (exact height ties can break the descent argument): else flood again
-        // from the seeds alone.  On by default; CTWS_VERIFY=0 turns it off.
+        // fixpoint check of every voxel (a guard: the descent argument and the frontier's
+        // convergence make a violation impossible); on a violation the batch is flooded again
+        // from the seeds alone.  On by default (CTWS_VERIFY=0 turns it off).
         if (h->verify) {
             HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
             if (pl.nd_ws == 3)
-                k_flood_verify<3><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
+                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
             else
-                k_flood_verify<2><<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
+                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
             LAUNCHCHK();
             HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
@@ -1016,29 +1069,39 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int n_auto_blocks = 0;
     if (cfg->size_filter > 0) {
         uint32_t* counts = (uint32_t*)w.A;
-        k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
-        if (pl.nd_ws == 2) {
-            // one LDS histogram per slice quarter over the slice's label range
-            k_hist2d<<<dim3((unsigned)maxZ * 4, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key,
-                                                                          packed ? 1 : 0, w.sb, counts, 4);
-        } else {
-            // 32K voxels per workgroup: the LDS histogram is cleared and flushed once per 128 voxels
-            dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 2048), nb);
-            const int bins = (int64_t)max_seeds + 1 <= kHistBins ? (int)max_seeds + 1 : 0;
-            k_hist<<<hg, 256, sizeof(uint32_t) * (size_t)bins, h->stream>>>(w.desc, w.stat, w.lab, w.key,
-                                                                            packed ? 1 : 0, counts, bins);
-        }
-        LAUNCHCHK();
+        auto histogram = [&]() -> int {
+            k_hist_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, counts);
+            if (pl.nd_ws == 2) {
+                // one LDS histogram per slice quarter over the slice's label range
+                const dim3 g2((unsigned)maxZ * 4, nb);
+                if (packed) k_hist2d<1><<<g2, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, w.sb, counts, 4);
+                else k_hist2d<0><<<g2, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, w.sb, counts, 4);
+            } else {
+                // 32K voxels per workgroup: the LDS histogram is cleared / flushed once per 128 voxels
+                dim3 hg((unsigned)std::min<int64_t>((maxN + 32767) / 32768, 2048), nb);
+                const int bins = (int64_t)max_seeds + 1 <= kHistBins ? (int)max_seeds + 1 : 0;
+                const size_t lds = sizeof(uint32_t) * (size_t)bins;
+                if (packed) k_hist<1><<<hg, 256, lds, h->stream>>>(w.desc, w.stat, w.lab, w.key, counts, bins);
+                else k_hist<0><<<hg, 256, lds, h->stream>>>(w.desc, w.stat, w.lab, w.key, counts, bins);
+            }
+            LAUNCHCHK();
+            return CTWS_OK;
+        };
+        if ((r = histogram()) != CTWS_OK) return r;
         if (packed) {
             // survivors -> regrow seeds, removed voxels -> open; then the frontier relaxation
-            HIPCHK(hipMemsetAsync(w.surv, 0, sizeof(uint32_t) * TS, h->stream));
-            k_regrow_init<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts, excl, w.hm,
-                                                     w.key, w.cls, w.fopen, w.front0, w.surv);
-            LAUNCHCHK();
             std::vector<BlockStat> s3(nb);
-            HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipMemcpyAsync(s3.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
+            auto regrow_init = [&]() -> int {
+                HIPCHK(hipMemsetAsync(w.surv, 0, sizeof(uint32_t) * TS, h->stream));
+                k_regrow_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts, excl,
+                                                         w.hm, w.key, w.cls, w.fopen, w.front0, w.surv);
+                LAUNCHCHK();
+                HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+                HIPCHK(hipMemcpyAsync(s3.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
+                HIPCHK(hipStreamSynchronize(h->stream));
+                return CTWS_OK;
+            };
+            if ((r = regrow_init()) != CTWS_OK) return r;
             for (int i = 0; i < nb; ++i) {
                 if (!s3[i].active) continue;
                 const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
@@ -1143,7 +1206,13 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             LAUNCHCHK();
         }
         mark("crop_cc");
-        k_output<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff);
+        bool any_plain = false;
+        for (int i = 0; i < nb; ++i) any_plain |= desc[i].crop == 0;
+        // uncropped blocks count their distinct ids in W (cropped blocks: n_cc of the crop CC)
+        if (any_plain) HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+        k_output<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
+                                             (unsigned long long*)w.W);
+        if (any_plain) k_count_ids<<<dim3(64, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.W);
         LAUNCHCHK();
         mark("output");
     }
@@ -1177,6 +1246,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : (pl.pass2 ? CTWS_BLOCK_EMPTY_PASS2 : CTWS_BLOCK_EMPTY);
         blocks[i].max_label = st[i].active ? st[i].max_label : 0;
+        // distinct nonzero output ids: the labels, plus the bare offset of unlabelled in-mask
+        // voxels (empty block: only that one, watershed.py:310-321); block 0's offset is 0
+        const uint32_t bare = (st[i].active ? st[i]._p[0] : 1u) && desc[i].id_offset != 0;
+        blocks[i].n_ids = pl.pass2 ? -1 : (int32_t)((st[i].active ? st[i].n_cc : 0u) + bare);
         if (!st[i].active) continue;
         uint32_t err = st[i].err;
         const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
@@ -1228,6 +1301,7 @@ int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, b
     for (int i = 0; i < n; ++i) {
         ctws_block& b = blocks[i];
         b.status = CTWS_BLOCK_WRITTEN;
+        b.n_ids = 0;
         b.max_label = 0;
         if (!device_ptrs && b.mask) {
             const int64_t* sh = b.outer_shape;
@@ -1258,7 +1332,7 @@ int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, b
         while (e < todo.size()) {
             const ctws_block& b = blocks[todo[e]];
             const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
-            if (e > k && vox + nv > budget) break;
+            if (e > k && (vox + nv > budget || e - k >= 4096)) break;  // <= 4096 blocks (worklist entries)
             vox += nv;
             ++e;
         }
@@ -1322,6 +1396,7 @@ int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, b
         }
         for (int i = 0; i < nb; ++i) {
             blocks[todo[k + i]].status = bb[i].status;
+            blocks[todo[k + i]].n_ids = bb[i].n_ids;
             blocks[todo[k + i]].max_label = bb[i].max_label;
         }
         k = e;
@@ -1349,7 +1424,8 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
-    if (const char* t = std::getenv("CTWS_FRONTIER_ITERS")) h->frontier_max_iters = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))
+        h->frontier_max_iters = std::max(0, std::min(kFrontierMaxItersCap, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_GAUSS_W")) {
         const int v = std::atoi(t);
         h->gauss_w = (v == 8 || v == 16 || v == 32) ? v : 0;
@@ -1377,7 +1453,7 @@ void ctws_close(ctws_handle* h) {
     Workspace& w = h->ws;
     void* ptrs[] = {w.fin, w.dt, w.A, w.Bf, w.sm, w.hm, w.cls, w.P, w.PF, w.lab, w.key, w.W, w.Wp, w.csum,
                     w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.lines0, w.lines1, w.desc, w.stat, w.counter,
-                    w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1,
+                    w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
                     w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
                     h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p};
     for (void* p : ptrs)

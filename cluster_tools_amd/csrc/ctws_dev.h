@@ -65,6 +65,22 @@ constexpr uint32_t kErrLabelBits = 4u;   // auto-seeded regrow: labels beyond th
 constexpr uint32_t kErrTakeDict = 8u;    // pass 2: auto-seed label without a new_to_old entry
 constexpr uint32_t kErrUnsupported = 16u; // auto-seeded regrow in a block with >= 2^20 seeds (wide keys)
 
+// Pointers read from the block descriptor are generic to the compiler: accesses through them
+// become flat loads, and the waits the compiler puts around flat accesses serialise a wave's
+// loads.  gbl() asserts the global address space, so they are global loads that stay in flight.
+template <class T>
+using gptr_t = const T __attribute__((address_space(1)))*;
+template <class T>
+__device__ __forceinline__ gptr_t<T> gbl(const T* p) {
+    return (gptr_t<T>)p;
+}
+template <class T>
+using gwptr_t = T __attribute__((address_space(1)))*;
+template <class T>
+__device__ __forceinline__ gwptr_t<T> gblw(T* p) {
+    return (gwptr_t<T>)p;
+}
+
 // order-preserving float <-> uint32 mapping (total order for non-NaN floats)
 __device__ __forceinline__ uint32_t ordf(float f) {
     uint32_t u = __float_as_uint(f);
@@ -225,6 +241,61 @@ __device__ __forceinline__ uint32_t flood_label(const uint32_t* lab, const uint6
         return k == kInfKey ? 0u : (uint32_t)(k & ((1ull << 20) - 1ull));
     }
     return lab[i] & ~kFixedBit;
+}
+
+// ---- word tiles --------------------------------------------------------------------------
+// A wave handles one 64-voxel word of a row (lane = x - 64 * word), kWordWaves_ waves per
+// workgroup, grid-stride over the block's Z * Y * ceil(X / 64) words.  Rows whose length is
+// not a multiple of 256 keep every lane busy (a row-tile loop x += 256 runs its last pass
+// over a 576-voxel row with a quarter of the threads), x-neighbours are lane shuffles, and
+// a word is exactly one word of the frontier bitmaps.  BODY sees z, y, x, i (block C-order
+// index), row, xw (word in the row), wpr and `valid` (x < nx); every lane runs BODY (ballots
+// are legal), invalid lanes must not touch memory.
+#define WORD_TILES(nz, ny, nx, ...)                                                                          \
+    {                                                                                                        \
+        const int wpr = ((nx) + 63) >> 6;                                                                    \
+        const int64_t nwords_ = (int64_t)(nz) * (ny) * wpr;                                                  \
+        const int lane = threadIdx.x & 63;                                                                   \
+        for (int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w_ < nwords_;        \
+             w_ += (int64_t)gridDim.x * (blockDim.x >> 6)) {                                                 \
+            const int64_t row = w_ / wpr;                                                                    \
+            const int xw = (int)(w_ - row * wpr);                                                            \
+            const int z = (int)(row / (ny));                                                                 \
+            const int y = (int)(row - (int64_t)z * (ny));                                                    \
+            const int x = xw * 64 + lane;                                                                    \
+            const bool valid = x < (nx);                                                                     \
+            const int64_t i = row * (nx) + x;                                                                \
+            (void)z;                                                                                         \
+            (void)y;                                                                                         \
+            __VA_ARGS__                                                                                      \
+        }                                                                                                    \
+    }
+
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+    return (uint64_t)__shfl_up((long long)v, d);
+}
+__device__ __forceinline__ uint64_t shfl_down_u64(uint64_t v, int d) {
+    return (uint64_t)__shfl_down((long long)v, d);
+}
+
+// ---- packed flood keys: C (ordered float bits, 32) | d (12, saturating) | label (20) ----------
+constexpr uint64_t kPackInf = ~0ull;
+constexpr uint32_t kLabelBits = 20;
+constexpr uint64_t kLabelMask = (1ull << kLabelBits) - 1ull;
+constexpr uint64_t kDOne = 1ull << kLabelBits;
+constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
+
+// K(q) = f_q(min over the neighbours): a neighbour key `best` pushed into voxel q of height hb
+__device__ __forceinline__ uint64_t f_packed(uint32_t hb, uint64_t best) {
+    const uint32_t c = (uint32_t)(best >> 32);
+    if (hb > c) return ((uint64_t)hb << 32) | (best & kLabelMask);
+    return ((best & kDMask) == kDMask) ? best : best + kDOne;
+}
+
+// seed test: from the seed CC parents (pass 1: `cc` = PF after k_root_label) or, when cc is
+// null, from lab (kFixedBit; pass 2 and the fallbacks)
+__device__ __forceinline__ bool is_seed(const uint32_t* lab, const uint32_t* cc, int64_t gi) {
+    return cc ? cc[gi] != kNoParent : (lab[gi] & kFixedBit) != 0;
 }
 
 // rank of key f among set bits of a per-block bitmap with per-word exclusive prefix

@@ -38,6 +38,10 @@ __global__ void k_input_minmax(const BlockDesc*, BlockStat*);
 __global__ void k_prep_edt_x(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
 template <int KMAX>
 __global__ void k_prep_edt_x_reg(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
+template <int KMAX, class T>
+__global__ void k_prep_edt_x_co(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
+template <class T>
+__global__ void k_input_minmax_t(const BlockDesc*, BlockStat*);
 template <int W>
 __global__ void k_edt_col(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*, uint32_t*,
                           uint32_t*);
@@ -71,7 +75,8 @@ __global__ void k_root_label(const BlockDesc*, const BlockStat*, int, uint32_t*,
 __global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const float*, uint32_t*, uint64_t*,
                              uint8_t*, int);
 __global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
-                         const uint32_t*, const uint32_t*);
+                         const uint32_t*, const uint32_t*, unsigned long long*);
+__global__ void k_count_ids(const BlockDesc*, BlockStat*, const uint64_t*);
 
 // k_tilecc.hip: LDS block-based union-find (plateaus, seed CC, halo-crop CC)
 enum CcMode { CC_PLATEAU = 0, CC_SEED = 1, CC_CROP = 2 };
@@ -116,24 +121,29 @@ __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*,
                                uint64_t*, uint64_t*, uint32_t*);
 template <int ND, int U>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                           const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
+                           const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
+                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
+__global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>
 __global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint32_t*,
                                const uint32_t*, uint32_t*);
+constexpr int kWordWaves = 4;  // waves per workgroup of the word-tiled kernels
 __global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
                               uint64_t*, uint8_t*);
 
 // k_post.hip
 __global__ void k_slice_seed_base(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
 __global__ void k_hist_zero(const BlockDesc*, const BlockStat*, uint32_t*);
-__global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, uint32_t*, int);
+template <int PACKED>
+__global__ void k_hist(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, uint32_t*, int);
 constexpr int kHistBins = 16384;  // largest LDS histogram of k_hist
 __global__ void k_size_filter(const BlockDesc*, const BlockStat*, FilterParams, const uint32_t*, const uint8_t*,
                               const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, int);
 __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
                             uint32_t*, int, int);
-__global__ void k_hist2d(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
+template <int PACKED>
+__global__ void k_hist2d(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
                          uint32_t*, int);
 __global__ void k_regrow_init(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*, const uint8_t*,
                               const float*, uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*);

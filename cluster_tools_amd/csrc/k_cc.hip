@@ -253,18 +253,23 @@ __device__ __forceinline__ int64_t outer_of_inner(const BlockDesc& B, int z, int
 // the voxel's component (k_tile_cc<.., CC_CROP> + k_root_label; kNoParent = background).
 // Otherwise the final ws label is computed from the flood result as _apply_watershed leaves
 // it: 3-D: masked -> 0 (:245-248); 2-D: per-slice label + slice offset, masked -> 0 (:220-237).
+// Uncropped blocks also mark their final labels in the (zeroed) bitmap W, so that
+// k_count_ids can count the distinct output ids (the label sets have gaps after the size
+// filter).
 __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D, BlockStat* S,
                                                 const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
                                                 int packed, const uint32_t* __restrict__ PFg,
-                                                const uint32_t* __restrict__ sb, const uint32_t* __restrict__ soff) {
+                                                const uint32_t* __restrict__ sb, const uint32_t* __restrict__ soff,
+                                                unsigned long long* W) {
     const BlockDesc& B = D[blockIdx.y];
     const bool active = S[blockIdx.y].active;
     const uint32_t* P = PFg + B.ibase;
-    uint64_t* __restrict__ out = B.out;
+    const gwptr_t<uint64_t> out = gblw(B.out);
     uint32_t mx = 0;
+    bool zero_in = false;  // an in-mask voxel without a label: its output is the bare id offset
     ROW_TILES(B.IZ, B.IY, B.IX, {
         const int64_t o = outer_of_inner(B, z, y, x);
-        const bool inm = !B.mask || B.mask[o];
+        const bool inm = !B.mask || gbl(B.mask)[o];
         uint64_t v = 0;  // empty block: constant offset (watershed.py:310-321)
         if (active) {
             uint32_t l;
@@ -280,9 +285,34 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
             v = l;
         }
         out[i] = inm ? v + B.id_offset : v;
+        zero_in |= active && inm && v == 0;
+        if (active && !B.crop) {
+            const uint32_t l = (uint32_t)v;
+            // only the first lane of each run of equal labels along the wave marks it, and it
+            // reads the bit before the atomic: the few words of a block's labels are read by
+            // every wave of the block, so same-address traffic is kept to a few lanes per wave
+            const uint32_t lp = (uint32_t)__shfl_up((int)l, 1);
+            const bool first = l != 0u && ((threadIdx.x & 63) == 0 || lp != l);
+            if (first && !((W[B.wbase + (l >> 6)] >> (l & 63)) & 1ull)) atomicOr(&W[B.wbase + (l >> 6)], 1ull << (l & 63));
+        }
     })
     mx = wg_reduce_u32(mx, OpMax());
     if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);
+    if (__ballot(zero_in) && (threadIdx.x & 63) == 0 && !S[blockIdx.y]._p[0]) atomicOr(&S[blockIdx.y]._p[0], 1u);
+}
+
+// distinct ids of an uncropped block: popcount of its label bitmap (k_output) -> n_cc
+__global__ void __launch_bounds__(256) k_count_ids(const BlockDesc* __restrict__ D, BlockStat* S,
+                                                   const uint64_t* __restrict__ W) {
+    const BlockDesc& B = D[blockIdx.y];
+    BlockStat& st = S[blockIdx.y];
+    if (!st.active || B.crop) return;
+    const int64_t nw = (int64_t)(st.max_label >> 6) + 1;
+    uint32_t c = 0;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x)
+        c += (uint32_t)__popcll(W[B.wbase + w]);
+    c = wg_reduce_u32(c, OpAdd());
+    if (threadIdx.x == 0 && c) atomicAdd(&st.n_cc, c);
 }
 
 // point every element of a union-find forest directly at its root; roots set their scan-key

@@ -292,6 +292,125 @@ template __global__ void k_prep_edt_x_reg<4>(const BlockDesc*, BlockStat*, PrepP
 template __global__ void k_prep_edt_x_reg<8>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
 template __global__ void k_prep_edt_x_reg<16>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
 
+// Coalesced variant (X <= 64 * KMAX): lane l owns the voxels x = 64 k + l of the row, so every
+// load and store of a wave covers 64 consecutive voxels (a row of 576 voxels is 9 fully
+// coalesced 256-B accesses instead of 9 accesses strided by 36 B per lane).  The raw input
+// type is a template parameter and the loads are unconditional (clamped x) global loads, so
+// all KMAX loads of a lane are in flight together.  The foreground bits of each 64-voxel
+// segment k are one ballot, mk[k] (wave-uniform); the nearest foreground to the left / right
+// of x comes from mk[k] masked at the lane plus the last / first foreground of the segments
+// before / after.  3-D datasets only (4-D inputs use k_prep_edt_x).  Same results as
+// k_prep_edt_x.
+template <int KMAX, class T>
+__global__ void __launch_bounds__(256) k_prep_edt_x_co(const BlockDesc* __restrict__ D, BlockStat* S, PrepParams pp,
+                                                       float* __restrict__ fin, uint32_t* __restrict__ g2) {
+    const BlockDesc& B = D[blockIdx.y];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+    if (row >= (int64_t)B.Z * B.Y) return;
+    const int X = B.X;
+    const int K = (X + 63) >> 6;
+    const float mn = unordf(S[blockIdx.y].in_min);
+    const float den = unordf(S[blockIdx.y].in_max) - mn;  // max(x - min) == max - min (monotone rounding)
+    const int64_t rbase = row * X;
+    const gptr_t<T> src = gbl((const T*)B.input) + rbase;
+    const gptr_t<uint8_t> msk = B.mask ? gbl(B.mask) + rbase : nullptr;
+    T raw[KMAX];
+    uint8_t mv[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) raw[k] = src[min(64 * k + lane, X - 1)];
+    if (msk) {
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) mv[k] = msk[min(64 * k + lane, X - 1)];
+    }
+    uint64_t mk[KMAX];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int x = 64 * k + lane;
+        const bool in = k < K && x < X;
+        float a = (float)raw[k] - mn;
+        if (den > 0.0f) a = a / den;
+        if (pp.invert) a = 1.0f - a;
+        if (msk && !mv[k]) a = 1.0f;
+        if (in) fin[B.base + rbase + x] = a;
+        mk[k] = __ballot(in && a > pp.threshold);
+        any |= mk[k] != 0ull;
+    }
+    // any foreground in the block? (_apply_dt: np.sum(threshd) == 0 -> None)
+    if (any && lane == 0 && !*(volatile uint32_t*)&S[blockIdx.y].fg) atomicOr(&S[blockIdx.y].fg, 1u);
+    // last foreground at or before each segment, first at or after
+    int lastk[KMAX], firstk[KMAX];
+    {
+        int l = -1;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            if (mk[k]) l = 64 * k + 63 - __builtin_clzll(mk[k]);
+            lastk[k] = l;
+        }
+        int f = 0x3FFFFFFF;
+#pragma unroll
+        for (int k = KMAX - 1; k >= 0; --k) {
+            if (mk[k]) f = 64 * k + __builtin_ctzll(mk[k]);
+            firstk[k] = f;
+        }
+    }
+    const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);  // bits <= lane
+    const uint64_t ge = ~0ull << lane;                                    // bits >= lane
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int x = 64 * k + lane;
+        const uint64_t ml = mk[k] & le, mr = mk[k] & ge;
+        const int left = ml ? 64 * k + 63 - __builtin_clzll(ml) : (k > 0 ? lastk[k - 1] : -1);
+        const int right = mr ? 64 * k + __builtin_ctzll(mr) : (k + 1 < KMAX ? firstk[k + 1] : 0x3FFFFFFF);
+        const int dl = left < 0 ? 0x3FFFFFFF : x - left;
+        const int dr = right >= 0x3FFFFFFF ? 0x3FFFFFFF : right - x;
+        const int d = min(dl, dr);
+        if (k < K && x < X) g2[B.base + rbase + x] = (d >= 0x3FFFFFFF) ? kInfD2 : (uint32_t)(pp.px2 * d * d);
+    }
+}
+#define CTWS_PREP_CO(K)                                                                                \
+    template __global__ void k_prep_edt_x_co<K, uint8_t>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);  \
+    template __global__ void k_prep_edt_x_co<K, uint16_t>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*); \
+    template __global__ void k_prep_edt_x_co<K, float>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);    \
+    template __global__ void k_prep_edt_x_co<K, double>(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
+CTWS_PREP_CO(4)
+CTWS_PREP_CO(8)
+CTWS_PREP_CO(16)
+#undef CTWS_PREP_CO
+
+// per-block min / max of a 3-D input of type T: 8 global loads in flight per thread
+template <class T>
+__global__ void __launch_bounds__(256) k_input_minmax_t(const BlockDesc* __restrict__ D, BlockStat* S) {
+    const BlockDesc& B = D[blockIdx.y];
+    const gptr_t<T> src = gbl((const T*)B.input);
+    const int64_t n = B.N;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    constexpr int U = 8;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * U) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[min(i0 + u * stride, n - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t o = ordf((float)v[u]);
+            mn = min(mn, o);
+            mx = max(mx, o);
+        }
+    }
+    mn = wg_reduce_u32(mn, OpMin());
+    mx = wg_reduce_u32(mx, OpMax());
+    if (threadIdx.x == 0) {
+        atomic_min_if(&S[blockIdx.y].in_min, mn);
+        atomic_max_if(&S[blockIdx.y].in_max, mx);
+    }
+}
+template __global__ void k_input_minmax_t<uint8_t>(const BlockDesc*, BlockStat*);
+template __global__ void k_input_minmax_t<uint16_t>(const BlockDesc*, BlockStat*);
+template __global__ void k_input_minmax_t<float>(const BlockDesc*, BlockStat*);
+template __global__ void k_input_minmax_t<double>(const BlockDesc*, BlockStat*);
+
 // Correctly rounded sqrtf of an integer n < 2^24 (vigra: sqrt on the float32 dest).  The
 // hardware v_sqrt_f32 is not correctly rounded, so round a double sqrt to float and fix it
 // with exact arithmetic: the float r is correct iff mid(r-,r)^2 < n < mid(r,r+)^2 (midpoints

@@ -220,17 +220,7 @@ namespace ctws {
 // then all threads switch to lines along the next axis.  LDS words are 64-bit and written
 // whole, so concurrent readers never see a torn key.
 // =========================================================================================
-constexpr uint64_t kPackInf = ~0ull;
-constexpr uint32_t kLabelBits = 20;
-constexpr uint64_t kLabelMask = (1ull << kLabelBits) - 1ull;
-constexpr uint64_t kDOne = 1ull << kLabelBits;
-constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
-
-__device__ __forceinline__ uint64_t f_packed(uint32_t hb, uint64_t best) {
-    const uint32_t c = (uint32_t)(best >> 32);
-    if (hb > c) return ((uint64_t)hb << 32) | (best & kLabelMask);
-    return ((best & kDMask) == kDMask) ? best : best + kDOne;
-}
+// packed key helpers (kPackInf, f_packed): ctws_dev.h
 
 template <int ND>
 struct PTile;
@@ -553,9 +543,6 @@ namespace ctws {
 // One pass over the volume instead of a global pointer-jumping pass per doubling.
 // seed test / seed label: from the seed CC parents (pass 1: `cc` = PF after k_root_label) or,
 // when cc is null, from lab (kFixedBit; pass 2 and the fallbacks)
-__device__ __forceinline__ bool is_seed(const uint32_t* lab, const uint32_t* cc, int64_t gi) {
-    return cc ? cc[gi] != kNoParent : (lab[gi] & kFixedBit) != 0;
-}
 __device__ __forceinline__ uint32_t seed_label(const uint32_t* lab, const uint32_t* cc, int64_t base, uint32_t r) {
     if (cc) return cc_label(cc + base, cc[base + r]);
     const uint32_t l = lab[base + r];
@@ -734,49 +721,30 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
                                                       uint32_t* __restrict__ nopen) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const int64_t nrows = (int64_t)B.Z * B.Y;
-    const int wpr = (B.X + 63) >> 6;
     uint32_t cnt_open = 0;  // statistics (CTWS_TRACE): voxels left to the relaxation
-    for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
-        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
-            // the kRows chains advance together, so their loads overlap
-            uint32_t e[kRows];
-            float hv[kRows];
-#pragma unroll
-            for (int rr = 0; rr < kRows; ++rr) {
-                const int64_t gi = B.base + (r0 + rr) * B.X + x;
-                const bool ok = r0 + rr < nrows;
-                e[rr] = ok ? par[gi] : kDescRes;
-                hv[rr] = ok ? h[gi] : 0.0f;
-            }
-            for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
-                bool more = false;
-#pragma unroll
-                for (int rr = 0; rr < kRows; ++rr)
-                    if (!(e[rr] & kDescRes)) {
-                        e[rr] = par[B.base + e[rr]];
-                        more = true;
-                    }
-                if (!more) break;
-            }
-#pragma unroll
-            for (int rr = 0; rr < kRows; ++rr) {
-                const int64_t row = r0 + rr;
-                if (row >= nrows) break;
-                const int64_t gi = B.base + row * B.X + x;
-                const uint32_t lr = e[rr] & ~kDescRes;
-                const bool res = lr != 0;
-                key[gi] = res ? (((uint64_t)ordf(hv[rr]) << 32) | (uint64_t)lr) : kPackInf;
-                fixedv[gi] = res ? 1 : 0;
-                const uint64_t op = __ballot(!res);
-                const uint64_t fi = __ballot(res);
-                if ((threadIdx.x & 63) == 0) {
-                    open[B.fbase + row * wpr + (x >> 6)] = op;
-                    chg[B.fbase + row * wpr + (x >> 6)] = fi;
-                    cnt_open += (uint32_t)__popcll(op);
-                }
-            }
+    // word tiles: a wave's ballot is exactly one word of the open / changed bitmaps
+    WORD_TILES(B.Z, B.Y, B.X, {
+        const int64_t gi = B.base + i;
+        uint32_t e = valid ? par[gi] : kDescRes;
+        const float hv = valid ? h[gi] : 0.0f;
+        for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
+            if (e & kDescRes) break;
+            e = par[B.base + e];
         }
+        const uint32_t lr = e & ~kDescRes;
+        const bool res = lr != 0;
+        if (valid) {
+            key[gi] = res ? (((uint64_t)ordf(hv) << 32) | (uint64_t)lr) : kPackInf;
+            fixedv[gi] = res ? 1 : 0;
+        }
+        const uint64_t op = __ballot(valid && !res);
+        const uint64_t fi = __ballot(valid && res);
+        if (lane == 0) {
+            open[B.fbase + w_] = op;
+            chg[B.fbase + w_] = fi;
+        }
+        cnt_open += lane == 0 ? (uint32_t)__popcll(op) : 0u;
+    })
     if (nopen) {
         cnt_open = wg_reduce_u32(cnt_open, OpAdd());
         if (threadIdx.x == 0 && cnt_open) atomicAdd(&nopen[blockIdx.y], cnt_open);
@@ -785,13 +753,18 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
 
 // One iteration of the frontier relaxation.  frontier = (neighbours of the voxels changed in
 // the previous iteration) & open; every frontier voxel recomputes K = f(min of its
-// neighbours' keys) in place (monotone: keys only decrease, so a neighbour updated in the same
-// launch is fine; a stale read is repaired by the next iteration, as the neighbour's change
-// is recorded).  A wave owns 64 consecutive words: it builds their frontier from the previous
-// changed bitmap, expands the set bits into an LDS list and relaxes 64 voxels per step, one
-// per lane; its changed bits collect in LDS and are stored whole (no memset, no global
-// atomics).
+// neighbours' keys) in place (a stale read is repaired by the next iteration, as the
+// neighbour's change is recorded).  Work is a list of 64-word chunks (one wave per entry):
+// the chunks that contain open voxels in iteration 0, afterwards the chunks next to a chunk
+// that changed in the previous iteration — so a late iteration with a handful of active
+// chunks costs a handful of waves, not a pass over every chunk of the batch.  A wave builds
+// its chunk's frontier from the previous changed bitmap, expands the set bits into an LDS
+// list and relaxes 64 voxels per step, one per lane; its changed bits collect in LDS and are
+// stored whole.  Chunk generations instead of cleared flags: gen[it & 1][ch] = it + 1 when
+// chunk ch changed in iteration it, so a word of the previous changed bitmap is valid iff
+// gen[(it + 1) & 1][ch] == it; qgen[ch] = it + 1 when ch is queued for iteration it + 1.
 constexpr int kFrontierWaves = 4;
+constexpr uint32_t kWlChunkBits = 20;  // list entry = block << 20 | chunk
 
 // position of the k-th (0-based) set bit of w (k < popcount(w))
 __device__ __forceinline__ int kth_set_bit(uint64_t w, int k) {
@@ -811,52 +784,72 @@ __device__ __forceinline__ int kth_set_bit(uint64_t w, int k) {
     return pos;
 }
 
+// iteration-0 list: every chunk holding an open voxel.  A wave takes 64 consecutive chunks,
+// reads each one's 64 words coalesced (one word per lane) and appends the non-empty ones with
+// one atomic.
+__global__ void __launch_bounds__(256) k_frontier_list0(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                        const uint64_t* __restrict__ open, uint32_t* __restrict__ list,
+                                                        uint32_t* __restrict__ cnt) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwords = (int64_t)B.Z * B.Y * ((B.X + 63) >> 6);
+    const int64_t nch = (nwords + 63) >> 6;
+    const uint64_t* op = open + B.fbase;
+    for (int64_t c0 = ((int64_t)blockIdx.x * kFrontierWaves + (threadIdx.x >> 6)) * 64; c0 < nch;
+         c0 += (int64_t)gridDim.x * kFrontierWaves * 64) {
+        uint64_t m = 0ull;  // bit k: chunk c0 + k holds an open voxel
+        for (int k = 0; k < 64 && c0 + k < nch; ++k) {
+            const int64_t wi = (c0 + k) * 64 + lane;
+            const bool any = __ballot(wi < nwords && op[wi] != 0ull) != 0ull;
+            m |= (any ? 1ull : 0ull) << k;
+        }
+        if (!m) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, 0);
+        if ((m >> lane) & 1ull)
+            list[base + __popcll(m & ((1ull << lane) - 1ull))] = (blockIdx.y << kWlChunkBits) | (uint32_t)(c0 + lane);
+    }
+}
+
 template <int ND, int kFrontierUnroll>
 __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                   const float* __restrict__ h, uint64_t* __restrict__ key,
                                                   const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
-                                                  uint64_t* __restrict__ cnext, const uint32_t* __restrict__ fprev,
-                                                  uint32_t* __restrict__ fnext, uint32_t* __restrict__ flag,
+                                                  uint64_t* __restrict__ cnext, const uint32_t* __restrict__ gprev,
+                                                  uint32_t* __restrict__ gnext, int it, const uint32_t* __restrict__ list,
+                                                  const uint32_t* __restrict__ cnt, uint32_t* __restrict__ list_next,
+                                                  uint32_t* __restrict__ cnt_next, uint32_t* __restrict__ qgen,
                                                   uint32_t* __restrict__ nvisit, int reps) {
     __shared__ uint64_t schg[kFrontierWaves][64];
     __shared__ uint64_t sfw[kFrontierWaves][64];
     __shared__ int spre[kFrontierWaves][64];
     __shared__ int srow[kFrontierWaves][64];
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int wpr = (B.X + 63) >> 6;
-    const int64_t ws = (int64_t)B.Y * wpr;
-    const int64_t nwords = (int64_t)B.Z * ws;
-    const int64_t YX = (int64_t)B.Y * B.X;
-    const uint64_t* cp = cprev + B.fbase;
-    const uint64_t* op = open + B.fbase;
-    uint64_t* cn = cnext + B.fbase;
-    uint64_t* kb = key + B.base;
-    const float* hb = h + B.base;
-    const uint32_t* fp = fprev + (B.fbase >> 6);
-    uint32_t* fnx = fnext + (B.fbase >> 6);
-    const int64_t nchunks = (nwords + 63) >> 6;
-    // word w of the previous changed bitmap (0 when its chunk was quiet)
-    auto cw = [&](int64_t w) -> uint64_t { return fp[w >> 6] ? cp[w] : 0ull; };
-    bool any = false;
-    for (int64_t w0 = ((int64_t)blockIdx.x * kFrontierWaves + wv) * 64; w0 < nwords;
-         w0 += (int64_t)gridDim.x * kFrontierWaves * 64) {
-        const int64_t ch0 = w0 >> 6;
-        {
-            // quiet neighbourhood: nothing to do in this chunk
-            uint32_t q = fp[ch0];
-            if (ch0 > 0) q |= fp[ch0 - 1];
-            if (ch0 + 1 < nchunks) q |= fp[ch0 + 1];
-            if (ND == 3) {
-                if (w0 - ws >= 0) q |= fp[(w0 - ws) >> 6] | fp[(w0 - ws + 63) >> 6];
-                if (w0 + ws < nwords) q |= fp[(w0 + ws) >> 6] | fp[min(nwords - 1, w0 + ws + 63) >> 6];
-            }
-            if (!q) {
-                if (lane == 0) fnx[ch0] = 0u;
-                continue;
-            }
-        }
+    const uint32_t n_entries = *cnt;
+    const uint32_t prev_gen = (uint32_t)it;  // gprev[ch] == it: changed in iteration it - 1
+    for (uint32_t e0 = blockIdx.x * kFrontierWaves + wv; e0 < n_entries; e0 += gridDim.x * kFrontierWaves) {
+        const uint32_t ent = list[e0];
+        const int bi = (int)(ent >> kWlChunkBits);
+        const int64_t ch0 = ent & ((1u << kWlChunkBits) - 1u);
+        const BlockDesc& B = D[bi];
+        const int wpr = (B.X + 63) >> 6;
+        const int64_t ws = (int64_t)B.Y * wpr;
+        const int64_t nwords = (int64_t)B.Z * ws;
+        const int64_t YX = (int64_t)B.Y * B.X;
+        const uint64_t* cp = cprev + B.fbase;
+        const uint64_t* op = open + B.fbase;
+        uint64_t* cn = cnext + B.fbase;
+        uint64_t* kb = key + B.base;
+        const float* hb = h + B.base;
+        const uint32_t* gp = gprev + (B.fbase >> 6);
+        uint32_t* gn = gnext + (B.fbase >> 6);
+        uint32_t* qg = qgen + (B.fbase >> 6);
+        const int64_t nchunks = (nwords + 63) >> 6;
+        // word w of the previous changed bitmap (0 unless its chunk changed in iteration it - 1)
+        auto cw = [&](int64_t w) -> uint64_t { return gp[w >> 6] == prev_gen ? cp[w] : 0ull; };
+        const int64_t w0 = ch0 * 64;
         const int64_t wl = w0 + lane;
         uint64_t f = 0ull;
         int row = 0, xw = 0;
@@ -880,126 +873,133 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
         const int z0 = row / B.Y, y0 = row - z0 * B.Y;
         uint64_t acc = 0ull;  // changed bits of this word over all local sweeps
         for (int rep = 0;; ++rep) {
-        // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list is
-        // bit (e - pre[j]) of word j, the last j with pre[j] <= e
-        const int cnt = __popcll(f);
-        int incl = cnt;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
-        }
-        const int total = __shfl(incl, 63);
-        if (total == 0) break;
-        if (nvisit && lane == 0) atomicAdd(&nvisit[blockIdx.y], (uint32_t)total);
-        schg[wv][lane] = 0ull;
-        sfw[wv][lane] = f;
-        spre[wv][lane] = incl - cnt;
-        srow[wv][lane] = row * 64 + xw;  // row < 2^25 (Z * Y <= 2^22)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (int t0 = 0; t0 < total; t0 += 64 * kFrontierUnroll) {
-            int64_t vi[kFrontierUnroll];
-            int vj[kFrontierUnroll], vb[kFrontierUnroll];
-            uint64_t nb[kFrontierUnroll][6];
-            uint64_t own[kFrontierUnroll];
-            float hv[kFrontierUnroll];
+            // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list
+            // is bit (e - pre[j]) of word j, the last j with pre[j] <= e
+            const int cnt_bits = __popcll(f);
+            int incl = cnt_bits;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            const int total = __shfl(incl, 63);
+            if (total == 0) break;
+            if (nvisit && lane == 0) atomicAdd(&nvisit[bi], (uint32_t)total);
+            schg[wv][lane] = 0ull;
+            sfw[wv][lane] = f;
+            spre[wv][lane] = incl - cnt_bits;
+            srow[wv][lane] = row * 64 + xw;  // row < 2^25 (Z * Y <= 2^22)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            for (int t0 = 0; t0 < total; t0 += 64 * kFrontierUnroll) {
+                int64_t vi[kFrontierUnroll];
+                int vj[kFrontierUnroll], vb[kFrontierUnroll];
+                uint64_t nb[kFrontierUnroll][6];
+                uint64_t own[kFrontierUnroll];
+                float hv[kFrontierUnroll];
 #pragma unroll
-            for (int u = 0; u < kFrontierUnroll; ++u) {
-                const int e = t0 + u * 64 + lane;
-                vi[u] = -1;
-                vj[u] = 0;
-                vb[u] = 0;
+                for (int u = 0; u < kFrontierUnroll; ++u) {
+                    const int e = t0 + u * 64 + lane;
+                    vi[u] = -1;
+                    vj[u] = 0;
+                    vb[u] = 0;
 #pragma unroll
-                for (int k = 0; k < 6; ++k) nb[u][k] = kPackInf;
-                own[u] = kPackInf;
-                hv[u] = 0.0f;
-                if (e < total) {
-                    int j = 0;
+                    for (int k = 0; k < 6; ++k) nb[u][k] = kPackInf;
+                    own[u] = kPackInf;
+                    hv[u] = 0.0f;
+                    if (e < total) {
+                        int j = 0;
 #pragma unroll
-                    for (int step = 32; step > 0; step >>= 1)
-                        if (spre[wv][j + step] <= e) j += step;
-                    const int b = kth_set_bit(sfw[wv][j], e - spre[wv][j]);
-                    const int rx = srow[wv][j];
-                    const int r = rx >> 6, xq = rx & 63;
-                    const int z = r / B.Y, y = r - z * B.Y;
-                    const int x = xq * 64 + b;
-                    const int64_t i = (int64_t)r * B.X + x;
-                    vi[u] = i;
-                    vj[u] = j;
-                    vb[u] = b;
-                    if (ND == 3) {
-                        if (z > 0) nb[u][0] = kb[i - YX];
-                        if (z + 1 < B.Z) nb[u][1] = kb[i + YX];
+                        for (int step = 32; step > 0; step >>= 1)
+                            if (spre[wv][j + step] <= e) j += step;
+                        const int b = kth_set_bit(sfw[wv][j], e - spre[wv][j]);
+                        const int rx = srow[wv][j];
+                        const int r = rx >> 6, xq = rx & 63;
+                        const int z = r / B.Y, y = r - z * B.Y;
+                        const int x = xq * 64 + b;
+                        const int64_t i = (int64_t)r * B.X + x;
+                        vi[u] = i;
+                        vj[u] = j;
+                        vb[u] = b;
+                        if (ND == 3) {
+                            if (z > 0) nb[u][0] = kb[i - YX];
+                            if (z + 1 < B.Z) nb[u][1] = kb[i + YX];
+                        }
+                        if (y > 0) nb[u][2] = kb[i - B.X];
+                        if (y + 1 < B.Y) nb[u][3] = kb[i + B.X];
+                        if (x > 0) nb[u][4] = kb[i - 1];
+                        if (x + 1 < B.X) nb[u][5] = kb[i + 1];
+                        own[u] = kb[i];
+                        hv[u] = hb[i];
                     }
-                    if (y > 0) nb[u][2] = kb[i - B.X];
-                    if (y + 1 < B.Y) nb[u][3] = kb[i + B.X];
-                    if (x > 0) nb[u][4] = kb[i - 1];
-                    if (x + 1 < B.X) nb[u][5] = kb[i + 1];
-                    own[u] = kb[i];
-                    hv[u] = hb[i];
                 }
-            }
 #pragma unroll
-            for (int u = 0; u < kFrontierUnroll; ++u) {
-                if (vi[u] < 0) continue;
-                uint64_t m = min(min(min(nb[u][0], nb[u][1]), min(nb[u][2], nb[u][3])), min(nb[u][4], nb[u][5]));
-                if (m == kPackInf) continue;
-                const uint64_t k = f_packed(ordf(hv[u]), m);
-                if (k != own[u]) {
-                    kb[vi[u]] = k;
-                    atomicOr((unsigned long long*)&schg[wv][vj[u]], 1ull << vb[u]);
+                for (int u = 0; u < kFrontierUnroll; ++u) {
+                    if (vi[u] < 0) continue;
+                    uint64_t m = min(min(min(nb[u][0], nb[u][1]), min(nb[u][2], nb[u][3])), min(nb[u][4], nb[u][5]));
+                    if (m == kPackInf) continue;
+                    const uint64_t k = f_packed(ordf(hv[u]), m);
+                    if (k != own[u]) {
+                        kb[vi[u]] = k;
+                        atomicOr((unsigned long long*)&schg[wv][vj[u]], 1ull << vb[u]);
+                    }
                 }
             }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t c = schg[wv][lane];
+            acc |= c;
+            if (__ballot(c != 0ull) == 0ull || rep + 1 >= reps) break;
+            // local sweep: the neighbours of this sweep's changes that lie in the same chunk
+            // (x within the row's words, y within the chunk's rows); changes are also in acc, so
+            // the neighbours outside the chunk see them in the next launch
+            f = (c << 1) | (c >> 1);
+            const uint64_t cxm = __shfl(c, (lane + 63) & 63), cxp = __shfl(c, (lane + 1) & 63);
+            if (xw > 0 && lane > 0) f |= cxm >> 63;
+            if (xw + 1 < wpr && lane < 63) f |= cxp << 63;
+            const uint64_t cym = __shfl(c, lane >= wpr ? lane - wpr : lane);
+            const uint64_t cyp = __shfl(c, lane + wpr < 64 ? lane + wpr : lane);
+            if (y0 > 0 && lane >= wpr) f |= cym;
+            if (y0 + 1 < B.Y && lane + wpr < 64) f |= cyp;
+            f &= opw;
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        const uint64_t c = schg[wv][lane];
-        acc |= c;
-        if (__ballot(c != 0ull) == 0ull || rep + 1 >= reps) break;
-        // local sweep: the neighbours of this sweep's changes that lie in the same chunk
-        // (x within the row's words, y within the chunk's rows); changes are also in acc, so
-        // the neighbours outside the chunk see them in the next launch
-        f = (c << 1) | (c >> 1);
-        const uint64_t cxm = __shfl(c, (lane + 63) & 63), cxp = __shfl(c, (lane + 1) & 63);
-        if (xw > 0 && lane > 0) f |= cxm >> 63;
-        if (xw + 1 < wpr && lane < 63) f |= cxp << 63;
-        const uint64_t cym = __shfl(c, lane >= wpr ? lane - wpr : lane);
-        const uint64_t cyp = __shfl(c, lane + wpr < 64 ? lane + wpr : lane);
-        if (y0 > 0 && lane >= wpr) f |= cym;
-        if (y0 + 1 < B.Y && lane + wpr < 64) f |= cyp;
-        f &= opw;
-        }
-        const bool chunk_changed = __ballot(acc != 0ull) != 0ull;
-        if (chunk_changed && wl < nwords) cn[wl] = acc;
-        if (lane == 0) fnx[ch0] = chunk_changed ? 1u : 0u;
-        any |= chunk_changed;
+        if (__ballot(acc != 0ull) == 0ull) continue;
+        // the chunk changed: publish its changed words and queue the chunks whose frontier can
+        // hold a neighbour of a changed voxel (x / y: the adjacent chunks; 3-D z: the chunks
+        // of the words +- one slice)
+        if (wl < nwords) cn[wl] = acc;
+        if (lane == 0) gn[ch0] = (uint32_t)it + 1u;
+        int64_t cand = -1;
+        if (lane == 0) cand = ch0;
+        else if (lane == 1 && ch0 > 0) cand = ch0 - 1;
+        else if (lane == 2 && ch0 + 1 < nchunks) cand = ch0 + 1;
+        // (a chunk straddling a slice boundary reaches the previous / next slice with part of
+        // its words only: the word range is clamped, not dropped)
+        else if (ND == 3 && lane == 3 && w0 + 63 - ws >= 0) cand = max((int64_t)0, w0 - ws) >> 6;
+        else if (ND == 3 && lane == 4 && w0 + 63 - ws >= 0) cand = min(nwords - 1, w0 + 63 - ws) >> 6;
+        else if (ND == 3 && lane == 5 && w0 + ws < nwords) cand = (w0 + ws) >> 6;
+        else if (ND == 3 && lane == 6 && w0 + ws < nwords) cand = min(nwords - 1, w0 + 63 + ws) >> 6;
+        bool push = false;
+        if (cand >= 0) push = atomicMax(&qg[cand], (uint32_t)it + 1u) < (uint32_t)it + 1u;
+        const uint64_t pm = __ballot(push);
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(cnt_next, (uint32_t)__popcll(pm));
+        base = (uint32_t)__shfl((int)base, 0);
+        if (push)
+            list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
     }
-    if (__ballot(any) && lane == 0 && !*(volatile uint32_t*)flag) atomicOr(flag, 1u);
 }
-template __global__ void k_frontier<3, 1>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
-                                          uint32_t*, uint32_t*, int);
-template __global__ void k_frontier<2, 1>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
-                                          uint32_t*, uint32_t*, int);
-template __global__ void k_frontier<3, 2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
-                                          uint32_t*, uint32_t*, int);
-template __global__ void k_frontier<3, 4>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
-                                          uint32_t*, uint32_t*, int);
-template __global__ void k_frontier<3, 8>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
-                                          uint32_t*, uint32_t*, int);
-template __global__ void k_frontier<2, 2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
-                                          uint32_t*, uint32_t*, int);
-template __global__ void k_frontier<2, 4>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
-                                          uint32_t*, uint32_t*, int);
-template __global__ void k_frontier<2, 8>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                          const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*, uint32_t*,
-                                          uint32_t*, uint32_t*, int);
+#define CTWS_FRONTIER_INST(ND, U)                                                                                 \
+    template __global__ void k_frontier<ND, U>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,        \
+                                               const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,        \
+                                               uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, \
+                                               uint32_t*, uint32_t*, int);
+CTWS_FRONTIER_INST(3, 1)
+CTWS_FRONTIER_INST(2, 1)
+CTWS_FRONTIER_INST(3, 2)
+CTWS_FRONTIER_INST(2, 2)
+CTWS_FRONTIER_INST(3, 4)
+CTWS_FRONTIER_INST(2, 4)
+#undef CTWS_FRONTIER_INST
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
@@ -1025,7 +1025,10 @@ __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restr
     }
 }
 
-// fixpoint check of the packed flood: K(q) == f(min_p K(p)) for every non-seed voxel
+// fixpoint check of the packed flood: K(q) == f(min_p K(p)) for every non-seed voxel.  Word
+// tiles: a wave reads a 64-voxel row word coalesced; x-neighbours come from the neighbouring
+// lanes, the rows above / below (and the slices) are loads that the neighbouring waves'
+// own reads keep in cache.
 template <int ND>
 __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint64_t* __restrict__ key,
@@ -1035,34 +1038,42 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
     if (!S[blockIdx.y].active) return;
     const uint64_t* k = key + B.base;
     const int64_t YX = (int64_t)B.Y * B.X;
-    const int64_t nrows = (int64_t)B.Z * B.Y;
+    const uint32_t* seedsrc = cc ? cc : lab;  // seed: cc != kNoParent, or lab has kFixedBit
     bool bad = false;
-    for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
-        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
-#pragma unroll
-            for (int rr = 0; rr < kRows; ++rr) {
-                const int64_t row = r0 + rr;
-                if (row >= nrows) break;
-                const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
-                const int64_t i = row * B.X + x;
-                uint64_t m = kPackInf;
-                if (ND == 3) {
-                    if (z > 0) m = min(m, k[i - YX]);
-                    if (z + 1 < B.Z) m = min(m, k[i + YX]);
-                }
-                if (y > 0) m = min(m, k[i - B.X]);
-                if (y + 1 < B.Y) m = min(m, k[i + B.X]);
-                if (x > 0) m = min(m, k[i - 1]);
-                if (x + 1 < B.X) m = min(m, k[i + 1]);
-                const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(h[B.base + i]), m);
-                const bool b1 = !is_seed(lab, cc, B.base + i) && e != k[i];
-                if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
-                    const uint32_t slot = atomicAdd(&flag[1], 1u);
-                    if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + i);
-                }
-                bad |= b1;
-            }
+    WORD_TILES(B.Z, B.Y, B.X, {
+        // every load unconditional (clamped index) so that they are all in flight together
+        const int64_t ic = valid ? i : row * B.X;
+        const uint64_t own0 = k[ic];
+        const uint64_t kym = k[y > 0 ? ic - B.X : ic], kyp = k[y + 1 < B.Y ? ic + B.X : ic];
+        uint64_t kzm = kPackInf, kzp = kPackInf;
+        if (ND == 3) {
+            kzm = k[z > 0 ? ic - YX : ic];
+            kzp = k[z + 1 < B.Z ? ic + YX : ic];
         }
+        const uint64_t kxm = k[x > 0 && valid ? ic - 1 : ic], kxp = k[x + 1 < B.X ? ic + 1 : ic];
+        const float hv = h[B.base + ic];
+        const uint32_t sv = seedsrc[B.base + ic];
+        const uint64_t own = valid ? own0 : kPackInf;
+        uint64_t l = shfl_up_u64(own, 1), r = shfl_down_u64(own, 1);
+        if (lane == 0) l = (x > 0) ? kxm : kPackInf;
+        if (lane == 63) r = (x + 1 < B.X) ? kxp : kPackInf;
+        if (x + 1 >= B.X) r = kPackInf;
+        uint64_t m = min(l, r);
+        if (y > 0) m = min(m, kym);
+        if (y + 1 < B.Y) m = min(m, kyp);
+        if (ND == 3) {
+            if (z > 0) m = min(m, kzm);
+            if (z + 1 < B.Z) m = min(m, kzp);
+        }
+        const bool seed = cc ? sv != kNoParent : (sv & kFixedBit) != 0;
+        const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(hv), m);
+        const bool b1 = valid && !seed && e != own;
+        if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
+            const uint32_t slot = atomicAdd(&flag[1], 1u);
+            if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + i);
+        }
+        bad |= b1;
+    })
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 template __global__ void k_flood_verify<3>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,

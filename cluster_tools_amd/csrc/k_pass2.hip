@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(256) k_p2_zero_dt(const BlockDesc* __restrict_
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     BLOCK_LOOP(i, B) {
-        if (B.init[i] != 0) dt[B.base + i] = 0.0f;
+        if (gbl(B.init)[i] != 0) dt[B.base + i] = 0.0f;
     }
 }
 
@@ -90,13 +90,13 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
     BLOCK_LOOP(i, B) {
         int z, y, x;
         inner_to_zyx(i, YX, B.X, z, y, x);
-        const uint64_t u = B.init[i];
+        const uint64_t u = gbl(B.init)[i];
         uint64_t k = kEmptyKey;
         if (u != 0) {
             // (uint32)u == 0: the setitem truncation makes the voxel background
             if ((uint32_t)u != 0)
                 k = (B.nd_ws == 3) ? (uint64_t)(uint32_t)u : (((uint64_t)z << 33) | kInitTag | (uint32_t)u);
-        } else if (!B.mask || B.mask[i]) {
+        } else if (!B.mask || gbl(B.mask)[i]) {
             const uint32_t gl = cc_label(PF, PF[i]);  // seed label (0: background)
             if (gl) {
                 if (B.nd_ws == 3) {
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(256) k_p2_excl(const BlockDesc* __restrict__ D
     const int64_t YX = (int64_t)B.Y * B.X;
     const uint32_t nl = S[blockIdx.y].n_seeds;
     BLOCK_LOOP(i, B) {
-        const uint64_t u = B.init[i];
+        const uint64_t u = gbl(B.init)[i];
         if (u == 0) continue;
         if (B.nd_ws == 3) {
             if (u <= nl) excl[B.base + u] = 1;
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(256) k_p2_check(const BlockDesc* __restrict__ 
     if (!S[blockIdx.y].active || B.nd_ws != 2) return;
     const int64_t YX = (int64_t)B.Y * B.X;
     BLOCK_LOOP(i, B) {
-        const uint64_t u = B.init[i];
+        const uint64_t u = gbl(B.init)[i];
         const int z = (int)(i / YX);
         if (i == (int64_t)z * YX) {
             // a shifted new seed that wraps to 0 would have become background
@@ -264,12 +264,12 @@ __global__ void __launch_bounds__(256) k_p2_output(const BlockDesc* __restrict__
         const int64_t o = ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0);
         const uint32_t l = lab[B.base + o] & ~kFixedBit;
         uint32_t v = 0;
-        if (l && (!B.mask || B.mask[o])) {
+        if (l && (!B.mask || gbl(B.mask)[o])) {
             v = oldv[B.base + l];
             if (B.nd_ws == 2 && !oldt[B.base + l]) v = v + (uint32_t)B.id_offset + soff[B.sbase + z + B.iz0];
         }
         mx = max(mx, v);
-        B.out[i] = v;
+        gblw(B.out)[i] = v;
     }
     mx = wg_reduce_u32(mx, OpMax());
     if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);
@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(256) k_slice_inmask(const BlockDesc* __restric
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
     BLOCK_LOOP(i, B) {
-        if (B.mask && !B.mask[i]) continue;
+        if (B.mask && !gbl(B.mask)[i]) continue;
         uint32_t* f = flag + B.sbase + (B.nd_ws == 2 ? (int)(i / YX) : 0);
         if (!*f) *f = 1;
     }

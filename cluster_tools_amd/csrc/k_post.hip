@@ -43,9 +43,10 @@ __global__ void __launch_bounds__(256) k_hist_zero(const BlockDesc* __restrict__
 // LDS, sized by the host to the batch's largest seed count so that a few thousand labels do
 // not cap the occupancy) and flushes its non-zero bins with one global atomic each; a block
 // with more labels than bins counts with global atomics.
+template <int PACKED>
 __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, const BlockStat* S,
                                               const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
-                                              int packed, uint32_t* __restrict__ counts, int bins) {
+                                              uint32_t* __restrict__ counts, int bins) {
     extern __shared__ uint32_t sh[];
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
@@ -64,7 +65,18 @@ __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, c
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t i = ib + u * 256 + threadIdx.x;
-            lv[u] = i < i1 ? flood_label(lab, key, packed, B.base + i) : 0xFFFFFFFFu;
+            const int64_t ic = B.base + min(i, i1 - 1);  // unconditional loads: all in flight
+            if (PACKED) {
+                const uint64_t kv = key[ic];
+                lv[u] = (uint32_t)(kv & ((1ull << 20) - 1ull)) | (kv == kInfKey ? 0x80000000u : 0u);
+            } else {
+                lv[u] = lab[ic] & ~kFixedBit;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = ib + u * 256 + threadIdx.x;
+            lv[u] = i >= i1 ? 0xFFFFFFFFu : ((lv[u] & 0x80000000u) ? 0u : lv[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -95,10 +107,11 @@ __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, c
 // slice-major), so each workgroup counts a quarter of one slice into a small LDS histogram of
 // that range — no contention on a block-wide table of tens of thousands of labels.
 constexpr int kHist2dBins = 8192;
+template <int PACKED>
 __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                 const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
-                                                int packed, const uint32_t* __restrict__ sb,
-                                                uint32_t* __restrict__ counts, int splits) {
+                                                const uint32_t* __restrict__ sb, uint32_t* __restrict__ counts,
+                                                int splits) {
     __shared__ uint32_t sh[kHist2dBins];
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
@@ -121,7 +134,18 @@ __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t i = ib + u * 256 + threadIdx.x;
-            lv[u] = i < i1 ? flood_label(lab, key, packed, B.base + i) : 0u;
+            const int64_t ic = B.base + min(i, i1 - 1);  // unconditional loads: all in flight
+            if (PACKED) {
+                const uint64_t kv = key[ic];
+                lv[u] = (uint32_t)(kv & ((1ull << 20) - 1ull)) | (kv == kInfKey ? 0x80000000u : 0u);
+            } else {
+                lv[u] = lab[ic] & ~kFixedBit;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = ib + u * 256 + threadIdx.x;
+            lv[u] = (i < i1 && !(lv[u] & 0x80000000u)) ? lv[u] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -161,48 +185,43 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
                                                      uint32_t* __restrict__ survivors) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const int64_t nrows = (int64_t)B.Z * B.Y;
-    const int wpr = (B.X + 63) >> 6;
     constexpr uint64_t kLab = (1ull << 20) - 1ull;
-    for (int64_t r0 = (int64_t)blockIdx.x * kRows; r0 < nrows; r0 += (int64_t)gridDim.x * kRows)
-        for (int x = threadIdx.x; x < B.X; x += blockDim.x) {
-            uint64_t kv[kRows];
-            uint8_t fx[kRows];
-#pragma unroll
-            for (int rr = 0; rr < kRows; ++rr) {
-                const int64_t gi = B.base + (r0 + rr) * B.X + x;
-                const bool ok = r0 + rr < nrows;
-                kv[rr] = ok ? key[gi] : kInfKey;
-                fx[rr] = ok ? fixedv[gi] : 0;
-            }
-#pragma unroll
-            for (int rr = 0; rr < kRows; ++rr) {
-                const int64_t row = r0 + rr;
-                if (row >= nrows) break;
-                const int64_t gi = B.base + row * B.X + x;
-                const uint32_t l = kv[rr] == kInfKey ? 0u : (uint32_t)(kv[rr] & kLab);
-                const bool keep = l != 0 && (counts[B.base + l] >= size_filter || (excl && excl[B.base + l]));
-                if (keep) {
-                    if (!fx[rr]) {
-                        key[gi] = ((uint64_t)ordf(h[gi]) << 32) | (uint64_t)l;
-                        fixedv[gi] = 1;
-                    }
-                } else {
-                    if (kv[rr] != kInfKey) key[gi] = kInfKey;
-                    if (fx[rr]) fixedv[gi] = 0;
+    // word tiles: a wave's ballot is exactly one word of the open / changed bitmaps
+    WORD_TILES(B.Z, B.Y, B.X, {
+        // loads unconditional (clamped index): key, seed flag and height together, then the
+        // label's count
+        const int64_t gi = B.base + (valid ? i : row * B.X);
+        const uint64_t kv0 = key[gi];
+        const uint8_t fx0 = fixedv[gi];
+        const float hv = h[gi];
+        const uint64_t kv = valid ? kv0 : kInfKey;
+        const uint8_t fx = valid ? fx0 : 0;
+        const uint32_t l = kv == kInfKey ? 0u : (uint32_t)(kv & kLab);
+        const uint32_t cnt = counts[B.base + l];
+        const bool ex = excl ? excl[B.base + l] != 0 : false;
+        const bool keep = l != 0 && (cnt >= size_filter || ex);
+        if (valid) {
+            if (keep) {
+                if (!fx) {
+                    key[gi] = ((uint64_t)ordf(hv) << 32) | (uint64_t)l;
+                    fixedv[gi] = 1;
                 }
-                const uint64_t op = __ballot(!keep);
-                const uint64_t kp = __ballot(keep);
-                if ((threadIdx.x & 63) == 0) {
-                    open[B.fbase + row * wpr + (x >> 6)] = op;
-                    chg[B.fbase + row * wpr + (x >> 6)] = kp;
-                    if (kp) {
-                        uint32_t* sv = survivors + B.sbase + (B.nd_ws == 2 ? (int)(row / B.Y) : 0);
-                        if (!*sv) *sv = 1;
-                    }
-                }
+            } else {
+                if (kv != kInfKey) key[gi] = kInfKey;
+                if (fx) fixedv[gi] = 0;
             }
         }
+        const uint64_t op = __ballot(valid && !keep);
+        const uint64_t kp = __ballot(valid && keep);
+        if (lane == 0) {
+            open[B.fbase + w_] = op;
+            chg[B.fbase + w_] = kp;
+            if (kp) {
+                uint32_t* sv = survivors + B.sbase + (B.nd_ws == 2 ? z : 0);
+                if (!*sv) *sv = 1;
+            }
+        }
+    })
 }
 
 // Auto-seeded regrow: a slice (2-D) / block (3-D) whose every segment was removed leaves
@@ -293,6 +312,15 @@ __global__ void __launch_bounds__(256) k_auto_seed_set(const BlockDesc* __restri
     }
     if (err) atomicOr(&st.err, err);
 }
+
+template __global__ void k_hist<0>(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, uint32_t*,
+                                   int);
+template __global__ void k_hist<1>(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, uint32_t*,
+                                   int);
+template __global__ void k_hist2d<0>(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*,
+                                     const uint32_t*, uint32_t*, int);
+template __global__ void k_hist2d<1>(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*,
+                                     const uint32_t*, uint32_t*, int);
 
 // zero small segments; survivors become the regrow seeds (fixed, key (h, 0, label)).
 // Packed keys: a voxel that is already fixed (seed or steepest-descent voxel of the first
@@ -400,7 +428,7 @@ __global__ void __launch_bounds__(256) k_slice_max(const BlockDesc* __restrict__
         for (int u = 0; u < U; ++u) {
             const int64_t i = ib + u * 256 + threadIdx.x;
             lv[u] = i < i1 ? flood_label(lab, key, packed, B.base + i) : 0u;
-            in[u] = i < i1 && (!B.mask || B.mask[i]);
+            in[u] = i < i1 && (!B.mask || gbl(B.mask)[i]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -433,7 +461,7 @@ __global__ void __launch_bounds__(256) k_finalize_ws(const BlockDesc* __restrict
     const int64_t YX = (int64_t)B.Y * B.X;
     BLOCK_LOOP(i, B) {
         uint32_t l = flood_label(lab, key, packed, B.base + i);
-        const bool inm = !B.mask || B.mask[i];
+        const bool inm = !B.mask || gbl(B.mask)[i];
         if (B.nd_ws == 2) {
             const int z = (int)(i / YX);
             l = inm ? (l - sb[B.sbase + z]) + soff[B.sbase + z] : 0u;

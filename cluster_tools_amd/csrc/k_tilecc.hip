@@ -75,7 +75,7 @@ template <int MODE>
 __device__ __forceinline__ uint32_t cc_value(const BlockDesc& B, const CcArgs& a, bool plat, int z, int y, int x) {
     if (MODE == CC_CROP) {
         const int64_t o = ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0);
-        if (B.mask && !B.mask[o]) return kLNone;
+        if (B.mask && !gbl(B.mask)[o]) return kLNone;
         const uint32_t l = flood_label(a.lab, a.key, a.packed, B.base + o);
         return l ? l : kLNone;
     } else {

@@ -173,6 +173,7 @@ class Handle:
         for i, r in enumerate(results):
             r['status'] = int(arr[i].status)
             r['max_label'] = int(arr[i].max_label)
+            r['n_ids'] = int(arr[i].n_ids)
         return results
 
     # ---- device (torch) blocks ----------------------------------------------------------
@@ -180,7 +181,7 @@ class Handle:
         """Same with torch tensors resident on this GPU: blocks[i] has 'input' (outer tensor),
         'output' (inner uint64/int64 tensor), optional 'mask' (uint8 tensor), 'initial_seeds'
         (outer int64 tensor, pass 2), 'inner_begin', 'crop_relabel', 'block_id'.
-        Returns [(status, max_label)]."""
+        Returns [(status, max_label, n_ids)]."""
         import torch
         cfg = make_cfg(config, block_shape, pass_id)
         n = len(blocks)
@@ -216,7 +217,7 @@ class Handle:
             c.block_id = int(b.get('block_id', 0))
             c.output = out.data_ptr()
         self._check(lib().ctws_ws_blocks_device(self._h, C.byref(cfg), arr, n), 'ctws_ws_blocks_device')
-        return [(int(arr[i].status), int(arr[i].max_label)) for i in range(n)]
+        return [(int(arr[i].status), int(arr[i].max_label), int(arr[i].n_ids)) for i in range(n)]
 
     # ---- RelabelWorkflow kernels ---------------------------------------------------------
     def unique_u64(self, labels):

@@ -1,0 +1,112 @@
+"""Multi-GPU block sharding: one process per GPU, torch.distributed (RCCL on MI355X, gloo on CPU).
+
+SURVEY.md §8(e).  Blocks are independent units (watershed.py:285-341), so a rank owns a
+contiguous range of the C-order block list — z-slabs of the block grid — and processes it
+without communication.  There are exactly two exchanges:
+
+* the per-block label-count exchange that turns the block-local ids into compact global ids.
+  The reference computes them with files: FindUniques writes per-job uniques, FindLabeling
+  takes np.unique of their concatenation and numbers them consecutively
+  (relabel/find_labeling.py:104-116; the same scan over per-block counts is
+  thresholded_components/merge_offsets.py:106-122).  Watershed ids of block b are
+  b * prod(block_shape) + local, so the sorted global uniques are the blocks' sorted uniques
+  in block order, and the new id of the k-th nonzero unique of block b is
+  1 + (number of nonzero uniques of the blocks before b) + k.  One all-gather of an int64 per
+  block plus a prefix sum replaces the two file round trips.
+* two-pass mode (two_pass_watershed.py:224-228): a pass-2 block reads the pass-1 labels of its
+  halo, `initial_seeds = ds_out[input_bb]`.  Under z-slab sharding only the z-halo rows at a
+  slab boundary belong to another rank; after pass 1 each rank sends its first / last
+  halo[0] rows of labels to the neighbouring ranks (point-to-point over xGMI).
+
+Single-process use (world 1) needs no process group: the functions fall back to local
+computation.
+"""
+import numpy as np
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist if (dist.is_available() and dist.is_initialized()) else None
+
+
+def shard_range(n_items, rank, world):
+    """[begin, end) of the contiguous share of `rank` (sizes differ by at most one)."""
+    return n_items * rank // world, n_items * (rank + 1) // world
+
+
+def shard_blocks(block_list, rank, world):
+    """The rank's contiguous share of a C-order block list (z-slabs of the block grid)."""
+    b, e = shard_range(len(block_list), rank, world)
+    return list(block_list[b:e])
+
+
+def gather_counts(local_counts, device=None):
+    """All-gather the per-block counts of every rank (ranks may hold different numbers of
+    blocks).  Returns one int64 numpy array in rank order, i.e. global block order."""
+    import torch
+    dist = _dist()
+    local = torch.as_tensor(np.asarray(local_counts, dtype=np.int64), device=device)
+    if dist is None or dist.get_world_size() == 1:
+        return local.cpu().numpy()
+    world = dist.get_world_size()
+    n = torch.tensor([local.numel()], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes)
+    padded = torch.zeros(m, dtype=torch.int64, device=device)
+    padded[:local.numel()] = local
+    parts = [torch.zeros(m, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(parts, padded)
+    return np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)])
+
+
+def compact_offsets(all_counts):
+    """Exclusive scan of the per-block nonzero-unique counts (global block order): block b's
+    k-th nonzero id (k = 0, 1, ...) gets the new id offsets[b] + k + 1.  Also returns the new
+    max id (relabel/find_labeling.py:108-116: 0 keeps 0, the others are numbered from 1)."""
+    c = np.asarray(all_counts, dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum(c)[:-1]]) if len(c) else np.zeros(0, np.int64)
+    return offs.astype(np.int64), int(c.sum())
+
+
+def block_relabel_table(block_uniques, offset):
+    """(old, new) of one block: its sorted uniques -> offset + 1 + rank (0 stays 0)."""
+    u = np.asarray(block_uniques, dtype=np.uint64)
+    nz = u[u != 0]
+    new = np.arange(offset + 1, offset + 1 + len(nz), dtype=np.uint64)
+    if len(nz) != len(u):
+        return np.concatenate([[0], nz]).astype(np.uint64), np.concatenate([[0], new]).astype(np.uint64)
+    return nz, new
+
+
+def exchange_z_halos(vol, lo, hi):
+    """Fill the z-halo rows of a rank's labels from its slab neighbours.
+
+    `vol` is the rank's (lo + Z + hi, Y, X) tensor: rows [lo, lo + Z) are its own labels;
+    rows [0, lo) receive the last lo own rows of rank - 1, rows [lo + Z, lo + Z + hi) the
+    first hi own rows of rank + 1 (slabs are contiguous in rank order, so both neighbours'
+    halos across a shared boundary have the same thickness).  Rows without a neighbouring
+    rank are left as they are.  Point-to-point, one send and one receive per neighbour."""
+    dist = _dist()
+    if dist is None or dist.get_world_size() == 1:
+        return vol
+    rank, world = dist.get_rank(), dist.get_world_size()
+    Z = vol.shape[0] - lo - hi
+    ops, recv_lo, recv_hi = [], None, None
+    if rank > 0 and lo:
+        ops.append(dist.P2POp(dist.isend, vol[lo:2 * lo].contiguous(), rank - 1))
+        recv_lo = vol.new_empty((lo,) + tuple(vol.shape[1:]))
+        ops.append(dist.P2POp(dist.irecv, recv_lo, rank - 1))
+    if rank + 1 < world and hi:
+        ops.append(dist.P2POp(dist.isend, vol[lo + Z - hi:lo + Z].contiguous(), rank + 1))
+        recv_hi = vol.new_empty((hi,) + tuple(vol.shape[1:]))
+        ops.append(dist.P2POp(dist.irecv, recv_hi, rank + 1))
+    if ops:
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    if recv_lo is not None:
+        vol[:lo] = recv_lo
+    if recv_hi is not None:
+        vol[lo + Z:] = recv_hi
+    return vol

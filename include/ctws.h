@@ -117,7 +117,9 @@ typedef struct ctws_block {
     uint64_t*       output;          /* inner-shaped uint64                                */
     uint64_t        max_label;       /* out: largest local label before the id offset      */
     int32_t         status;          /* out: CTWS_BLOCK_*                                  */
-    int32_t         _pad1;
+    int32_t         n_ids;           /* out: distinct nonzero output ids of the block (pass */
+                                     /* 0; -1 in pass 2): the per-block count of the       */
+                                     /* compact-id exclusive scan (find_labeling.py:104)   */
 } ctws_block;
 
 typedef struct ctws_handle ctws_handle;

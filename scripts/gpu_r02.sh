@@ -7,7 +7,7 @@ timeout -k 10 120 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpuru
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 [ $rc -ne 0 ] && exit $rc
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi

@@ -19,8 +19,11 @@ VI_TOL = 0.01
 ARE_TOL = 1e-3
 # Inputs whose hmap is dominated by exact ties (4-level quantized, no smoothing): vigra orders
 # equal priorities by binary-heap position, which no deterministic parallel schedule
-# reproduces; there the GPU must still equal the flood model exactly.
-TIE_DOMINATED = {'3d_plateaus'}
+# reproduces.  There the GPU must equal the flood model exactly (test_flood_matches_model_
+# exactly), the whole VI gap must be the model's tie order (VI(GPU, heap) == VI(model, heap)),
+# and the gap stays below the recorded synthetic worst case.  Every BASELINE
+# config meets the VI bar itself (tests/test_config_blocks.py).
+TIE_DOMINATED = {'3d_plateaus': 1.2}
 
 
 def _oracle_seeds(config, dt):
@@ -94,8 +97,13 @@ def test_fragments_vi(gpu_handle, name):
     are, _ = rand_scores(out, gt, ign)
     print('%s: VI split %.2e merge %.2e, ARE %.2e, exact %s' % (name, vis, vim, are, np.array_equal(out, gt)))
     if name in TIE_DOMINATED:
-        pytest.skip('tie-dominated input: VI %.3f vs vigra heap order (GPU == model checked above)'
-                    % (vis + vim))
+        with O.flood_model():
+            model = O.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=3)])[0]
+        gap = sum(vi_scores(model['output'], gt, ign))
+        print('%s: tie-dominated, VI(model, heap) %.3f' % (name, gap))
+        assert abs((vis + vim) - gap) <= 1e-9, (vis + vim, gap)
+        assert gap <= TIE_DOMINATED[name], gap
+        return
     assert vis + vim <= VI_TOL, (vis, vim)
     assert are <= ARE_TOL, are
     # ids live in this block's offset range; masked voxels are 0 (watershed.py:331-337)

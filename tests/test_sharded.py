@@ -1,0 +1,122 @@
+"""Multi-process (world_size 2, gloo on CPU) tests of the block-sharding exchanges
+(cluster_tools_amd/watershed/sharded.py):
+
+* per-block label counts all-gathered + exclusively scanned give exactly the consecutive ids
+  RelabelWorkflow's FindLabeling assigns (relabel/find_labeling.py:104-116) on the same
+  blocks — including blocks with gaps in their ids, all-zero blocks, the constant-offset
+  empty blocks and ranks holding different numbers of blocks;
+* the two-pass z-halo exchange delivers each neighbour's boundary rows.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as tmp
+
+from cluster_tools_amd.watershed import sharded
+
+V = 4 * 16 * 16          # prod(block_shape) of the synthetic blocks
+N_BLOCKS = 7             # odd: the two ranks hold 3 and 4 blocks
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _ws_like_outputs(seed=0):
+    """Per-block uint64 outputs shaped like watershed outputs: block_id * V + local ids with
+    gaps (size-filtered labels), some background 0, block 2 empty (constant offset), block 5
+    all background."""
+    rng = np.random.RandomState(seed)
+    outs = []
+    for b in range(N_BLOCKS):
+        if b == 2:
+            outs.append(np.full(V, b * V, np.uint64))
+            continue
+        if b == 5:
+            outs.append(np.zeros(V, np.uint64))
+            continue
+        local = rng.choice(np.arange(1, V), size=rng.randint(5, 40), replace=False)
+        x = (b * V + rng.choice(local, size=V)).astype(np.uint64)
+        x[rng.rand(V) < 0.1] = 0
+        outs.append(x)
+    return outs
+
+
+def _find_labeling_reference(outs):
+    """FindUniques + FindLabeling + Write on the whole set, as the reference numbers them."""
+    u = np.unique(np.concatenate(outs))
+    start = 0 if u[0] == 0 else 1
+    new = np.arange(start, start + len(u), dtype=np.uint64)
+    lut = dict(zip(u.tolist(), new.tolist()))
+    return [np.array([lut[v] for v in o.tolist()], np.uint64) for o in outs]
+
+
+def _worker(rank, world, port, outdir):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        outs = _ws_like_outputs()
+        mine = sharded.shard_blocks(list(range(N_BLOCKS)), rank, world)
+        uniques = {b: np.unique(outs[b]) for b in mine}
+        counts = [int((uniques[b] != 0).sum()) for b in mine]
+        all_counts = sharded.gather_counts(counts)
+        offs, n_ids = sharded.compact_offsets(all_counts)
+        for b in mine:
+            old, new = sharded.block_relabel_table(uniques[b], int(offs[b]))
+            lut = dict(zip(old.tolist(), new.tolist()))
+            np.save(os.path.join(outdir, 'block_%d.npy' % b), np.array([lut[v] for v in outs[b].tolist()], np.uint64))
+        np.save(os.path.join(outdir, 'n_ids_%d.npy' % rank), np.array([n_ids]))
+        # two-pass z-halo exchange: rank r's own rows hold 100 * r + row index
+        hz, Z = 2, 5
+        vol = torch.full((Z + 2 * hz, 3, 4), -1, dtype=torch.int64)
+        for z in range(Z):
+            vol[hz + z] = 100 * rank + z
+        sharded.exchange_z_halos(vol, hz, hz)
+        np.save(os.path.join(outdir, 'halo_%d.npy' % rank), vol.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharding_is_contiguous_and_complete():
+    for n, w in ((7, 2), (256, 8), (3, 8)):
+        parts = [sharded.shard_blocks(list(range(n)), r, w) for r in range(w)]
+        assert sum(parts, []) == list(range(n))
+        assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+def test_compact_offsets_single_process_equals_find_labeling():
+    outs = _ws_like_outputs(seed=3)
+    ref = _find_labeling_reference(outs)
+    uniques = [np.unique(o) for o in outs]
+    offs, n_ids = sharded.compact_offsets([int((u != 0).sum()) for u in uniques])
+    for o, u, off, r in zip(outs, uniques, offs, ref):
+        old, new = sharded.block_relabel_table(u, int(off))
+        lut = dict(zip(old.tolist(), new.tolist()))
+        assert np.array_equal(np.array([lut[v] for v in o.tolist()], np.uint64), r)
+    assert n_ids == max(int(r.max()) for r in ref)
+
+
+def test_two_ranks_gloo_offsets_and_halo_exchange(tmp_path):
+    world = 2
+    tmp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    outs = _ws_like_outputs()
+    ref = _find_labeling_reference(outs)
+    for b in range(N_BLOCKS):
+        got = np.load(tmp_path / ('block_%d.npy' % b))
+        assert np.array_equal(got, ref[b]), b
+    n0, n1 = (int(np.load(tmp_path / ('n_ids_%d.npy' % r))[0]) for r in range(world))
+    assert n0 == n1 == max(int(r.max()) for r in ref)
+    h0 = np.load(tmp_path / 'halo_0.npy')
+    h1 = np.load(tmp_path / 'halo_1.npy')
+    hz, Z = 2, 5
+    assert (h0[:hz] == -1).all()                          # outer slab: untouched
+    assert (h0[Z + hz:] == h1[hz:2 * hz]).all()            # rank 1's first own rows
+    assert (h1[:hz] == h0[Z:Z + hz]).all()                 # rank 0's last own rows
+    assert (h1[Z + hz:] == -1).all()
