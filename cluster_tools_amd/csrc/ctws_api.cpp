@@ -103,6 +103,7 @@ struct ctws_handle {
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int gauss_w = 0;  // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
+    int gauss_yx = 1;  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     int frontier_unroll = 1;  // CTWS_FRONTIER_UNROLL (1, 2, 4, 8): list entries per lane in flight
     int frontier_reps = 4;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch
@@ -354,6 +355,10 @@ const GaussKernel kGaussRowR[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_ROWR)};
 const GaussKernel kGaussColR32[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_COL32)};
 const GaussKernel kGaussColR16[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_COL16)};
 const GaussKernel kGaussColR8[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_COL8)};
+#define CTWS_YX(R) &k_gauss_yx<R>
+using GaussYxKernel = decltype(&k_gauss_yx<1>);
+const GaussYxKernel kGaussYx[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_YX)};
+#undef CTWS_YX
 #undef CTWS_R12
 #undef CTWS_ROWR
 #undef CTWS_COL32
@@ -381,8 +386,6 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
         const int a = axes[i];
         auto taps = gaussian_taps(sig[a]);
         const int r = (int)taps.size() / 2;
-        const int L = a == 0 ? maxZ : (a == 1 ? maxY : maxX);
-        (void)L;
         double* dtaps = w.taps + (taps_slot * 3 + a) * 128;
         double* htaps = h->h_taps + (taps_slot * 3 + a) * 128;
         std::memcpy(htaps, taps.data(), sizeof(double) * taps.size());
@@ -390,6 +393,24 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
         float* out = (i == na - 1) ? dst : ((i % 2 == 0) ? w.A : w.Bf);
         GaussParams gp{a, r, (i == 0 && hmap_src) ? 1 : 0};
         const float* in = (i == 0 && hmap_src) ? w.fin : cur;
+        // the last two axes y, x with one radius: fused tile kernel (k_gauss_yx)
+        if (h->gauss_yx && a == 1 && i + 1 == na - 1 && axes[i + 1] == 2 && r >= 1 && r <= kGaussMaxR) {
+            auto tx = gaussian_taps(sig[2]);
+            if ((int)tx.size() / 2 == r) {
+                double* dtx = w.taps + (taps_slot * 3 + 2) * 128;
+                double* htx = h->h_taps + (taps_slot * 3 + 2) * 128;
+                std::memcpy(htx, tx.data(), sizeof(double) * tx.size());
+                HIPCHK(hipMemcpyAsync(dtx, htx, sizeof(double) * tx.size(), hipMemcpyHostToDevice, h->stream));
+                const int TX = 128 - 2 * r;
+                const int64_t ntiles = (int64_t)maxZ * ((maxY + kGaussYxTY - 1) / kGaussYxTY) * ((maxX + TX - 1) / TX);
+                dim3 g((unsigned)ntiles, nb);
+                hipLaunchKernelGGL(kGaussYx[r], g, dim3(256), 0, h->stream, w.desc, w.stat, gp.hmap_src, hp,
+                                   (const double*)dtaps, (const double*)dtx, in, (const float*)w.dt,
+                                   (const uint32_t*)w.smin, (const uint32_t*)w.smax, dst);
+                LAUNCHCHK();
+                return CTWS_OK;
+            }
+        }
         if (r >= 1 && r <= kGaussMaxR) {
             // sliding-window kernels (k_gauss.hip)
             if (a == 2) {
@@ -1426,6 +1447,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))
         h->frontier_max_iters = std::max(0, std::min(kFrontierMaxItersCap, std::atoi(t)));
+    if (const char* t = std::getenv("CTWS_GAUSS_YX")) h->gauss_yx = std::atoi(t);
     if (const char* t = std::getenv("CTWS_GAUSS_W")) {
         const int v = std::atoi(t);
         h->gauss_w = (v == 8 || v == 16 || v == 32) ? v : 0;

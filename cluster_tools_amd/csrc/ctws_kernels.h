@@ -63,6 +63,11 @@ __global__ void k_gauss_col_r(const BlockDesc*, const BlockStat*, GaussParams, H
 template <int R>
 __global__ void k_gauss_row_r(const BlockDesc*, const BlockStat*, GaussParams, HmapParams, const double*, const float*,
                               const float*, const uint32_t*, const uint32_t*, float*);
+// fused y + x passes on 2-D tiles: kGaussYxTY rows x (128 - 2R) columns per workgroup
+constexpr int kGaussYxTY = 32;
+template <int R>
+__global__ void k_gauss_yx(const BlockDesc*, const BlockStat*, int, HmapParams, const double*, const double*,
+                           const float*, const float*, const uint32_t*, const uint32_t*, float*);
 
 // k_cc.hip
 __global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, uint32_t*);

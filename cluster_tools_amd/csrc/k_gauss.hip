@@ -315,7 +315,148 @@ __global__ void __launch_bounds__(256) k_gauss_row_r(const BlockDesc* __restrict
     }
 }
 
+// =========================================================================================
+// Fused y + x passes on a 2-D tile of one slice (both axes with radius R).  The separate
+// passes write the y-smoothed volume to HBM and read it back (16 B per voxel for the pair);
+// here the y result stays in LDS (as float, exactly the rounding between axes vigra does), so
+// a pair costs 4 B in + 4 B out per voxel plus halo re-reads (mostly L2 hits).
+//   tile: kYxTY rows x (128 - 2R) columns of outputs; the LDS window is (kYxTY + 2R) x 128,
+//   rows/columns outside the block reflected at staging, so both passes read plain LDS.
+//   y pass: thread = (column, half of the rows), a 16-output sliding window per thread;
+//   x pass: thread = (row, eighth of the row); outputs go back through LDS for coalesced
+//   stores.  Arithmetic per output as gauss_run: double products over ascending positions.
+// Tiles of one XCD are contiguous (blockIdx round-robins over the 8 XCDs), so vertically
+// adjacent tiles that share halo rows share an L2.
+// =========================================================================================
+constexpr int kYxTY = kGaussYxTY;
+constexpr int kYxP = 129;  // LDS pitch: 128 + 1
+
+__host__ __device__ constexpr int gauss_yx_tx(int R) { return 128 - 2 * R; }
+
+template <int R>
+__global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ D, const BlockStat* S, int hmap_src,
+                                                  HmapParams hp, const double* __restrict__ taps_y,
+                                                  const double* __restrict__ taps_x, const float* __restrict__ in,
+                                                  const float* __restrict__ dt, const uint32_t* smin,
+                                                  const uint32_t* smax, float* __restrict__ out) {
+    constexpr int TX = gauss_yx_tx(R);
+    constexpr int NROW = kYxTY + 2 * R;
+    constexpr int NL = NROW / 2;  // staged rows per thread
+    __shared__ float win_s[NROW * kYxP];
+    const BlockDesc& B = D[blockIdx.y];
+    const BlockStat& st = S[blockIdx.y];
+    if (!st.active) return;
+    const int Y = B.Y, X = B.X;
+    const int ntx = (X + TX - 1) / TX, nty = (Y + kYxTY - 1) / kYxTY;
+    // XCD-contiguous tile order
+    const int n = gridDim.x, per = n >> 3;
+    const int bid = blockIdx.x;
+    const int t = bid < (per << 3) ? (bid & 7) * per + (bid >> 3) : bid;
+    if (t >= B.Z * nty * ntx) return;
+    const int z = t / (nty * ntx), rem = t - z * (nty * ntx);
+    const int y0 = (rem / ntx) * kYxTY, x0 = (rem % ntx) * TX;
+    const int tid = threadIdx.x;
+    const int c = tid & 127, half = tid >> 7;
+    auto refl = [](int p, int L) { return min(max(reflect_idx(p, L), 0), L - 1); };
+    const int64_t sbase = B.base + (int64_t)z * Y * X;
+    const int gx = refl(x0 - R + c, X);
+    // ---- stage: NL rows per thread, all loads in flight
+    if (hmap_src) {
+        float mn, mx;
+        if (hp.per_slice) {
+            mn = unordf(smin[B.sbase + z]);
+            mx = unordf(smax[B.sbase + z]);
+        } else {
+            mn = unordf(st.dt_min);
+            mx = unordf(st.dt_max);
+        }
+        const float den = mx - mn;
+        float vf[NL], vd[NL];
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            const int64_t gi = sbase + (int64_t)refl(y0 - R + 2 * i + half, Y) * X + gx;
+            vf[i] = gbl(in)[gi];
+            vd[i] = gbl(dt)[gi];
+        }
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            float d = vd[i] - mn;
+            if (den > 0.0f) d = d / den;
+            d = 1.0f - d;
+            const float t1 = hp.a * vf[i];
+            const float t2 = hp.b * d;
+            win_s[(2 * i + half) * kYxP + c] = t1 + t2;
+        }
+    } else {
+        float v[NL];
+#pragma unroll
+        for (int i = 0; i < NL; ++i) v[i] = gbl(in)[sbase + (int64_t)refl(y0 - R + 2 * i + half, Y) * X + gx];
+#pragma unroll
+        for (int i = 0; i < NL; ++i) win_s[(2 * i + half) * kYxP + c] = v[i];
+    }
+    __syncthreads();
+    // ---- y pass: column c, output rows [16 half, 16 half + 16)
+    {
+        double k[2 * R + 1];
+        load_taps<R>(taps_y, k);
+        const int p0 = half * (kYxTY / 2);
+        double w[2 * R + 1];
+#pragma unroll
+        for (int m = 0; m < 2 * R; ++m) w[m] = (double)win_s[(p0 + m) * kYxP + c];
+        float res[kYxTY / 2];
+#pragma unroll
+        for (int i = 0; i < kYxTY / 2; ++i) {
+            w[(i + 2 * R) % (2 * R + 1)] = (double)win_s[(p0 + i + 2 * R) * kYxP + c];
+            double sum = 0.0;
+#pragma unroll
+            for (int m = 0; m <= 2 * R; ++m) sum += k[2 * R - m] * w[(i + m) % (2 * R + 1)];
+            res[i] = (float)sum;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kYxTY / 2; ++i) win_s[(p0 + i) * kYxP + c] = res[i];
+    }
+    __syncthreads();
+    // ---- x pass: row p, columns [xs, xe) of the TX outputs
+    constexpr int RUNX = (TX + 7) / 8;
+    const int p = tid >> 3, j = tid & 7;
+    const int xs = (j * TX) >> 3, xe = ((j + 1) * TX) >> 3;
+    {
+        double k[2 * R + 1];
+        load_taps<R>(taps_x, k);
+        const float* rb = win_s + p * kYxP + xs;
+        double w[2 * R + 1];
+#pragma unroll
+        for (int m = 0; m < 2 * R; ++m) w[m] = (double)rb[m];
+        float res[RUNX];
+#pragma unroll
+        for (int i = 0; i < RUNX; ++i) {
+            // the phantom output of a short run reads at most column 128 (the pad word)
+            w[(i + 2 * R) % (2 * R + 1)] = (double)rb[i + 2 * R];
+            double sum = 0.0;
+#pragma unroll
+            for (int m = 0; m <= 2 * R; ++m) sum += k[2 * R - m] * w[(i + m) % (2 * R + 1)];
+            res[i] = (float)sum;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < RUNX; ++i)
+            if (xs + i < xe) win_s[p * kYxP + xs + i] = res[i];
+    }
+    __syncthreads();
+    // ---- coalesced stores of the valid part of the tile
+    const int ny = min(kYxTY, Y - y0), nx = min(TX, X - x0);
+    gwptr_t<float> o = gblw(out) + sbase + (int64_t)y0 * X + x0;
+    for (int v = tid; v < kYxTY * TX; v += 256) {
+        const int pp = v / TX, xx = v - pp * TX;
+        if (pp < ny && xx < nx) o[(int64_t)pp * X + xx] = win_s[pp * kYxP + xx];
+    }
+}
+
 #define CTWS_GAUSS_R(R)                                                                                          \
+    template __global__ void k_gauss_yx<R>(const BlockDesc*, const BlockStat*, int, HmapParams, const double*,     \
+                                           const double*, const float*, const float*, const uint32_t*,             \
+                                           const uint32_t*, float*);                                               \
     template __global__ void k_gauss_col_r<32, R>(const BlockDesc*, const BlockStat*, GaussParams, HmapParams,      \
                                                   const double*, const float*, const float*, const uint32_t*,       \
                                                   const uint32_t*, float*);                                        \
