@@ -95,6 +95,8 @@ struct ctws_handle {
     // relabel (k_relabel.hip)
     DevBuf rl_lab, rl_bits, rl_cnt, rl_offs, rl_out, rl_keys, rl_vals, rl_red;
     int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
+    // EDT: counters (64 B) + columns queued for the lower-envelope pass (k_edt_col_fh)
+    DevBuf edt_fh;
     // test hooks
     int stop_after = 0;
     int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
@@ -858,22 +860,39 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         EdtColParams ep{1, pl.pitch[1] * pl.pitch[1], pl.dt_2d, pl.dt_2d, 0u};
         dim3 gy((unsigned)((int64_t)maxZ * ((maxX + Wy - 1) / Wy)), nb);
         const size_t ldsy = (size_t)maxY * Wy * 4;
-        auto launch_col = [&](int W, dim3 g, size_t lds, EdtColParams p, const uint32_t* gin, uint32_t* gout) {
+        // columns that may go to the lower-envelope pass: one entry each at most
+        int64_t ncols = 0, ncols_z = 0;
+        for (auto& d : desc) {
+            ncols += (int64_t)d.Z * d.X;
+            ncols_z += (int64_t)d.Y * d.X;
+        }
+        if (!pl.dt_2d) ncols = std::max(ncols, ncols_z);
+        if ((r = grow(h, h->edt_fh, 64 + 8 * (size_t)ncols)) != CTWS_OK) return r;
+        uint32_t* fh_cnt = (uint32_t*)h->edt_fh.p;
+        unsigned long long* fh_list = (unsigned long long*)((char*)h->edt_fh.p + 64);
+        HIPCHK(hipMemsetAsync(fh_cnt, 0, 64, h->stream));
+        const unsigned gfh = (unsigned)std::min<int64_t>((ncols + 255) / 256, 1024);
+        auto launch_col = [&](int W, dim3 g, size_t lds, EdtColParams p, const uint32_t* gin, uint32_t* gout,
+                              uint32_t* cnt) {
             if (W == 32)
-                k_edt_col<32><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax);
+                k_edt_col<32><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list,
+                                                          cnt);
             else if (W == 16)
-                k_edt_col<16><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax);
+                k_edt_col<16><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list,
+                                                          cnt);
             else
-                k_edt_col<8><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax);
+                k_edt_col<8><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list,
+                                                         cnt);
+            k_edt_col_fh<<<gfh, 256, 0, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list, cnt);
         };
-        launch_col(Wy, gy, ldsy, ep, (uint32_t*)w.A, (uint32_t*)w.Bf);
+        launch_col(Wy, gy, ldsy, ep, (uint32_t*)w.A, (uint32_t*)w.Bf, fh_cnt);
         LAUNCHCHK();
         if (!pl.dt_2d) {
             const int Wz = h->edt_w ? h->edt_w : edt_col_width(maxZ);
             dim3 gz((unsigned)((int64_t)maxY * ((maxX + Wz - 1) / Wz)), nb);
             const size_t ldsz = (size_t)maxZ * Wz * 4;
             EdtColParams ez{2, pl.pitch[0] * pl.pitch[0], 1, 0, 0u};
-            launch_col(Wz, gz, ldsz, ez, (uint32_t*)w.Bf, nullptr);
+            launch_col(Wz, gz, ldsz, ez, (uint32_t*)w.Bf, nullptr, fh_cnt + 1);
             LAUNCHCHK();
             if (pl.nd_ws == 2) {
                 dim3 gs((unsigned)maxZ, nb);
@@ -881,6 +900,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 LAUNCHCHK();
             }
         }
+    }
+    if (h->trace) {
+        uint32_t c[2];
+        HIPCHK(hipMemcpy(c, h->edt_fh.p, sizeof(c), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[ctws] edt lower-envelope columns: y %u z %u\n", c[0], c[1]);
     }
     if (pl.pass2 && pl.nd_ws == 2) {
         // two_pass_watershed.py:139: no maxima on initial seeds; per-slice dt stats again
@@ -1477,7 +1501,8 @@ void ctws_close(ctws_handle* h) {
                     w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.lines0, w.lines1, w.desc, w.stat, w.counter,
                     w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
                     w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
-                    h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p};
+                    h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p,
+                    h->edt_fh.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);

@@ -42,9 +42,12 @@ template <int KMAX, class T>
 __global__ void k_prep_edt_x_co(const BlockDesc*, BlockStat*, PrepParams, float*, uint32_t*);
 template <class T>
 __global__ void k_input_minmax_t(const BlockDesc*, BlockStat*);
+constexpr int kEdtSearchCap = 48;  // bounded-search steps before a column goes to k_edt_col_fh
 template <int W>
 __global__ void k_edt_col(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*, uint32_t*,
-                          uint32_t*);
+                          uint32_t*, unsigned long long*, uint32_t*);
+__global__ void k_edt_col_fh(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*, uint32_t*,
+                             uint32_t*, const unsigned long long*, const uint32_t*);
 __global__ void k_dt_slice_stats(const BlockDesc*, const BlockStat*, const float*, uint32_t*, uint32_t*);
 __global__ void k_set_active(const BlockDesc*, BlockStat*, int);
 

@@ -430,17 +430,25 @@ __device__ __forceinline__ float sqrt_rn_int(uint32_t n) {
 }
 
 // ---- EDT pass along y (stride X) or z (stride Y*X), LDS-staged columns -----------------
-// Tile: the full line (length L) x W consecutive x positions.  Bounded brute force:
+// Tile: the full line (length L) x W consecutive x positions.  Bounded search:
 //   best = g[p]; for r = 1.. while p2 r^2 < best: best = min(best, g[p +- r] + p2 r^2)
+// exact (no candidate farther than sqrt(best / p2) can win) and O(distance) per voxel, which on
+// boundary maps is a handful of LDS reads.  A voxel still searching after kEdtSearchCap steps
+// (a line with no or far-away foreground) stops; its column is queued and k_edt_col_fh redoes
+// the column with the Felzenszwalb-Huttenlocher lower envelope of parabolas, O(L) per column
+// whatever the distances.  Capped voxels stay out of the dt statistics (k_edt_col_fh adds
+// its column's).
 // FINAL: clamp to maxDist = ceil(dmax) and write sqrtf(d2) as float, with dt statistics.
 
 template <int W>
 __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D, BlockStat* S, EdtColParams ep,
                                                  const uint32_t* __restrict__ gin, uint32_t* __restrict__ gout,
                                                  float* __restrict__ dt, uint32_t* __restrict__ slice_min,
-                                                 uint32_t* __restrict__ slice_max) {
+                                                 uint32_t* __restrict__ slice_max, unsigned long long* fh_list,
+                                                 uint32_t* fh_cnt) {
     extern __shared__ __attribute__((aligned(16))) int smem_i[];
     uint32_t* col = (uint32_t*)smem_i;
+    __shared__ uint32_t capped_cols;  // bit c: a voxel of column c hit kEdtSearchCap
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int nxc = (B.X + W - 1) / W;
@@ -462,22 +470,36 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
             r0, L, RS, [&](int p) { return colok ? gsrc[p * lstride] : kInfD2; },
             [&](int p, uint32_t v) { col[p * W + c] = v; });
     }
+    if (threadIdx.x == 0) capped_cols = 0u;
     __syncthreads();
     uint32_t mn = 0xFFFFFFFFu, mx = 0u;
     const uint32_t maxd = ep.per_slice ? (uint32_t)(B.Y * B.Y + B.X * B.X) : B.maxd;
+    bool capped_any = false;
+    const uint32_t p2 = (uint32_t)ep.p2;
     for (int p = r0; p < L; p += RS) {
         uint32_t best = col[p * W + c];
-        for (int r = 1;; ++r) {
-            const uint32_t rr = (uint32_t)ep.p2 * (uint32_t)(r * r);
-            if (rr >= best) break;
-            const bool lo = p - r >= 0, hi = p + r < L;
-            if (!lo && !hi) break;
-            if (lo) best = min(best, col[(p - r) * W + c] + rr);
-            if (hi) best = min(best, col[(p + r) * W + c] + rr);
+        // radii r and r + 1 per step: four LDS reads in flight (clamped index, INF outside the
+        // line; INF + p2 r^2 < 2^31 never wins)
+        const int rlim = max(p, L - 1 - p);  // no candidates beyond
+        const int rcap = min(rlim, kEdtSearchCap);
+        int r = 1;
+        for (; r <= rcap; r += 2) {
+            const uint32_t rr0 = p2 * (uint32_t)(r * r);
+            if (rr0 >= best) break;
+            const uint32_t rr1 = p2 * (uint32_t)((r + 1) * (r + 1));
+            const uint32_t a = col[max(p - r, 0) * W + c], b = col[min(p + r, L - 1) * W + c];
+            const uint32_t a1 = col[max(p - r - 1, 0) * W + c], b1 = col[min(p + r + 1, L - 1) * W + c];
+            const uint32_t m0 = min(p - r >= 0 ? a : kInfD2, p + r < L ? b : kInfD2);
+            const uint32_t m1 = min(p - r - 1 >= 0 ? a1 : kInfD2, p + r + 1 < L ? b1 : kInfD2);
+            best = min(best, min(m0 + rr0, m1 + rr1));
         }
+        const bool capped = r <= rlim && p2 * (uint32_t)(r * r) < best;
         if (!colok) continue;
+        capped_any |= capped;
         const int64_t gi = B.base + obase + p * lstride + xb + c;
-        if (ep.final_pass) {
+        if (ep.final_pass && capped) {
+            // k_edt_col_fh rewrites the column
+        } else if (ep.final_pass) {
             const uint32_t d2 = min(best, maxd);
             const float v = sqrt_rn_int(d2);
             dt[gi] = v;
@@ -487,6 +509,13 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
         } else {
             gout[gi] = best;
         }
+    }
+    if (capped_any) atomicOr(&capped_cols, 1u << c);
+    __syncthreads();
+    if (threadIdx.x < W && ((capped_cols >> threadIdx.x) & 1u)) {
+        const uint32_t e = atomicAdd(fh_cnt, 1u);
+        fh_list[e] = ((unsigned long long)blockIdx.y << 48) | ((unsigned long long)o << 24) |
+                     (unsigned long long)(xb + threadIdx.x);
     }
     if (ep.final_pass) {
         // workgroup reduce, then per block (3-D ws) and per slice (2-D dt: o is z)
@@ -514,12 +543,110 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
     }
 }
 
-template __global__ void k_edt_col<32>(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*,
-                                       uint32_t*, uint32_t*);
-template __global__ void k_edt_col<16>(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*,
-                                       uint32_t*, uint32_t*);
-template __global__ void k_edt_col<8>(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*,
-                                      uint32_t*, uint32_t*);
+#define CTWS_EDT_COL(W)                                                                                          \
+    template __global__ void k_edt_col<W>(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*,   \
+                                          float*, uint32_t*, uint32_t*, unsigned long long*, uint32_t*);
+CTWS_EDT_COL(32)
+CTWS_EDT_COL(16)
+CTWS_EDT_COL(8)
+#undef CTWS_EDT_COL
+
+// floor(a / b) for b > 0
+__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+// Columns queued by k_edt_col: the exact 1-D squared distance transform of the line by the lower
+// envelope of the parabolas p2 (u - s)^2 + g[s] over the finite g[s] (Felzenszwalb-Huttenlocher,
+// in Meijster's integer form: parabola u takes over from the stack top s at
+// w = 1 + floor((p2 (u^2 - s^2) + g[u] - g[s]) / (2 p2 (u - s)))).  One thread per column.  The
+// stack (s | t << 16 per entry, t = first position of the entry's interval) lives in the
+// column's own output cells: entry k sits at position k <= t[k] <= u, so the backward pass
+// reads an entry before the output of its position is written.  Same values as the bounded
+// search (min over all finite g of g[s] + p2 (u - s)^2, kInfD2 on an all-INF line).
+__global__ void __launch_bounds__(256) k_edt_col_fh(const BlockDesc* __restrict__ D, BlockStat* S, EdtColParams ep,
+                                                    const uint32_t* __restrict__ gin, uint32_t* gout, float* dt,
+                                                    uint32_t* __restrict__ slice_min, uint32_t* __restrict__ slice_max,
+                                                    const unsigned long long* __restrict__ fh_list,
+                                                    const uint32_t* __restrict__ fh_cnt) {
+    const uint32_t n = *fh_cnt;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        const unsigned long long ent = fh_list[e];
+        const int bi = (int)(ent >> 48), o = (int)((ent >> 24) & 0xFFFFFFull), x = (int)(ent & 0xFFFFFFull);
+        const BlockDesc& B = D[bi];
+        const int L = (ep.axis == 1) ? B.Y : B.Z;
+        const int64_t lstride = (ep.axis == 1) ? B.X : (int64_t)B.Y * B.X;
+        const int64_t obase = (ep.axis == 1) ? (int64_t)o * B.Y * B.X : (int64_t)o * B.X;
+        const int64_t cb = B.base + obase + x;
+        const uint32_t* g = gin + cb;
+        uint32_t* stk = (ep.final_pass ? (uint32_t*)dt : gout) + cb;
+        const int64_t p2 = ep.p2;
+        int q = -1, s_top = 0, t_top = 0;
+        int64_t g_top = 0;
+        for (int u = 0; u < L; ++u) {
+            const uint32_t gu32 = g[u * lstride];
+            if (gu32 >= kInfD2) continue;
+            const int64_t gu = gu32;
+            while (q >= 0) {
+                const int64_t fs = p2 * (int64_t)(t_top - s_top) * (t_top - s_top) + g_top;
+                const int64_t fu = p2 * (int64_t)(t_top - u) * (t_top - u) + gu;
+                if (fs <= fu) break;
+                if (--q >= 0) {
+                    const uint32_t wd = stk[q * lstride];
+                    s_top = (int)(wd & 0xFFFFu);
+                    t_top = (int)(wd >> 16);
+                    g_top = g[s_top * lstride];
+                }
+            }
+            if (q < 0) {
+                q = 0;
+                s_top = u;
+                t_top = 0;
+                g_top = gu;
+                stk[0] = (uint32_t)u;
+            } else {
+                const int64_t num = p2 * ((int64_t)u * u - (int64_t)s_top * s_top) + gu - g_top;
+                const int64_t w = 1 + floor_div(num, 2 * p2 * (u - s_top));
+                if (w < L) {
+                    ++q;
+                    s_top = u;
+                    t_top = (int)w;
+                    g_top = gu;
+                    stk[q * lstride] = (uint32_t)u | ((uint32_t)w << 16);
+                }
+            }
+        }
+        uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+        const uint32_t maxd = ep.per_slice ? (uint32_t)(B.Y * B.Y + B.X * B.X) : B.maxd;
+        for (int u = L - 1; u >= 0; --u) {
+            uint32_t best = kInfD2;
+            if (q >= 0) {
+                best = (uint32_t)min(p2 * (int64_t)(u - s_top) * (u - s_top) + g_top, (int64_t)kInfD2);
+                if (u == t_top && --q >= 0) {
+                    const uint32_t wd = stk[q * lstride];
+                    s_top = (int)(wd & 0xFFFFu);
+                    t_top = (int)(wd >> 16);
+                    g_top = g[s_top * lstride];
+                }
+            }
+            if (ep.final_pass) {
+                const float v = sqrt_rn_int(min(best, maxd));
+                dt[cb + u * lstride] = v;
+                const uint32_t ov = ordf(v);
+                mn = min(mn, ov);
+                mx = max(mx, ov);
+            } else {
+                gout[cb + u * lstride] = best;
+            }
+        }
+        if (ep.final_pass) {
+            atomic_min_if(&S[bi].dt_min, mn);
+            atomic_max_if(&S[bi].dt_max, mx);
+            if (ep.axis == 1) {
+                atomic_min_if(&slice_min[B.sbase + o], mn);
+                atomic_max_if(&slice_max[B.sbase + o], mx);
+            }
+        }
+    }
+}
 
 // per-slice min / max of dt (2-D ws on a 3-D dt): one workgroup per slice chunk
 __global__ void __launch_bounds__(256) k_dt_slice_stats(const BlockDesc* __restrict__ D, const BlockStat* S,

@@ -35,7 +35,14 @@ def make_cases():
     xn = _x(seed=14).copy()
     rng = np.random.RandomState(5)
     xn[:4] = rng.rand(4, SHAPE[1], SHAPE[2]).astype(np.float32)
+    # a few boundary voxels in a large empty volume: most EDT lines are far from (or without)
+    # foreground, so the bounded search hands them to the lower-envelope pass (k_edt_col_fh)
+    xs = np.zeros((12, 160, 144), np.float32)
+    xs[3, 20, 30] = xs[3, 150, 100] = xs[9, 80, 5] = 1.0
+    xs[6, :, 70] = 1.0
     return {
+        '3d_sparse_fg': (dict(D3), dict(input=xs)),
+        '2d_sparse_fg': ({}, dict(input=xs)),
         '3d_sizefilter_all': (dict(D3, size_filter=10 ** 9), dict(input=x)),
         '2d_sizefilter_all': (dict(size_filter=10 ** 9), dict(input=x)),
         '2d_sizefilter_noise_slices': (dict(size_filter=200), dict(input=xn)),

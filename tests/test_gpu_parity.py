@@ -22,8 +22,10 @@ ARE_TOL = 1e-3
 # reproduces.  There the GPU must equal the flood model exactly (test_flood_matches_model_
 # exactly), the whole VI gap must be the model's tie order (VI(GPU, heap) == VI(model, heap)),
 # and the gap stays below the recorded synthetic worst case.  Every BASELINE
-# config meets the VI bar itself (tests/test_config_blocks.py).
-TIE_DOMINATED = {'3d_plateaus': 1.2}
+# config meets the VI bar itself (tests/test_config_blocks.py).  The sparse-foreground cases
+# are tie-dominated too: a distance transform of a few isolated points has exactly equal
+# values on every symmetric position.
+TIE_DOMINATED = {'3d_plateaus': 1.2, '2d_sparse_fg': 0.1, '3d_sparse_fg': 0.2}
 
 
 def _oracle_seeds(config, dt):
