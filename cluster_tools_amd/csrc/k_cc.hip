@@ -58,27 +58,37 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
     uint8_t* __restrict__ cl = cls + B.base;
     uint32_t nplat = 0;
     const float NEG = -__builtin_huge_valf();
+    const gptr_t<float> gp = gbl(p);
     ROW_TILES(Z, Y, X, {
-        const float c = p[i];
+        // neighbour loads at clamped positions (unconditional: all in flight together), the
+        // positions outside the block selected away
+        const float c = gp[i];
         float w[8];
+        const bool yl = y > 0, yh = y + 1 < Y, xl = x > 0, xh = x + 1 < X;
+        const int64_t dym = yl ? X : 0, dyp = yh ? X : 0;
+        const int64_t dxm = xl ? 1 : 0, dxp = xh ? 1 : 0;
         if (B.nd_ws == 3) {
-            w[0] = z > 0 ? p[i - YX] : NEG;
-            w[1] = z + 1 < Z ? p[i + YX] : NEG;
-            w[2] = y > 0 ? p[i - X] : NEG;
-            w[3] = y + 1 < Y ? p[i + X] : NEG;
-            w[4] = x > 0 ? p[i - 1] : NEG;
-            w[5] = x + 1 < X ? p[i + 1] : NEG;
+            const bool zl = z > 0, zh = z + 1 < Z;
+            const float a0 = gp[i - (zl ? YX : 0)], a1 = gp[i + (zh ? YX : 0)];
+            const float a2 = gp[i - dym], a3 = gp[i + dyp], a4 = gp[i - dxm], a5 = gp[i + dxp];
+            w[0] = zl ? a0 : NEG;
+            w[1] = zh ? a1 : NEG;
+            w[2] = yl ? a2 : NEG;
+            w[3] = yh ? a3 : NEG;
+            w[4] = xl ? a4 : NEG;
+            w[5] = xh ? a5 : NEG;
             w[6] = w[7] = NEG;
         } else {
-            const bool yl = y > 0, yh = y + 1 < Y, xl = x > 0, xh = x + 1 < X;
-            w[0] = yl && xl ? p[i - X - 1] : NEG;
-            w[1] = yl ? p[i - X] : NEG;
-            w[2] = yl && xh ? p[i - X + 1] : NEG;
-            w[3] = xl ? p[i - 1] : NEG;
-            w[4] = xh ? p[i + 1] : NEG;
-            w[5] = yh && xl ? p[i + X - 1] : NEG;
-            w[6] = yh ? p[i + X] : NEG;
-            w[7] = yh && xh ? p[i + X + 1] : NEG;
+            const float a0 = gp[i - dym - dxm], a1 = gp[i - dym], a2 = gp[i - dym + dxp], a3 = gp[i - dxm];
+            const float a4 = gp[i + dxp], a5 = gp[i + dyp - dxm], a6 = gp[i + dyp], a7 = gp[i + dyp + dxp];
+            w[0] = yl && xl ? a0 : NEG;
+            w[1] = yl ? a1 : NEG;
+            w[2] = yl && xh ? a2 : NEG;
+            w[3] = xl ? a3 : NEG;
+            w[4] = xh ? a4 : NEG;
+            w[5] = yh && xl ? a5 : NEG;
+            w[6] = yh ? a6 : NEG;
+            w[7] = yh && xh ? a7 : NEG;
         }
         bool gt = false, eq = false;
         _Pragma("unroll") for (int k = 0; k < 8; ++k) {

@@ -584,31 +584,47 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     const float* hb = h + B.base;
     constexpr int PER = TN / 256;  // voxels per thread: c = threadIdx.x + k * 256
     static_assert(TN % 256 == 0 && PER <= 32, "");
-    // seed flags of the thread's voxels: all loads issued before the first use
+    // seed entries of the thread's voxels (cc parent or lab), then the halo heights: every load
+    // unconditional (clamped index, global address space) so that all of them are in flight
+    // together; out-of-block values are selected away afterwards
+    const uint32_t* sdsrc = cc ? cc : lab;
     uint32_t inm = 0, seedm = 0;
-    {
-        bool sd[PER];
+    uint32_t sv[PER];
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int c = threadIdx.x + k * 256;
-            const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-            const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
-            const bool in = gz < B.Z && gy < B.Y && gx < B.X;
-            inm |= (in ? 1u : 0u) << k;
-            sd[k] = in && is_seed(lab, cc, B.base + gz * YX + (int64_t)gy * B.X + gx);
-        }
-#pragma unroll
-        for (int k = 0; k < PER; ++k) seedm |= (sd[k] ? 1u : 0u) << k;
+    for (int k = 0; k < PER; ++k) {
+        const int c = threadIdx.x + k * 256;
+        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+        const int gz = min(z0 + lz, B.Z - 1), gy = min(y0 + ly, B.Y - 1), gx = min(x0 + lx, B.X - 1);
+        inm |= ((z0 + lz < B.Z && y0 + ly < B.Y && x0 + lx < B.X) ? 1u : 0u) << k;
+        sv[k] = gbl(sdsrc)[B.base + gz * YX + (int64_t)gy * B.X + gx];
     }
-    staged_loop<8>(
-        (int)threadIdx.x, HN, 256,
-        [&](int c) -> uint32_t {
+    {
+        constexpr int NH = (HN + 255) / 256;
+        uint32_t hv[NH];
+#pragma unroll
+        for (int k = 0; k < NH; ++k) {
+            const int c = min((int)threadIdx.x + k * 256, HN - 1);
             const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
             const int gz = z0 + hz - ZOFF, gy = y0 + hy - 1, gx = x0 + hx - 1;
-            if (gz < 0 || gz >= B.Z || gy < 0 || gy >= B.Y || gx < 0 || gx >= B.X) return 0xFFFFFFFFu;
-            return ordf(hb[gz * YX + (int64_t)gy * B.X + gx]);
-        },
-        [&](int c, uint32_t v) { sh[c] = v; });
+            const int cz = min(max(gz, 0), B.Z - 1), cy = min(max(gy, 0), B.Y - 1), cx = min(max(gx, 0), B.X - 1);
+            hv[k] = __float_as_uint(gbl(hb)[cz * YX + (int64_t)cy * B.X + cx]);
+        }
+#pragma unroll
+        for (int k = 0; k < NH; ++k) {
+            const int c = (int)threadIdx.x + k * 256;
+            if (c < HN) {
+                const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
+                const int gz = z0 + hz - ZOFF, gy = y0 + hy - 1, gx = x0 + hx - 1;
+                const bool out = gz < 0 || gz >= B.Z || gy < 0 || gy >= B.Y || gx < 0 || gx >= B.X;
+                sh[c] = out ? 0xFFFFFFFFu : ordf(__uint_as_float(hv[k]));
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const bool sd = cc ? sv[k] != kNoParent : (sv[k] & kFixedBit) != 0u;
+        seedm |= (((inm >> k) & 1u) && sd ? 1u : 0u) << k;
+    }
     __syncthreads();
     // parents
 #pragma unroll
@@ -665,21 +681,26 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
         if (!__syncthreads_or(moved)) break;
     }
     // tile roots: seed label (seeds) or 0 (local minima without a seed, ties), kept in sh[]
-    // (the heights are no longer read)
+    // (the heights are no longer read).  The label comes from the seed entry loaded above: a
+    // cc root carries it, a non-root cc entry needs its root's (one more load, unconditional)
     {
         uint32_t rl[PER];
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int c = threadIdx.x + k * 256;
-            const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-            rl[k] = 0u;
-            if ((seedm >> k) & 1u)
-                rl[k] = seed_label(lab, cc, B.base, (uint32_t)((z0 + lz) * YX + (int64_t)(y0 + ly) * B.X + x0 + lx));
+            const uint32_t v = sv[k];
+            const bool need = cc && v != kNoParent && !(v & kRootBit) && ((seedm >> k) & 1u);
+            rl[k] = gbl(cc ? cc : lab)[B.base + (need ? v : 0u)];
         }
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int c = threadIdx.x + k * 256;
-            if (sp[c] == c) sh[c] = rl[k];
+            const uint32_t v = sv[k];
+            uint32_t l = 0u;
+            if ((seedm >> k) & 1u) {
+                if (!cc) l = v & ~kFixedBit;
+                else l = (v & kRootBit) ? (v & ~kRootBit) : (rl[k] & ~kRootBit);
+            }
+            if (sp[c] == c) sh[c] = l;
         }
     }
     __syncthreads();
@@ -724,9 +745,10 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
     uint32_t cnt_open = 0;  // statistics (CTWS_TRACE): voxels left to the relaxation
     // word tiles: a wave's ballot is exactly one word of the open / changed bitmaps
     WORD_TILES(B.Z, B.Y, B.X, {
-        const int64_t gi = B.base + i;
-        uint32_t e = valid ? par[gi] : kDescRes;
-        const float hv = valid ? h[gi] : 0.0f;
+        const int64_t gi = B.base + (valid ? i : 0);
+        const uint32_t e0 = gbl(par)[gi];
+        const float hv = gbl(h)[gi];
+        uint32_t e = valid ? e0 : kDescRes;
         for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
             if (e & kDescRes) break;
             e = par[B.base + e];

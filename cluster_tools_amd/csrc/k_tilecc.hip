@@ -145,14 +145,54 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         return MODE == CC_PLATEAU ? (uint32_t)c : fkey_local<TZ, TY>(lz, ly, lx);
     };
-    // load values (all loads of the thread issued before the stores)
+    // load values: every load unconditional (position clamped into the domain, global address
+    // space) so that all of a thread's loads are in flight together; non-members and positions
+    // outside the domain are selected away afterwards.  Same values as cc_value.
     uint32_t vv[PER];
+    {
+        uint64_t l0[PER];
+        uint32_t l1[PER];
+        uint32_t inm = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int c = threadIdx.x + j * 256;
-        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-        const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
-        vv[j] = (z < nz && y < ny && x < nx) ? cc_value<MODE>(B, a, plat, z, y, x) : kLNone;
+        for (int j = 0; j < PER; ++j) {
+            const int c = threadIdx.x + j * 256;
+            const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+            const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
+            inm |= ((z < nz && y < ny && x < nx) ? 1u : 0u) << j;
+            const int cz = min(z, nz - 1), cy = min(y, ny - 1), cx = min(x, nx - 1);
+            if (MODE == CC_CROP) {
+                const int64_t o = ((int64_t)(cz + B.iz0) * B.Y + (cy + B.iy0)) * B.X + (cx + B.ix0);
+                l0[j] = a.packed ? gbl(a.key)[B.base + o] : (uint64_t)gbl(a.lab)[B.base + o];
+                l1[j] = B.mask ? (uint32_t)gbl(B.mask)[o] : 1u;
+            } else {
+                const int64_t i = B.base + ((int64_t)cz * B.Y + cy) * B.X + cx;
+                l0[j] = gbl(a.cls)[i];
+                l1[j] = MODE == CC_PLATEAU ? __float_as_uint(gbl(a.v)[i]) : 0u;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            uint32_t v = kLNone;
+            if (MODE == CC_CROP) {
+                uint32_t l = a.packed ? (l0[j] == kInfKey ? 0u : (uint32_t)(l0[j] & kLabelMask))
+                                      : ((uint32_t)l0[j] & ~kFixedBit);
+                if (!l1[j]) l = 0u;  // masked
+                v = l ? l : kLNone;
+            } else if (MODE == CC_PLATEAU) {
+                v = (l0[j] & 2) ? (l1[j] == 0x80000000u ? 0u : l1[j]) : kLNone;
+            } else {
+                const uint32_t cl = (uint32_t)l0[j];
+                v = (cl & 1) ? kLNone : 1u;
+                if (!(cl & 1) && (cl & 2) && plat && ((inm >> j) & 1u)) {
+                    // a plateau voxel: maximum iff its plateau is (k_plateau_flag's bit 4)
+                    const int c = threadIdx.x + j * 256;
+                    const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+                    const int64_t i = ((int64_t)(z0 + lz) * B.Y + (y0 + ly)) * B.X + (x0 + lx);
+                    v = cc_is_max(a.cls + B.base, a.Pp + B.base, i, plat) ? 1u : kLNone;
+                }
+            }
+            vv[j] = ((inm >> j) & 1u) ? v : kLNone;
+        }
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) sv[threadIdx.x + j * 256] = vv[j];
