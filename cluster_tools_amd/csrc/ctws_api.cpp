@@ -105,7 +105,8 @@ struct ctws_handle {
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int gauss_w = 0;  // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
-    int gauss_yx = 1;  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
+    int gauss_yx = 1;
+    int words_per_wave = 32;  // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     int frontier_unroll = 1;  // CTWS_FRONTIER_UNROLL (1, 2, 4, 8): list entries per lane in flight
     int frontier_reps = 4;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch
@@ -793,7 +794,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     const dim3 rg((unsigned)std::min<int64_t>((maxRows + kRows - 1) / kRows, 16384), nb);
     const dim3 rig((unsigned)std::min<int64_t>((maxIRows + kRows - 1) / kRows, 16384), nb);
     // word-tile kernels: one wave per 64-voxel row word, kWordWaves waves per workgroup
-    const dim3 wtg((unsigned)std::min<int64_t>((maxRows * ((maxX + 63) / 64) + kWordWaves - 1) / kWordWaves, 65535), nb);
+    // (h->words_per_wave words per wave: a workgroup per handful of words would make the
+    // dispatch of ~10^6 workgroups the bottleneck)
+    const int64_t wpw = (int64_t)kWordWaves * h->words_per_wave;
+    const dim3 wtg((unsigned)std::min<int64_t>((maxRows * ((maxX + 63) / 64) + wpw - 1) / wpw, 65535), nb);
+    const dim3 wtig((unsigned)std::min<int64_t>((maxIRows * ((maxIX + 63) / 64) + wpw - 1) / wpw, 65535), nb);
     size_t ev = 0;
     std::vector<const char*> names;
     auto mark = [&](const char* name) {
@@ -1255,7 +1260,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         for (int i = 0; i < nb; ++i) any_plain |= desc[i].crop == 0;
         // uncropped blocks count their distinct ids in W (cropped blocks: n_cc of the crop CC)
         if (any_plain) HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-        k_output<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
+        k_output<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
                                              (unsigned long long*)w.W);
         if (any_plain) k_count_ids<<<dim3(64, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.W);
         LAUNCHCHK();
@@ -1472,6 +1477,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))
         h->frontier_max_iters = std::max(0, std::min(kFrontierMaxItersCap, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_GAUSS_YX")) h->gauss_yx = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_WORDS_PER_WAVE")) h->words_per_wave = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_GAUSS_W")) {
         const int v = std::atoi(t);
         h->gauss_w = (v == 8 || v == 16 || v == 32) ? v : 0;

@@ -62,15 +62,18 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
     ROW_TILES(Z, Y, X, {
         // neighbour loads at clamped positions (unconditional: all in flight together), the
         // positions outside the block selected away
-        const float c = gp[i];
+        const int64_t ic = i;
+        const int xq = x;
+        const bool valid = true;
+        const float c = gp[ic];
         float w[8];
-        const bool yl = y > 0, yh = y + 1 < Y, xl = x > 0, xh = x + 1 < X;
+        const bool yl = y > 0, yh = y + 1 < Y, xl = xq > 0, xh = xq + 1 < X;
         const int64_t dym = yl ? X : 0, dyp = yh ? X : 0;
         const int64_t dxm = xl ? 1 : 0, dxp = xh ? 1 : 0;
         if (B.nd_ws == 3) {
             const bool zl = z > 0, zh = z + 1 < Z;
-            const float a0 = gp[i - (zl ? YX : 0)], a1 = gp[i + (zh ? YX : 0)];
-            const float a2 = gp[i - dym], a3 = gp[i + dyp], a4 = gp[i - dxm], a5 = gp[i + dxp];
+            const float a0 = gp[ic - (zl ? YX : 0)], a1 = gp[ic + (zh ? YX : 0)];
+            const float a2 = gp[ic - dym], a3 = gp[ic + dyp], a4 = gp[ic - dxm], a5 = gp[ic + dxp];
             w[0] = zl ? a0 : NEG;
             w[1] = zh ? a1 : NEG;
             w[2] = yl ? a2 : NEG;
@@ -79,8 +82,8 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
             w[5] = xh ? a5 : NEG;
             w[6] = w[7] = NEG;
         } else {
-            const float a0 = gp[i - dym - dxm], a1 = gp[i - dym], a2 = gp[i - dym + dxp], a3 = gp[i - dxm];
-            const float a4 = gp[i + dxp], a5 = gp[i + dyp - dxm], a6 = gp[i + dyp], a7 = gp[i + dyp + dxp];
+            const float a0 = gp[ic - dym - dxm], a1 = gp[ic - dym], a2 = gp[ic - dym + dxp], a3 = gp[ic - dxm];
+            const float a4 = gp[ic + dxp], a5 = gp[ic + dyp - dxm], a6 = gp[ic + dyp], a7 = gp[ic + dyp + dxp];
             w[0] = yl && xl ? a0 : NEG;
             w[1] = yl ? a1 : NEG;
             w[2] = yl && xh ? a2 : NEG;
@@ -95,8 +98,8 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
             gt |= w[k] > c;
             eq |= w[k] == c;
         }
-        cl[i] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
-        nplat += eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
+        if (valid) cl[i] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
+        nplat += valid && eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
     })
     nplat = wg_reduce_u32(nplat, OpAdd());
     if (threadIdx.x == 0 && nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
@@ -277,27 +280,32 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
     const gwptr_t<uint64_t> out = gblw(B.out);
     uint32_t mx = 0;
     bool zero_in = false;  // an in-mask voxel without a label: its output is the bare id offset
-    ROW_TILES(B.IZ, B.IY, B.IX, {
-        const int64_t o = outer_of_inner(B, z, y, x);
+    // word tiles over the inner block: lanes past the row end read a clamped position and
+    // store nothing
+    WORD_TILES(B.IZ, B.IY, B.IX, {
+        const int xq = valid ? x : B.IX - 1;
+        const int64_t iq = row * B.IX + xq;
+        const int64_t o = outer_of_inner(B, z, y, xq);
         const bool inm = !B.mask || gbl(B.mask)[o];
         uint64_t v = 0;  // empty block: constant offset (watershed.py:310-321)
         if (active) {
             uint32_t l;
             if (B.crop) {
-                const uint32_t p = P[i];
+                const uint32_t p = gbl(P)[iq];
                 l = p == kNoParent ? 0u : cc_label(P, p);
             } else {
-                l = flood_label(lab, key, packed, B.base + o);
+                l = packed ? (uint32_t)(gbl(key)[B.base + o] & kLabelMask) : (gbl(lab)[B.base + o] & ~kFixedBit);
+                if (packed && gbl(key)[B.base + o] == kInfKey) l = 0u;
                 if (!inm) l = 0;
                 else if (B.nd_ws == 2) l = (l - sb[B.sbase + z + B.iz0]) + soff[B.sbase + z + B.iz0];
             }
-            mx = max(mx, l);
+            if (valid) mx = max(mx, l);
             v = l;
         }
-        out[i] = inm ? v + B.id_offset : v;
-        zero_in |= active && inm && v == 0;
+        if (valid) out[i] = inm ? v + B.id_offset : v;
+        zero_in |= valid && active && inm && v == 0;
         if (active && !B.crop) {
-            const uint32_t l = (uint32_t)v;
+            const uint32_t l = valid ? (uint32_t)v : 0u;
             // only the first lane of each run of equal labels along the wave marks it, and it
             // reads the bit before the atomic: the few words of a block's labels are read by
             // every wave of the block, so same-address traffic is kept to a few lanes per wave
@@ -335,7 +343,7 @@ __global__ void __launch_bounds__(256) k_flatten_roots(const BlockDesc* __restri
     uint64_t* W = Wg + B.wbase;
     const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
     ROW_TILES(nz, ny, nx, {
-        const uint32_t p = P[i];
+        const uint32_t p = gbl(P)[i];
         if (p == (uint32_t)i) {
             const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
             atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));

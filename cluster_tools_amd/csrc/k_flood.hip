@@ -869,30 +869,50 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
         uint32_t* gn = gnext + (B.fbase >> 6);
         uint32_t* qg = qgen + (B.fbase >> 6);
         const int64_t nchunks = (nwords + 63) >> 6;
-        // word w of the previous changed bitmap (0 unless its chunk changed in iteration it - 1)
-        auto cw = [&](int64_t w) -> uint64_t { return gp[w >> 6] == prev_gen ? cp[w] : 0ull; };
+        // word w of the previous changed bitmap (0 unless its chunk changed in iteration it - 1).
+        // All generation and word loads are unconditional (clamped word index, global address
+        // space) and issued together; the neighbours outside the block are selected away.
         const int64_t w0 = ch0 * 64;
         const int64_t wl = w0 + lane;
-        uint64_t f = 0ull;
-        int row = 0, xw = 0;
-        if (wl < nwords) {
-            row = (int)(wl / wpr);
-            xw = (int)(wl - (int64_t)row * wpr);
-            const int z = row / B.Y, y = row - z * B.Y;
-            const uint64_t c = cw(wl);
-            f = (c << 1) | (c >> 1);
-            if (xw > 0) f |= cw(wl - 1) >> 63;
-            if (xw + 1 < wpr) f |= cw(wl + 1) << 63;
-            if (y > 0) f |= cw(wl - wpr);
-            if (y + 1 < B.Y) f |= cw(wl + wpr);
-            if (ND == 3) {
-                if (z > 0) f |= cw(wl - ws);
-                if (z + 1 < B.Z) f |= cw(wl + ws);
-            }
-            f &= op[wl];  // open voxels only (their x < X)
+        const bool wok = wl < nwords;
+        const int64_t wc = wok ? wl : nwords - 1;
+        const int row = (int)(wc / wpr);
+        const int xw = (int)(wc - (int64_t)row * wpr);
+        const int zz = row / B.Y, yy = row - zz * B.Y;
+        constexpr int NW = ND == 3 ? 7 : 5;
+        int64_t wi[NW];
+        bool ok[NW];
+        wi[0] = wc;
+        ok[0] = wok;
+        wi[1] = wc - 1;
+        ok[1] = wok && xw > 0;
+        wi[2] = wc + 1;
+        ok[2] = wok && xw + 1 < wpr;
+        wi[3] = wc - wpr;
+        ok[3] = wok && yy > 0;
+        wi[4] = wc + wpr;
+        ok[4] = wok && yy + 1 < B.Y;
+        if (ND == 3) {
+            wi[5] = wc - ws;
+            ok[5] = wok && zz > 0;
+            wi[6] = wc + ws;
+            ok[6] = wok && zz + 1 < B.Z;
         }
-        const uint64_t opw = wl < nwords ? op[wl] : 0ull;
-        const int z0 = row / B.Y, y0 = row - z0 * B.Y;
+        uint32_t gv[NW];
+        uint64_t cv[NW];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int64_t w = ok[k] ? wi[k] : wc;
+            gv[k] = gbl(gp)[w >> 6];
+            cv[k] = gbl(cp)[w];
+        }
+        const uint64_t opw = wok ? gbl(op)[wc] : 0ull;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) cv[k] = (ok[k] && gv[k] == prev_gen) ? cv[k] : 0ull;
+        uint64_t f = (cv[0] << 1) | (cv[0] >> 1) | (cv[1] >> 63) | (cv[2] << 63) | cv[3] | cv[4];
+        if (ND == 3) f |= cv[5] | cv[6];
+        f &= opw;  // open voxels only (their x < X)
+        const int y0 = yy;
         uint64_t acc = 0ull;  // changed bits of this word over all local sweeps
         for (int rep = 0;; ++rep) {
             // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list
