@@ -560,6 +560,12 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     while (fiters < h->frontier_max_iters && !converged) {
         const int it0 = fiters;
         const int nl = std::min(kFrontierBatch, h->frontier_max_iters - it0);
+        std::vector<hipEvent_t> tev;
+        if (h->trace) {
+            tev.resize(nl + 1);
+            for (auto& e : tev) hipEventCreate(&e);
+            hipEventRecord(tev[0], h->stream);
+        }
         for (int k = 0; k < nl; ++k) {
             const int it = it0 + k;
 #define CTWS_FRONTIER(ND, U)                                                                                       \
@@ -578,11 +584,22 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
                 else CTWS_FRONTIER(2, 1);
             }
 #undef CTWS_FRONTIER
+            if (h->trace) hipEventRecord(tev[k + 1], h->stream);
         }
         LAUNCHCHK();
-        HIPCHK(hipMemcpyAsync(h->h_counter, w.wlcnt + it0 + 1, sizeof(uint32_t) * nl, hipMemcpyDeviceToHost,
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.wlcnt + it0, sizeof(uint32_t) * (nl + 1), hipMemcpyDeviceToHost,
                               h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
+        if (h->trace) {
+            for (int k = 0; k < nl; ++k) {
+                float ms = 0.f;
+                hipEventElapsedTime(&ms, tev[k], tev[k + 1]);
+                std::fprintf(stderr, "[ctws] frontier it %d: %u chunks, %.3f ms\n", it0 + k, h->h_counter[k], ms);
+                if (!h->h_counter[k + 1]) break;
+            }
+            for (auto& e : tev) hipEventDestroy(e);
+        }
+        std::memmove(h->h_counter, h->h_counter + 1, sizeof(uint32_t) * nl);
         for (int k = 0; k < nl; ++k) {
             ++fiters;
             if (!h->h_counter[k]) {  // nothing queued for the next iteration
@@ -694,7 +711,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
                             (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
         d.fbase = TF;
-        TF += ((int64_t)d.Z * d.Y * ((d.X + 63) / 64) + 63) & ~(int64_t)63;  // chunk aligned
+        // frontier bitmaps: rows padded to a multiple of 64, so that the block's chunks (64 rows
+        // x one word column, k_frontier) are exactly its words / 64
+        TF += (((int64_t)d.Z * d.Y + 63) / 64) * 64 * ((d.X + 63) / 64);
         T += d.N;
         TI += d.NI;
         TW += words_of(d.N);

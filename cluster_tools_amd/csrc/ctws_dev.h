@@ -274,6 +274,9 @@ __device__ __forceinline__ uint32_t flood_label(const uint32_t* lab, const uint6
 __device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
     return (uint64_t)__shfl_up((long long)v, d);
 }
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    return (uint64_t)__shfl((long long)v, src);
+}
 __device__ __forceinline__ uint64_t shfl_down_u64(uint64_t v, int d) {
     return (uint64_t)__shfl_down((long long)v, d);
 }
