@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -92,6 +93,16 @@ struct ctws_handle {
     uint64_t flood_tiles = 0, flood_iters = 0, flood_lines = 0;
     // host-pointer staging
     DevBuf st_in, st_mask, st_init, st_out;
+    // host-pointer path: two slots of pinned host staging + device staging, copy streams
+    struct HostSlot {
+        void* pin_in = nullptr;  // inputs | masks | initial seeds of a batch, packed
+        size_t pin_in_bytes = 0;
+        void* pin_out = nullptr;  // uint64 outputs of a batch
+        size_t pin_out_bytes = 0;
+        DevBuf d_in, d_out;
+        hipEvent_t ev_h2d = nullptr, ev_comp = nullptr, ev_d2h = nullptr;
+    } hslot[2];
+    hipStream_t s_in = nullptr, s_out = nullptr;
     // relabel (k_relabel.hip)
     DevBuf rl_lab, rl_bits, rl_cnt, rl_offs, rl_out, rl_keys, rl_vals, rl_red;
     int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
@@ -109,7 +120,7 @@ struct ctws_handle {
     int words_per_wave = 32;  // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     int frontier_unroll = 1;  // CTWS_FRONTIER_UNROLL (1, 2, 4, 8): list entries per lane in flight
-    int frontier_reps = 4;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch
+    int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
     // RCCL
@@ -1356,6 +1367,228 @@ int64_t batch_voxels_budget() {
     return 512ll << 20;  // ~26 GB of workspace at ~50 B per voxel
 }
 
+// ---- host-pointer path: pinned staging, copies overlapped with the compute -----------------
+// Batch j uses slot j & 1.  A worker thread packs batch j + 1's inputs into the slot's pinned
+// buffer and starts its host-to-device copy on s_in while the calling thread runs batch j on
+// the library stream; batch j's outputs go device-to-host on s_out and another worker unpacks
+// them into the callers' arrays while batch j + 1 computes.  Events order every reuse of a slot.
+void par_memcpy(const std::vector<std::pair<void*, const void*>>& dst_src, const std::vector<size_t>& sizes) {
+    size_t total = 0;
+    for (size_t v : sizes) total += v;
+    const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    if (total < (64u << 20) || nt == 1) {
+        for (size_t i = 0; i < sizes.size(); ++i) std::memcpy(dst_src[i].first, dst_src[i].second, sizes[i]);
+        return;
+    }
+    // split the byte range of the concatenated copies evenly over the threads
+    std::vector<std::thread> th;
+    const size_t per = (total + nt - 1) / nt;
+    for (unsigned t = 0; t < nt; ++t) {
+        const size_t b0 = t * per, b1 = std::min(total, b0 + per);
+        if (b0 >= b1) break;
+        th.emplace_back([&, b0, b1]() {
+            size_t off = 0;
+            for (size_t i = 0; i < sizes.size(); ++i) {
+                const size_t s0 = std::max(off, b0), s1 = std::min(off + sizes[i], b1);
+                if (s0 < s1)
+                    std::memcpy((char*)dst_src[i].first + (s0 - off), (const char*)dst_src[i].second + (s0 - off), s1 - s0);
+                off += sizes[i];
+                if (off >= b1) break;
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+}
+
+int grow_pinned(ctws_handle* h, void*& p, size_t& have, size_t bytes) {
+    if (have >= bytes) return CTWS_OK;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    have = 0;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 256), hipHostMallocDefault) != hipSuccess) {
+        h->err = "hipHostMalloc staging failed (" + std::to_string(bytes) + " bytes)";
+        return CTWS_ENOMEM;
+    }
+    have = bytes;
+    return CTWS_OK;
+}
+
+struct HostBatch {
+    int k, nb;  // blocks todo[k .. k + nb)
+    std::vector<size_t> in_off, in_sz, m_off, i_off, o_off, o_sz;
+    size_t in_bytes = 0, out_bytes = 0;
+};
+
+int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* blocks,
+                    const std::vector<int>& todo) {
+    int r;
+    const int64_t budget = batch_voxels_budget();
+    // batches and their packed layouts (inputs, masks and initial seeds in one buffer)
+    std::vector<HostBatch> hb;
+    size_t max_in = 0, max_out = 0;
+    for (size_t k = 0; k < todo.size();) {
+        size_t e = k;
+        int64_t vox = 0;
+        while (e < todo.size()) {
+            const ctws_block& b = blocks[todo[e]];
+            const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
+            if (e > k && (vox + nv > budget || e - k >= 4096)) break;
+            vox += nv;
+            ++e;
+        }
+        HostBatch B;
+        B.k = (int)k;
+        B.nb = (int)(e - k);
+        auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+        for (int i = 0; i < B.nb; ++i) {
+            const ctws_block& b = blocks[todo[k + i]];
+            const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
+            const size_t es = b.input_dtype == CTWS_U8 ? 1 : (b.input_dtype == CTWS_U16 ? 2 : (b.input_dtype == CTWS_F32 ? 4 : 8));
+            B.in_sz.push_back((size_t)nv * es * (size_t)std::max(1, b.n_channels));
+            B.in_off.push_back(B.in_bytes);
+            B.in_bytes += al(B.in_sz.back());
+            B.m_off.push_back(b.mask ? B.in_bytes : 0);
+            if (b.mask) B.in_bytes += al((size_t)nv);
+            B.i_off.push_back(b.initial_seeds ? B.in_bytes : 0);
+            if (b.initial_seeds) B.in_bytes += al((size_t)nv * 8);
+            B.o_sz.push_back((size_t)(b.inner_shape[0] * b.inner_shape[1] * b.inner_shape[2]) * 8);
+            B.o_off.push_back(B.out_bytes);
+            B.out_bytes += al(B.o_sz.back());
+        }
+        max_in = std::max(max_in, B.in_bytes);
+        max_out = std::max(max_out, B.out_bytes);
+        hb.push_back(std::move(B));
+        k = e;
+    }
+    if (hb.empty()) return CTWS_OK;
+    if (!h->s_in) {
+        HIPCHK(hipStreamCreateWithFlags(&h->s_in, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&h->s_out, hipStreamNonBlocking));
+        for (auto& sl : h->hslot) {
+            HIPCHK(hipEventCreateWithFlags(&sl.ev_h2d, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&sl.ev_comp, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&sl.ev_d2h, hipEventDisableTiming));
+        }
+    }
+    const int nslots = hb.size() > 1 ? 2 : 1;
+    for (int s = 0; s < nslots; ++s) {
+        auto& sl = h->hslot[s];
+        if ((r = grow_pinned(h, sl.pin_in, sl.pin_in_bytes, max_in)) != CTWS_OK) return r;
+        if ((r = grow_pinned(h, sl.pin_out, sl.pin_out_bytes, max_out)) != CTWS_OK) return r;
+        if ((r = grow(h, sl.d_in, max_in)) != CTWS_OK) return r;
+        if ((r = grow(h, sl.d_out, max_out)) != CTWS_OK) return r;
+        // a fresh handle's events have never been recorded: mark the slots free
+        HIPCHK(hipEventRecord(sl.ev_d2h, h->s_out));
+        HIPCHK(hipEventRecord(sl.ev_comp, h->stream));
+    }
+    // pack batch j's inputs into its slot and start the upload (worker thread)
+    auto stage_in = [&](int j) -> int {
+        const HostBatch& B = hb[j];
+        auto& sl = h->hslot[j % nslots];
+        std::vector<std::pair<void*, const void*>> ds;
+        std::vector<size_t> sz;
+        for (int i = 0; i < B.nb; ++i) {
+            const ctws_block& b = blocks[todo[B.k + i]];
+            const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
+            ds.push_back({(char*)sl.pin_in + B.in_off[i], b.input});
+            sz.push_back(B.in_sz[i]);
+            if (b.mask) {
+                ds.push_back({(char*)sl.pin_in + B.m_off[i], b.mask});
+                sz.push_back((size_t)nv);
+            }
+            if (b.initial_seeds) {
+                ds.push_back({(char*)sl.pin_in + B.i_off[i], b.initial_seeds});
+                sz.push_back((size_t)nv * 8);
+            }
+        }
+        // the slot's previous upload has been consumed once its batch computed
+        if (hipEventSynchronize(sl.ev_h2d) != hipSuccess) return CTWS_EHIP;
+        par_memcpy(ds, sz);
+        if (hipStreamWaitEvent(h->s_in, sl.ev_comp, 0) != hipSuccess ||
+            hipMemcpyAsync(sl.d_in.p, sl.pin_in, B.in_bytes, hipMemcpyHostToDevice, h->s_in) != hipSuccess ||
+            hipEventRecord(sl.ev_h2d, h->s_in) != hipSuccess)
+            return CTWS_EHIP;
+        return CTWS_OK;
+    };
+    // unpack batch j's outputs into the callers' arrays once downloaded (worker thread)
+    auto drain_out = [&](int j, std::vector<ctws_block>* bbp) -> int {
+        const HostBatch& B = hb[j];
+        auto& sl = h->hslot[j % nslots];
+        if (hipEventSynchronize(sl.ev_d2h) != hipSuccess) return CTWS_EHIP;
+        std::vector<std::pair<void*, const void*>> ds;
+        std::vector<size_t> sz;
+        for (int i = 0; i < B.nb; ++i) {
+            if ((*bbp)[i].status == CTWS_BLOCK_EMPTY_PASS2) continue;  // nothing written (:240-242)
+            ds.push_back({blocks[todo[B.k + i]].output, (char*)sl.pin_out + B.o_off[i]});
+            sz.push_back(B.o_sz[i]);
+        }
+        par_memcpy(ds, sz);
+        return CTWS_OK;
+    };
+    for (auto& sl : h->hslot) HIPCHK(hipEventRecord(sl.ev_h2d, h->s_in));
+    int rin = stage_in(0);
+    if (rin != CTWS_OK) return rin;
+    std::vector<std::vector<ctws_block>> bbs(hb.size());
+    std::thread t_in, t_out;
+    int r_in = CTWS_OK, r_out = CTWS_OK;
+    auto join_all = [&]() {
+        if (t_in.joinable()) t_in.join();
+        if (t_out.joinable()) t_out.join();
+    };
+    for (size_t j = 0; j < hb.size(); ++j) {
+        const HostBatch& B = hb[j];
+        auto& sl = h->hslot[j % nslots];
+        if (j + 1 < hb.size()) t_in = std::thread([&, j]() { r_in = stage_in((int)j + 1); });
+        std::vector<ctws_block>& bb = bbs[j];
+        bb.resize(B.nb);
+        std::vector<BlockIO> io(B.nb);
+        for (int i = 0; i < B.nb; ++i) {
+            bb[i] = blocks[todo[B.k + i]];
+            const ctws_block& b = bb[i];
+            io[i].in = (char*)sl.d_in.p + B.in_off[i];
+            io[i].mask = b.mask ? (const uint8_t*)((char*)sl.d_in.p + B.m_off[i]) : nullptr;
+            io[i].init = b.initial_seeds ? (const uint64_t*)((char*)sl.d_in.p + B.i_off[i]) : nullptr;
+            io[i].out = (uint64_t*)((char*)sl.d_out.p + B.o_off[i]);
+        }
+        // inputs uploaded; the slot's previous outputs downloaded
+        if (hipStreamWaitEvent(h->stream, sl.ev_h2d, 0) != hipSuccess ||
+            hipStreamWaitEvent(h->stream, sl.ev_d2h, 0) != hipSuccess) {
+            join_all();
+            return CTWS_EHIP;
+        }
+        if ((r = run_batch(h, cfg, pl, bb.data(), io.data(), B.nb)) != CTWS_OK) {
+            join_all();
+            return r;
+        }
+        HIPCHK(hipEventRecord(sl.ev_comp, h->stream));
+        // the slot's pinned outputs are free once the drain of batch j - 2 finished
+        if (t_out.joinable()) t_out.join();
+        if (r_out != CTWS_OK) {
+            join_all();
+            return r_out;
+        }
+        if (hipStreamWaitEvent(h->s_out, sl.ev_comp, 0) != hipSuccess ||
+            hipMemcpyAsync(sl.pin_out, sl.d_out.p, B.out_bytes, hipMemcpyDeviceToHost, h->s_out) != hipSuccess ||
+            hipEventRecord(sl.ev_d2h, h->s_out) != hipSuccess) {
+            join_all();
+            return CTWS_EHIP;
+        }
+        t_out = std::thread([&, j]() { r_out = drain_out((int)j, &bbs[j]); });
+        if (t_in.joinable()) t_in.join();
+        if (r_in != CTWS_OK) {
+            join_all();
+            return r_in;
+        }
+        for (int i = 0; i < B.nb; ++i) {
+            blocks[todo[B.k + i]].status = bb[i].status;
+            blocks[todo[B.k + i]].n_ids = bb[i].n_ids;
+            blocks[todo[B.k + i]].max_label = bb[i].max_label;
+        }
+    }
+    join_all();
+    return r_out;
+}
+
 int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, bool device_ptrs) {
     if (!h || !cfg || (!blocks && n > 0) || n < 0) return CTWS_EINVAL;
     h->err.clear();
@@ -1392,6 +1625,7 @@ int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, b
         }
         todo.push_back(i);
     }
+    if (!device_ptrs) return run_blocks_host(h, cfg, pl, blocks, todo);
     const int64_t budget = batch_voxels_budget();
     size_t k = 0;
     while (k < todo.size()) {
@@ -1414,54 +1648,7 @@ int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, b
                 io[i] = {bb[i].input, bb[i].mask, bb[i].initial_seeds, bb[i].output};
             if ((r = run_batch(h, cfg, pl, bb.data(), io.data(), nb)) != CTWS_OK) return r;
         } else {
-            // stage host buffers through device memory
-            size_t in_bytes = 0, m_bytes = 0, i_bytes = 0, o_bytes = 0;
-            std::vector<size_t> in_off(nb), m_off(nb), i_off(nb), o_off(nb), in_sz(nb);
-            for (int i = 0; i < nb; ++i) {
-                const ctws_block& b = bb[i];
-                const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
-                const size_t es = b.input_dtype == CTWS_U8 ? 1 : (b.input_dtype == CTWS_U16 ? 2 : (b.input_dtype == CTWS_F32 ? 4 : 8));
-                in_sz[i] = (size_t)nv * es * (size_t)std::max(1, b.n_channels);
-                in_off[i] = in_bytes;
-                in_bytes += (in_sz[i] + 255) & ~(size_t)255;
-                m_off[i] = m_bytes;
-                if (b.mask) m_bytes += ((size_t)nv + 255) & ~(size_t)255;
-                i_off[i] = i_bytes;
-                if (b.initial_seeds) i_bytes += (size_t)nv * 8;
-                o_off[i] = o_bytes;
-                o_bytes += (size_t)(b.inner_shape[0] * b.inner_shape[1] * b.inner_shape[2]) * 8;
-            }
-            if ((r = grow(h, h->st_in, in_bytes)) != CTWS_OK) return r;
-            if ((r = grow(h, h->st_mask, m_bytes)) != CTWS_OK) return r;
-            if ((r = grow(h, h->st_init, i_bytes)) != CTWS_OK) return r;
-            if ((r = grow(h, h->st_out, o_bytes)) != CTWS_OK) return r;
-            for (int i = 0; i < nb; ++i) {
-                const ctws_block& b = bb[i];
-                const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
-                char* din = (char*)h->st_in.p + in_off[i];
-                HIPCHK(hipMemcpyAsync(din, b.input, in_sz[i], hipMemcpyHostToDevice, h->stream));
-                io[i].in = din;
-                io[i].mask = nullptr;
-                if (b.mask) {
-                    uint8_t* dm = (uint8_t*)h->st_mask.p + m_off[i];
-                    HIPCHK(hipMemcpyAsync(dm, b.mask, (size_t)nv, hipMemcpyHostToDevice, h->stream));
-                    io[i].mask = dm;
-                }
-                io[i].init = nullptr;
-                if (b.initial_seeds) {
-                    uint64_t* di = (uint64_t*)((char*)h->st_init.p + i_off[i]);
-                    HIPCHK(hipMemcpyAsync(di, b.initial_seeds, (size_t)nv * 8, hipMemcpyHostToDevice, h->stream));
-                    io[i].init = di;
-                }
-                io[i].out = (uint64_t*)((char*)h->st_out.p + o_off[i]);
-            }
             if ((r = run_batch(h, cfg, pl, bb.data(), io.data(), nb)) != CTWS_OK) return r;
-            for (int i = 0; i < nb; ++i) {
-                if (bb[i].status == CTWS_BLOCK_EMPTY_PASS2) continue;  // nothing written (:240-242)
-                const size_t ob = (size_t)(bb[i].inner_shape[0] * bb[i].inner_shape[1] * bb[i].inner_shape[2]) * 8;
-                HIPCHK(hipMemcpyAsync(bb[i].output, io[i].out, ob, hipMemcpyDeviceToHost, h->stream));
-            }
-            HIPCHK(hipStreamSynchronize(h->stream));
         }
         for (int i = 0; i < nb; ++i) {
             blocks[todo[k + i]].status = bb[i].status;
@@ -1535,6 +1722,16 @@ void ctws_close(ctws_handle* h) {
         if (e) hipEventDestroy(e);
     if (h->h_counter) hipHostFree(h->h_counter);
     if (h->h_taps) hipHostFree(h->h_taps);
+    for (auto& sl : h->hslot) {
+        if (sl.pin_in) hipHostFree(sl.pin_in);
+        if (sl.pin_out) hipHostFree(sl.pin_out);
+        if (sl.d_in.p) hipFree(sl.d_in.p);
+        if (sl.d_out.p) hipFree(sl.d_out.p);
+        for (hipEvent_t e : {sl.ev_h2d, sl.ev_comp, sl.ev_d2h})
+            if (e) hipEventDestroy(e);
+    }
+    if (h->s_in) hipStreamDestroy(h->s_in);
+    if (h->s_out) hipStreamDestroy(h->s_out);
     if (h->comm) ncclCommDestroy(h->comm);
     hipStreamDestroy(h->stream);
     delete h;

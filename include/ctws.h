@@ -134,7 +134,11 @@ const char* ctws_last_error(const ctws_handle* h);
 
 /*
  * Run the watershed of `n_blocks` blocks.  input/mask/initial_seeds/output are HOST
- * pointers; the library stages them through pinned buffers and HBM.
+ * pointers.  The blocks run in device-memory-sized batches; each batch's inputs are packed
+ * (multi-threaded memcpy) into one of two pinned host buffers and uploaded on a copy stream
+ * while the previous batch computes, and its outputs are downloaded on a second copy stream
+ * and unpacked while the next batch computes.  The pinned and device staging buffers are kept
+ * by the handle (grow-only) for later calls.
  */
 int ctws_ws_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks);
 
