@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <type_traits>
 #include <cmath>
 #include <cstdint>
@@ -101,6 +102,7 @@ struct ctws_handle {
         size_t pin_out_bytes = 0;
         DevBuf d_in, d_out;
         hipEvent_t ev_h2d = nullptr, ev_comp = nullptr, ev_d2h = nullptr;
+        std::vector<hipEvent_t> ev_blk;  // per block of the batch: its output downloaded
     } hslot[2];
     hipStream_t s_in = nullptr, s_out = nullptr;
     // relabel (k_relabel.hip)
@@ -117,7 +119,11 @@ struct ctws_handle {
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int gauss_w = 0;  // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;
-    int words_per_wave = 32;  // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
+    int words_per_wave = 32;
+    int d2h_wgs = 32;
+    int host_threads = 8;
+    int host_batch_blocks = 0;  // CTWS_HOST_BATCH_BLOCKS: cap on blocks per host-path batch (0: voxel cap)
+    int64_t host_batch_voxels = (int64_t)256 << 20;  // CTWS_HOST_BATCH_VOXELS: smaller batches pipeline better  // CTWS_HOST_THREADS: memcpy threads per direction of the host path  // CTWS_D2H_WGS: workgroups of the device-to-host copy kernel (0: hipMemcpyAsync)  // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     int frontier_unroll = 1;  // CTWS_FRONTIER_UNROLL (1, 2, 4, 8): list entries per lane in flight
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
@@ -1372,10 +1378,12 @@ int64_t batch_voxels_budget() {
 // buffer and starts its host-to-device copy on s_in while the calling thread runs batch j on
 // the library stream; batch j's outputs go device-to-host on s_out and another worker unpacks
 // them into the callers' arrays while batch j + 1 computes.  Events order every reuse of a slot.
-void par_memcpy(const std::vector<std::pair<void*, const void*>>& dst_src, const std::vector<size_t>& sizes) {
+// (few threads: the calling thread's host round trips inside run_batch must not wait for a core)
+void par_memcpy(const std::vector<std::pair<void*, const void*>>& dst_src, const std::vector<size_t>& sizes,
+                unsigned max_threads) {
     size_t total = 0;
     for (size_t v : sizes) total += v;
-    const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const unsigned nt = std::max(1u, std::min(max_threads, std::thread::hardware_concurrency()));
     if (total < (64u << 20) || nt == 1) {
         for (size_t i = 0; i < sizes.size(); ++i) std::memcpy(dst_src[i].first, dst_src[i].second, sizes[i]);
         return;
@@ -1400,6 +1408,17 @@ void par_memcpy(const std::vector<std::pair<void*, const void*>>& dst_src, const
     for (auto& t : th) t.join();
 }
 
+// host <-> device copy in pieces of at most 1 GiB: larger copies are not given to the SDMA
+// engines but run as a blit kernel that competes with the compute kernels for the CUs
+hipError_t copy_pieces(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+    constexpr size_t kPiece = (size_t)1 << 30;
+    for (size_t o = 0; o < bytes; o += kPiece) {
+        const hipError_t e = hipMemcpyAsync((char*)dst + o, (const char*)src + o, std::min(kPiece, bytes - o), kind, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 int grow_pinned(ctws_handle* h, void*& p, size_t& have, size_t bytes) {
     if (have >= bytes) return CTWS_OK;
     if (p) hipHostFree(p);
@@ -1422,7 +1441,8 @@ struct HostBatch {
 int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* blocks,
                     const std::vector<int>& todo) {
     int r;
-    const int64_t budget = batch_voxels_budget();
+    // (r02: 8-12 blocks of config 3 per batch, 4.3 Gvoxel/s, against 4.0 at the device budget)
+    const int64_t budget = std::min(batch_voxels_budget(), h->host_batch_voxels);
     // batches and their packed layouts (inputs, masks and initial seeds in one buffer)
     std::vector<HostBatch> hb;
     size_t max_in = 0, max_out = 0;
@@ -1432,7 +1452,9 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
         while (e < todo.size()) {
             const ctws_block& b = blocks[todo[e]];
             const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
-            if (e > k && (vox + nv > budget || e - k >= 4096)) break;
+            if (e > k && (vox + nv > budget || e - k >= 4096 || (h->host_batch_blocks > 0 &&
+                                                                  (int)(e - k) >= h->host_batch_blocks)))
+                break;
             vox += nv;
             ++e;
         }
@@ -1482,16 +1504,20 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
         HIPCHK(hipEventRecord(sl.ev_comp, h->stream));
     }
     // pack batch j's inputs into its slot and start the upload (worker thread)
+    // pack batch j's inputs block by block into its slot, each block's upload starting as soon
+    // as it is packed (worker thread)
     auto stage_in = [&](int j) -> int {
         const HostBatch& B = hb[j];
         auto& sl = h->hslot[j % nslots];
-        std::vector<std::pair<void*, const void*>> ds;
-        std::vector<size_t> sz;
+        // the slot's previous upload is complete (and its batch computed: run_batch returns
+        // after its stream drained).  Copies wait on the host, never on another queue's event.
+        if (hipEventSynchronize(sl.ev_h2d) != hipSuccess) return CTWS_EHIP;
+        const auto t0 = std::chrono::steady_clock::now();
         for (int i = 0; i < B.nb; ++i) {
             const ctws_block& b = blocks[todo[B.k + i]];
             const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
-            ds.push_back({(char*)sl.pin_in + B.in_off[i], b.input});
-            sz.push_back(B.in_sz[i]);
+            std::vector<std::pair<void*, const void*>> ds{{(char*)sl.pin_in + B.in_off[i], b.input}};
+            std::vector<size_t> sz{B.in_sz[i]};
             if (b.mask) {
                 ds.push_back({(char*)sl.pin_in + B.m_off[i], b.mask});
                 sz.push_back((size_t)nv);
@@ -1500,29 +1526,31 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
                 ds.push_back({(char*)sl.pin_in + B.i_off[i], b.initial_seeds});
                 sz.push_back((size_t)nv * 8);
             }
+            par_memcpy(ds, sz, (unsigned)h->host_threads);
+            const size_t end = i + 1 < B.nb ? B.in_off[i + 1] : B.in_bytes;
+            if (copy_pieces((char*)sl.d_in.p + B.in_off[i], (char*)sl.pin_in + B.in_off[i], end - B.in_off[i],
+                            hipMemcpyHostToDevice, h->s_in) != hipSuccess)
+                return CTWS_EHIP;
         }
-        // the slot's previous upload has been consumed once its batch computed
-        if (hipEventSynchronize(sl.ev_h2d) != hipSuccess) return CTWS_EHIP;
-        par_memcpy(ds, sz);
-        if (hipStreamWaitEvent(h->s_in, sl.ev_comp, 0) != hipSuccess ||
-            hipMemcpyAsync(sl.d_in.p, sl.pin_in, B.in_bytes, hipMemcpyHostToDevice, h->s_in) != hipSuccess ||
-            hipEventRecord(sl.ev_h2d, h->s_in) != hipSuccess)
-            return CTWS_EHIP;
-        return CTWS_OK;
+        if (h->trace)
+            std::fprintf(stderr, "[ctws] host batch %d: pack %.1f ms (%zu B)\n", j,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3, B.in_bytes);
+        return hipEventRecord(sl.ev_h2d, h->s_in) == hipSuccess ? CTWS_OK : CTWS_EHIP;
     };
-    // unpack batch j's outputs into the callers' arrays once downloaded (worker thread)
+    // unpack batch j's outputs block by block as their downloads complete (worker thread)
     auto drain_out = [&](int j, std::vector<ctws_block>* bbp) -> int {
         const HostBatch& B = hb[j];
         auto& sl = h->hslot[j % nslots];
-        if (hipEventSynchronize(sl.ev_d2h) != hipSuccess) return CTWS_EHIP;
-        std::vector<std::pair<void*, const void*>> ds;
-        std::vector<size_t> sz;
+        const auto t0 = std::chrono::steady_clock::now();
         for (int i = 0; i < B.nb; ++i) {
             if ((*bbp)[i].status == CTWS_BLOCK_EMPTY_PASS2) continue;  // nothing written (:240-242)
-            ds.push_back({blocks[todo[B.k + i]].output, (char*)sl.pin_out + B.o_off[i]});
-            sz.push_back(B.o_sz[i]);
+            if (hipEventSynchronize(sl.ev_blk[i]) != hipSuccess) return CTWS_EHIP;
+            par_memcpy({{blocks[todo[B.k + i]].output, (char*)sl.pin_out + B.o_off[i]}}, {B.o_sz[i]},
+                       (unsigned)h->host_threads);
         }
-        par_memcpy(ds, sz);
+        if (h->trace)
+            std::fprintf(stderr, "[ctws] host batch %d: unpack %.1f ms (%zu B)\n", j,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3, B.out_bytes);
         return CTWS_OK;
     };
     for (auto& sl : h->hslot) HIPCHK(hipEventRecord(sl.ev_h2d, h->s_in));
@@ -1551,15 +1579,18 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             io[i].out = (uint64_t*)((char*)sl.d_out.p + B.o_off[i]);
         }
         // inputs uploaded; the slot's previous outputs downloaded
-        if (hipStreamWaitEvent(h->stream, sl.ev_h2d, 0) != hipSuccess ||
-            hipStreamWaitEvent(h->stream, sl.ev_d2h, 0) != hipSuccess) {
+        if (hipEventSynchronize(sl.ev_h2d) != hipSuccess || hipEventSynchronize(sl.ev_d2h) != hipSuccess) {
             join_all();
             return CTWS_EHIP;
         }
+        const auto tb = std::chrono::steady_clock::now();
         if ((r = run_batch(h, cfg, pl, bb.data(), io.data(), B.nb)) != CTWS_OK) {
             join_all();
             return r;
         }
+        if (h->trace)
+            std::fprintf(stderr, "[ctws] host batch %zu: compute %.1f ms\n", j,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count() * 1e3);
         HIPCHK(hipEventRecord(sl.ev_comp, h->stream));
         // the slot's pinned outputs are free once the drain of batch j - 2 finished
         if (t_out.joinable()) t_out.join();
@@ -1567,8 +1598,28 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             join_all();
             return r_out;
         }
-        if (hipStreamWaitEvent(h->s_out, sl.ev_comp, 0) != hipSuccess ||
-            hipMemcpyAsync(sl.pin_out, sl.d_out.p, B.out_bytes, hipMemcpyDeviceToHost, h->s_out) != hipSuccess ||
+        // download block by block, an event after each
+        while ((int)sl.ev_blk.size() < B.nb) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            sl.ev_blk.push_back(e);
+        }
+        hipError_t ce = hipSuccess;
+        void* hdst = nullptr;
+        if (h->d2h_wgs > 0) ce = hipHostGetDevicePointer(&hdst, sl.pin_out, 0);
+        for (int i = 0; i < B.nb && ce == hipSuccess; ++i) {
+            const size_t o = B.o_off[i], nbytes = (B.o_sz[i] + 15) & ~(size_t)15;
+            if (h->d2h_wgs > 0) {
+                k_copy_to_host<<<h->d2h_wgs, 256, 0, h->s_out>>>((const uint4*)((char*)sl.d_out.p + o),
+                                                                  (uint4*)((char*)hdst + o), nbytes / 16);
+                ce = hipGetLastError();
+            } else {
+                ce = copy_pieces((char*)sl.pin_out + o, (char*)sl.d_out.p + o, B.o_sz[i], hipMemcpyDeviceToHost,
+                                 h->s_out);
+            }
+            if (ce == hipSuccess) ce = hipEventRecord(sl.ev_blk[i], h->s_out);
+        }
+        if (ce != hipSuccess ||
             hipEventRecord(sl.ev_d2h, h->s_out) != hipSuccess) {
             join_all();
             return CTWS_EHIP;
@@ -1683,6 +1734,10 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))
         h->frontier_max_iters = std::max(0, std::min(kFrontierMaxItersCap, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_GAUSS_YX")) h->gauss_yx = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_HOST_BATCH_VOXELS")) h->host_batch_voxels = std::max<int64_t>(1, std::atoll(t));
+    if (const char* t = std::getenv("CTWS_HOST_BATCH_BLOCKS")) h->host_batch_blocks = std::max(0, std::atoi(t));
+    if (const char* t = std::getenv("CTWS_HOST_THREADS")) h->host_threads = std::max(1, std::atoi(t));
+    if (const char* t = std::getenv("CTWS_D2H_WGS")) h->d2h_wgs = std::max(0, std::atoi(t));
     if (const char* t = std::getenv("CTWS_WORDS_PER_WAVE")) h->words_per_wave = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_GAUSS_W")) {
         const int v = std::atoi(t);
@@ -1729,6 +1784,7 @@ void ctws_close(ctws_handle* h) {
         if (sl.d_out.p) hipFree(sl.d_out.p);
         for (hipEvent_t e : {sl.ev_h2d, sl.ev_comp, sl.ev_d2h})
             if (e) hipEventDestroy(e);
+        for (hipEvent_t e : sl.ev_blk) hipEventDestroy(e);
     }
     if (h->s_in) hipStreamDestroy(h->s_in);
     if (h->s_out) hipStreamDestroy(h->s_out);

@@ -177,6 +177,7 @@ __global__ void k_p2_output(const BlockDesc*, BlockStat*, const uint32_t*, const
 __global__ void k_slice_inmask(const BlockDesc*, const BlockStat*, uint32_t*);
 
 // k_relabel.hip (RelabelWorkflow: sorted uniques, assignment-table lookup)
+__global__ void k_copy_to_host(const uint4*, uint4*, size_t);
 __global__ void k_u64_range(const uint64_t*, int64_t, unsigned long long*);
 __global__ void k_u64_bits(const uint64_t*, int64_t, uint64_t, unsigned long long*);
 __global__ void k_bits_chunk_count(const uint64_t*, int64_t, uint32_t*);

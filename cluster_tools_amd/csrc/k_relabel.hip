@@ -143,4 +143,13 @@ __global__ void __launch_bounds__(256) k_u64_lookup(uint64_t* __restrict__ v, in
     if ((threadIdx.x & 63) == 0 && miss) atomicAdd(missing, miss);
 }
 
+// Device -> pinned host copy by a few workgroups (16-B stores, grid-stride).  The runtime moves
+// large device-to-host copies with a blit kernel over every CU, which starves the compute
+// kernels running concurrently; this copy leaves all but gridDim.x CUs to them.
+__global__ void __launch_bounds__(256) k_copy_to_host(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                      size_t n16) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 }  // namespace ctws
