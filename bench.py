@@ -229,6 +229,14 @@ def cpu_baseline(cfg_id, max_cores=16):
     return out, (blist[0]['block_id'], res[0][2])
 
 
+def progress(msg):
+    """A line on stderr per phase: long profiler passes show they are alive."""
+    print('[bench %.1fs] %s' % (time.time() - _T0, msg), file=sys.stderr, flush=True)
+
+
+_T0 = time.time()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -357,14 +365,17 @@ def main():
             offsets['scan'] = torch.cumsum(gathered, 0) - gathered
         return res
 
-    for _ in range(args.warmup):
+    progress('inputs staged: %d blocks, %d outer voxels' % (len(blocks), outer_vox))
+    for k in range(args.warmup):
         step(False)
+        progress('warmup step %d' % k)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         step(True)
+        progress('step %d' % k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -110,6 +110,15 @@ struct ctws_handle {
     int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
     // EDT: counters (64 B) + columns queued for the lower-envelope pass (k_edt_col_fh)
     DevBuf edt_fh;
+    // LDS tile relaxation (k_relax.hip): tile worklists, queued generation per tile, statistics
+    DevBuf rx_list0, rx_list1, rx_gen, rx_stats;
+    // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
+    DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
+    int64_t rx_tiles = 0;  // relaxation tiles of the current batch
+    // CTWS_RELAX=1: LDS tile relaxation (k_relax.hip) instead of the global-memory frontier.
+    // Off by default: r02 single stream, config 3 50.3 vs 22.6 ms, config 4 64.8 vs 45.1 ms per
+    // step (every tile re-solved ~3x: its halo is stale until the neighbours converged)
+    int relax = 0;
     // test hooks
     int stop_after = 0;
     int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
@@ -295,12 +304,14 @@ struct BlockIO {
 struct Plan {
     // validated, derived configuration
     int nd_ws, dt_2d, pass2;
+    int from_seeds;  // WatershedFromSeeds (watershed_from_seeds.py): given seeds, hmap = input
     int pitch[3];
     bool seeds_smooth, weights_smooth;
     double sig_seeds[3], sig_weights[3];
 };
 
 int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
+    p.from_seeds = 0;
     p.nd_ws = cfg->apply_ws_2d ? 2 : 3;
     p.dt_2d = cfg->apply_dt_2d ? 1 : 0;
     if (cfg->pass_id != 0 && cfg->pass_id != 1) {
@@ -554,8 +565,12 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 // key changes.  Batches of kFrontierBatch launches run between host checks of their flags; if
 // it has not converged after frontier_max_iters iterations (very long equal-height paths) the
 // tile flood finishes from the current keys.
+int run_relax(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
+              uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out);
+
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
                  uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
+    if (h->relax) return run_relax(h, pl, nb, TF, max_tiles, TT, packed, fst, iters_out, rounds_out, kms_out);
     Workspace& w = h->ws;
     const int64_t nch = TF / 64 + 1;
     uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
@@ -643,6 +658,88 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     return CTWS_OK;
 }
 
+// Relaxation of the open voxels in LDS tiles (k_relax.hip): iteration 0 solves every tile
+// that holds an open voxel, later iterations the tiles whose halo changed, until no tile is
+// queued.  Same contract as the frontier loop above (the open bitmap in w.fopen; keys of the
+// other voxels final), same fallback to the tile flood after frontier_max_iters launches.
+int run_relax(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
+              uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
+    Workspace& w = h->ws;
+    const int64_t TR = h->rx_tiles;
+    uint64_t* wl[2] = {(uint64_t*)h->rx_list0.p, (uint64_t*)h->rx_list1.p};
+    uint32_t* tgen = (uint32_t*)h->rx_gen.p;
+    uint32_t* rst = fst ? (uint32_t*)h->rx_stats.p : nullptr;
+    HIPCHK(hipMemsetAsync(tgen, 0, sizeof(uint32_t) * (size_t)TR, h->stream));
+    HIPCHK(hipMemsetAsync(w.wlcnt, 0, sizeof(uint32_t) * (size_t)(h->frontier_max_iters + 2), h->stream));
+    if (rst) HIPCHK(hipMemsetAsync(rst, 0, sizeof(uint32_t) * 128, h->stream));
+    const dim3 lg((unsigned)std::min<int64_t>((TR / nb + 255) / 256 + 1, 1024), nb);
+    if (pl.nd_ws == 3) k_relax_list0<3><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt);
+    else k_relax_list0<2><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt);
+    LAUNCHCHK();
+    // a wave per queued tile (4 per workgroup), grid-stride over the list (its length is on the device)
+    const unsigned rg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((TR + 3) / 4, 2048));
+    bool converged = false;
+    int iters = 0;
+    while (iters < h->frontier_max_iters && !converged) {
+        const int it0 = iters;
+        const int nl = std::min(kFrontierBatch, h->frontier_max_iters - it0);
+        for (int k = 0; k < nl; ++k) {
+            const int it = it0 + k;
+            if (pl.nd_ws == 3)
+                k_tile_relax<3><<<rg, 256, 0, h->stream>>>(w.desc, w.hm, w.key, w.fopen, wl[it & 1], w.wlcnt + it,
+                                                           wl[(it + 1) & 1], w.wlcnt + it + 1, tgen, it, rst);
+            else
+                k_tile_relax<2><<<rg, 256, 0, h->stream>>>(w.desc, w.hm, w.key, w.fopen, wl[it & 1], w.wlcnt + it,
+                                                           wl[(it + 1) & 1], w.wlcnt + it + 1, tgen, it, rst);
+        }
+        LAUNCHCHK();
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.wlcnt + it0, sizeof(uint32_t) * (nl + 1), hipMemcpyDeviceToHost,
+                              h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        if (h->trace)
+            for (int k = 0; k < nl; ++k) {
+                std::fprintf(stderr, "[ctws] relax it %d: %u tiles\n", it0 + k, h->h_counter[k]);
+                if (!h->h_counter[k + 1]) break;
+            }
+        for (int k = 0; k < nl; ++k) {
+            ++iters;
+            if (!h->h_counter[k + 1]) {  // nothing queued for the next iteration
+                converged = true;
+                break;
+            }
+        }
+    }
+    *iters_out += iters;
+    if (rst) {
+        uint32_t hs[128];
+        HIPCHK(hipMemcpy(hs, rst, sizeof(hs), hipMemcpyDeviceToHost));
+        double v = 0, rr = 0;
+        for (int k = 0; k < 64; ++k) {
+            v += hs[2 * k];
+            rr += hs[2 * k + 1];
+        }
+        // fst[nb..2nb): frontier visits per block (summed over the batch into block 0's slot)
+        uint32_t vv = (uint32_t)std::min(v, 4.0e9);
+        HIPCHK(hipMemcpy(fst + nb, &vv, sizeof(uint32_t), hipMemcpyHostToDevice));
+        if (h->trace) std::fprintf(stderr, "[ctws] relax: %.0f visits, %.0f tile rounds\n", v, rr);
+    }
+    if (!converged) {
+        int TZ, TY, TX;
+        flood_tile_dims(pl.nd_ws, packed, &TZ, &TY, &TX);
+        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+        k_frontier_tiles<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0,
+                           h->stream>>>(w.desc, w.stat, w.fopen, w.act0, TZ, TY, TX);
+        LAUNCHCHK();
+        int rounds = 0;
+        float kms = 0.f;
+        int r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds, &kms);
+        if (r != CTWS_OK) return r;
+        *rounds_out += rounds;
+        *kms_out += kms;
+    }
+    return CTWS_OK;
+}
+
 int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 
@@ -659,11 +756,63 @@ void add_timing(ctws_handle* h, const char* name, float v) {
     h->timings.push_back({name, v});
 }
 
+// ---- WatershedFromSeeds seeds (k_seeded.hip) ----------------------------------------------
+// The blocks' distinct seed values (hash), sorted per block (segmented radix sort), a label
+// per value = 1 + its rank; blocks without any seed get the strict minima of the hmap
+// (k_auto_minima + the bitmap rank, labels written by k_fs_auto_label once `packed` is known).
+int fs_seeds(ctws_handle* h, const std::vector<BlockDesc>& desc, int nb, int64_t TH, int64_t TW, int64_t TS,
+             int64_t maxH, int64_t maxRows, dim3 vg, dim3 wg) {
+    Workspace& w = h->ws;
+    int r;
+    const size_t nh = (size_t)std::max<int64_t>(TH, 1);
+    if ((r = grow(h, h->fs_vals, sizeof(uint32_t) * nh)) != CTWS_OK) return r;
+    if ((r = grow(h, h->fs_sorted, sizeof(uint32_t) * nh)) != CTWS_OK) return r;
+    if ((r = grow(h, h->fs_off, sizeof(int) * 2 * (size_t)nb)) != CTWS_OK) return r;
+    uint32_t* vals = (uint32_t*)h->fs_vals.p;
+    uint32_t* sorted = (uint32_t*)h->fs_sorted.p;
+    int* off = (int*)h->fs_off.p;
+    HIPCHK(hipMemsetAsync(w.hkey, 0xFF, sizeof(uint64_t) * nh, h->stream));
+    k_fs_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey);
+    const dim3 hg((unsigned)std::min<int64_t>((maxH + 255) / 256, 4096), nb);
+    k_fs_collect<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, vals);
+    k_fs_offsets<<<(nb + 255) / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb, off, off + nb);
+    LAUNCHCHK();
+    size_t tb = 0;
+    HIPCHK(fs_segmented_sort(nullptr, tb, vals, sorted, (int)nh, nb, off, off + nb, h->stream));
+    if ((r = grow(h, h->fs_tmp, tb)) != CTWS_OK) return r;
+    HIPCHK(fs_segmented_sort(h->fs_tmp.p, tb, vals, sorted, (int)nh, nb, off, off + nb, h->stream));
+    k_fs_rank<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, sorted, w.hpos);
+    LAUNCHCHK();
+    std::vector<BlockStat> st(nb);
+    HIPCHK(hipMemcpyAsync(st.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    std::vector<uint32_t> surv((size_t)std::max<int64_t>(TS, 1), 1u);
+    bool any = false;
+    for (int i = 0; i < nb; ++i)
+        if (st[i].n_seeds == 0) {
+            surv[desc[i].sbase] = 0u;
+            any = true;
+        }
+    HIPCHK(hipMemcpyAsync(w.surv, surv.data(), sizeof(uint32_t) * surv.size(), hipMemcpyHostToDevice, h->stream));
+    if (any) {
+        // watershedsNew with an all-zero seed image seeds from the strict minima of the hmap
+        HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+        const dim3 ag((unsigned)std::min<int64_t>(maxRows, 65535), nb);
+        k_auto_minima<<<ag, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.surv, w.W);
+        k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
+        k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 2);
+        k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
+        LAUNCHCHK();
+    }
+    // (surv stays in w.surv: k_fs_auto_label reads it; the size filter re-initialises it)
+    return CTWS_OK;
+}
+
 // ---- one batch, all pointers on the device ------------------------------------------------
 int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* blocks, const BlockIO* io, int nb) {
     Workspace& w = h->ws;
     std::vector<BlockDesc> desc(nb);
-    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0, TH = 0, TF = 0;
+    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0, TH = 0, TF = 0, TR = 0;
     int64_t maxH = 0, maxRows = 0, maxIRows = 0;
     int maxZ = 0, maxY = 0, maxX = 0, max_tiles = 0;
     int64_t maxN = 0, maxNI = 0;
@@ -714,7 +863,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         d.id_offset = (uint64_t)b.block_id * bvol;
         d.pass2 = (uint32_t)pl.pass2;
-        if (pl.pass2) {
+        if (pl.pass2 || pl.from_seeds) {
             if (!d.init) {
                 h->err = "pass 2 needs initial_seeds (ds_out[input_bb]) for every block";
                 return CTWS_EINVAL;
@@ -728,6 +877,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
                             (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
         d.fbase = TF;
+        {
+            // LDS relaxation tiles (RTile, k_relax.hip): 1 x 32 x 32 (2-D ws) or 8 x 8 x 16
+            const int rz = pl.nd_ws == 3 ? 8 : 1, ry = pl.nd_ws == 3 ? 8 : 32, rx = pl.nd_ws == 3 ? 16 : 32;
+            d.rbase = TR;
+            TR += (int64_t)((d.Z + rz - 1) / rz) * ((d.Y + ry - 1) / ry) * ((d.X + rx - 1) / rx);
+        }
         // frontier bitmaps: rows padded to a multiple of 64, so that the block's chunks (64 rows
         // x one word column, k_frontier) are exactly its words / 64
         TF += (((int64_t)d.Z * d.Y + 63) / 64) * 64 * ((d.X + 63) / 64);
@@ -782,7 +937,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         else
             dmax = std::pow((double)pl.pitch[0] * d.Z, 2) + std::pow((double)pl.pitch[1] * d.Y, 2) +
                    std::pow((double)pl.pitch[2] * d.X, 2);
-        if (dmax >= 16777216.0) {
+        if (dmax >= 16777216.0 && !pl.from_seeds) {
             h->err = "dmax >= 2^24: float32 squared distances are no longer exact";
             return CTWS_EUNSUPPORTED;
         }
@@ -809,6 +964,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     set_tiles(true);
     int r;
     if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb, TH, TF)) != CTWS_OK) return r;
+    if ((r = grow(h, h->rx_list0, sizeof(uint64_t) * (size_t)TR)) != CTWS_OK) return r;
+    if ((r = grow(h, h->rx_list1, sizeof(uint64_t) * (size_t)TR)) != CTWS_OK) return r;
+    if ((r = grow(h, h->rx_gen, sizeof(uint32_t) * (size_t)TR)) != CTWS_OK) return r;
+    if ((r = grow(h, h->rx_stats, sizeof(uint32_t) * 128)) != CTWS_OK) return r;
+    h->rx_tiles = TR;
     HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
     h->last_desc = desc;
     std::vector<BlockStat> st(nb);
@@ -833,8 +993,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     // (h->words_per_wave words per wave: a workgroup per handful of words would make the
     // dispatch of ~10^6 workgroups the bottleneck)
     const int64_t wpw = (int64_t)kWordWaves * h->words_per_wave;
-    const dim3 wtg((unsigned)std::min<int64_t>((maxRows * ((maxX + 63) / 64) + wpw - 1) / wpw, 65535), nb);
-    const dim3 wtig((unsigned)std::min<int64_t>((maxIRows * ((maxIX + 63) / 64) + wpw - 1) / wpw, 65535), nb);
+    // (x extents rounded to a multiple of 8: xcd_swizzle's id % 8 then labels one XCD per grid row)
+    auto r8 = [](int64_t v) { return (unsigned)std::min<int64_t>(v > 8 ? (v + 7) / 8 * 8 : v, 65528); };
+    const dim3 wtg(r8((maxRows * ((maxX + 63) / 64) + wpw - 1) / wpw), nb);
+    const dim3 wtig(r8((maxIRows * ((maxIX + 63) / 64) + wpw - 1) / wpw), nb);
     size_t ev = 0;
     std::vector<const char*> names;
     auto mark = [&](const char* name) {
@@ -864,24 +1026,27 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_input_minmax<<<g, 256, 0, h->stream>>>(w.desc, w.stat);
         }
         LAUNCHCHK();
-        PrepParams pp{(float)cfg->threshold, cfg->invert_inputs, cfg->agglomerate_channels, pl.pitch[2] * pl.pitch[2]};
+        // WatershedFromSeeds: _read_data without invert; the normalized input is the hmap
+        PrepParams pp{(float)cfg->threshold, pl.from_seeds ? 0 : cfg->invert_inputs, cfg->agglomerate_channels,
+                      pl.pitch[2] * pl.pitch[2]};
+        float* fin_out = pl.from_seeds ? w.hm : w.fin;
         dim3 gx((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
         // rows up to 1024 voxels: one wave per row in registers.  f32 rows of exactly 64 K voxels
         // move as float4 with lanes owning consecutive voxels (k_prep_edt_x_reg); other rows use
         // the lane-interleaved coalesced layout (k_prep_edt_x_co)
         auto launch_co = [&](auto kmax_c) {
             constexpr int KM = decltype(kmax_c)::value;
-            if (dt == CTWS_U8) k_prep_edt_x_co<KM, uint8_t><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
-            else if (dt == CTWS_U16) k_prep_edt_x_co<KM, uint16_t><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
-            else if (dt == CTWS_F32) k_prep_edt_x_co<KM, float><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
-            else k_prep_edt_x_co<KM, double><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+            if (dt == CTWS_U8) k_prep_edt_x_co<KM, uint8_t><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
+            else if (dt == CTWS_U16) k_prep_edt_x_co<KM, uint16_t><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
+            else if (dt == CTWS_F32) k_prep_edt_x_co<KM, float><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
+            else k_prep_edt_x_co<KM, double><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
         };
         if (typed && all_exact && maxX == 256)
-            k_prep_edt_x_reg<4><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+            k_prep_edt_x_reg<4><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
         else if (typed && all_exact && maxX == 512)
-            k_prep_edt_x_reg<8><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+            k_prep_edt_x_reg<8><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
         else if (typed && all_exact && maxX == 1024)
-            k_prep_edt_x_reg<16><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+            k_prep_edt_x_reg<16><<<gx, 256, 0, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
         else if (typed && maxX <= 256)
             launch_co(std::integral_constant<int, 4>());
         else if (typed && maxX <= 512)
@@ -889,12 +1054,20 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         else if (typed && maxX <= 1024)
             launch_co(std::integral_constant<int, 16>());
         else
-            k_prep_edt_x<<<gx, 256, 4 * (size_t)maxX * 4, h->stream>>>(w.desc, w.stat, pp, w.fin, (uint32_t*)w.A);
+            k_prep_edt_x<<<gx, 256, 4 * (size_t)maxX * 4, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
         LAUNCHCHK();
-        k_set_active<<<(nb + 255) / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb);
+        if (pl.from_seeds) k_fs_active<<<(nb + 255) / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb);
+        else k_set_active<<<(nb + 255) / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb);
         LAUNCHCHK();
     }
     mark("prep_edt_x");
+    bool packed = true;
+    uint32_t max_seeds = 0;  // sizes the LDS histogram of the size filter
+    std::vector<BlockStat> s2(nb);
+    const dim3 gsb((unsigned)((maxZ + 255) / 256), nb);
+    if (pl.from_seeds) {
+        if ((r = fs_seeds(h, desc, nb, TH, TW, TS, maxH, maxRows, vg, wg)) != CTWS_OK) return r;
+    } else {
     {
         // y pass (final for a 2-D dt), then z pass (3-D dt)
         const int Wy = h->edt_w ? h->edt_w : edt_col_width(maxY);
@@ -1010,7 +1183,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
     k_root_label<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.Wp);
-    const dim3 gsb((unsigned)((maxZ + 255) / 256), nb);
     if (pl.pass2) {
         // _apply_watershed_with_seeds: shifted seeds + initial seeds, relabelConsecutive
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
@@ -1026,16 +1198,16 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
         LAUNCHCHK();
     }
+    }  // !from_seeds
     // packed flood keys need labels < 2^20 in every block of the batch
-    bool packed = true;
-    uint32_t max_seeds = 0;  // sizes the LDS histogram of the size filter
-    std::vector<BlockStat> s2(nb);
     {
         HIPCHK(hipMemcpyAsync(s2.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
         for (auto& s : s2) {
-            if (s.n_seeds >= (1u << 20) - 1u) packed = false;
-            max_seeds = std::max(max_seeds, s.n_seeds);
+            // (WatershedFromSeeds: a seedless block's seeds are its n_auto strict minima)
+            const uint32_t ns = std::max(s.n_seeds, pl.from_seeds ? s.n_auto : 0u);
+            if (ns >= (1u << 20) - 1u) packed = false;
+            max_seeds = std::max(max_seeds, ns);
         }
         if (!packed) {
             set_tiles(false);
@@ -1045,7 +1217,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
     uint8_t* excl = nullptr;
     const bool descent = packed && !h->no_descent;
-    const bool cc_seeds = descent && !pl.pass2 && h->stop_after != CTWS_STOP_SEEDS;
+    const bool cc_seeds = descent && !pl.pass2 && !pl.from_seeds && h->stop_after != CTWS_STOP_SEEDS;
     const uint32_t* cc = cc_seeds ? w.PF : nullptr;
     if (pl.pass2) {
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
@@ -1054,6 +1226,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         excl = (uint8_t*)w.fin;  // free after the hmap
         k_p2_excl_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, excl);
         k_p2_excl<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, excl);
+    } else if (pl.from_seeds) {
+        // labels, keys and seed flags in the packed / wide key form (fs_seeds counted them)
+        k_fs_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.hm, w.lab, w.key, w.cls, packed ? 1 : 0);
+        k_fs_auto_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.surv, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
+                                                   packed ? 1 : 0);
     } else {
         // the descent flood reads the seeds from the CC parents directly (cc_seeds)
         if (!cc_seeds)
@@ -1245,6 +1422,14 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                                                w.soff);
         LAUNCHCHK();
         mark("output");
+    } else if (pl.from_seeds) {
+        // WatershedFromSeeds: labels -> seed values (uint64), masked voxels 0; no crop / offset
+        mark("finalize");
+        mark("crop_cc");
+        k_fs_output<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, (const uint32_t*)h->fs_sorted.p,
+                                               w.surv, cfg->size_filter > 0 ? 1 : 0);
+        LAUNCHCHK();
+        mark("output");
     } else {
         // ---- 2-D offsets (uncropped blocks only: a cropped block is renumbered by its CC) ----
         bool any_crop = false, any_plain2d = false;
@@ -1332,10 +1517,15 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : (pl.pass2 ? CTWS_BLOCK_EMPTY_PASS2 : CTWS_BLOCK_EMPTY);
         blocks[i].max_label = st[i].active ? st[i].max_label : 0;
+        if (pl.from_seeds) {
+            uint64_t mx;
+            std::memcpy(&mx, &st[i]._p[2], sizeof(mx));
+            blocks[i].max_label = mx;
+        }
         // distinct nonzero output ids: the labels, plus the bare offset of unlabelled in-mask
         // voxels (empty block: only that one, watershed.py:310-321); block 0's offset is 0
         const uint32_t bare = (st[i].active ? st[i]._p[0] : 1u) && desc[i].id_offset != 0;
-        blocks[i].n_ids = pl.pass2 ? -1 : (int32_t)((st[i].active ? st[i].n_cc : 0u) + bare);
+        blocks[i].n_ids = (pl.pass2 || pl.from_seeds) ? -1 : (int32_t)((st[i].active ? st[i].n_cc : 0u) + bare);
         if (!st[i].active) continue;
         uint32_t err = st[i].err;
         const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
@@ -1355,12 +1545,13 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (err) {
             blocks[i].status = CTWS_BLOCK_FAILED;
             char msg[256];
-            std::snprintf(msg, sizeof msg, "block %lld failed (%s%s%s%s%s); ", (long long)blocks[i].block_id,
+            std::snprintf(msg, sizeof msg, "block %lld failed (%s%s%s%s%s%s); ", (long long)blocks[i].block_id,
                           (err & kErrHashFull) ? "pass-2 relabel hash table full " : "",
                           (err & kErrCollision) ? "pass-2 2-D wrapped id collision not resolved " : "",
                           (err & kErrLabelBits) ? "auto-seed labels beyond 2^20 " : "",
                           (err & kErrTakeDict) ? "takeDict: no new_to_old entry, as in the reference " : "",
-                          (err & kErrUnsupported) ? "auto-seeded regrow with >= 2^20 seeds " : "");
+                          (err & kErrUnsupported) ? "auto-seeded regrow with >= 2^20 seeds " : "",
+                          (err & kErrOverflow) ? "seed id >= 2^32 - 1: Overflow detected, as in the reference " : "");
             h->err += msg;
         }
     }
@@ -1640,14 +1831,40 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
     return r_out;
 }
 
-int run_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n, bool device_ptrs) {
-    if (!h || !cfg || (!blocks && n > 0) || n < 0) return CTWS_EINVAL;
+int run_blocks(ctws_handle* h, const ctws_cfg* cfg_in, ctws_block* blocks, int n, bool device_ptrs,
+               bool from_seeds = false) {
+    if (!h || !cfg_in || (!blocks && n > 0) || n < 0) return CTWS_EINVAL;
     h->err.clear();
     h->timings.clear();
     HIPCHK(hipSetDevice(h->device));
+    ctws_cfg fcfg = *cfg_in;
+    if (from_seeds) {
+        // watershed_from_seeds.py: 3-D watershedsNew on the normalized input, no dt / smoothing
+        fcfg.apply_ws_2d = fcfg.apply_dt_2d = 0;
+        fcfg.has_pixel_pitch = 0;
+        fcfg.sigma_seeds_is_list = fcfg.sigma_weights_is_list = 0;
+        fcfg.sigma_seeds[0] = fcfg.sigma_weights[0] = 0.0;
+        fcfg.invert_inputs = 0;
+        fcfg.pass_id = 0;
+        for (int i = 0; i < n; ++i) {
+            ctws_block& b = blocks[i];
+            for (int k = 0; k < 3; ++k) {
+                if (b.inner_begin[k] != 0 || b.inner_shape[k] != b.outer_shape[k]) {
+                    h->err = "WatershedFromSeeds blocks have no halo: inner block == block";
+                    return CTWS_EINVAL;
+                }
+            }
+            if (!b.initial_seeds) {
+                h->err = "WatershedFromSeeds needs the seeds (ds_seeds[bb]) of every block";
+                return CTWS_EINVAL;
+            }
+        }
+    }
+    const ctws_cfg* cfg = &fcfg;
     Plan pl;
     int r = make_plan(h, cfg, pl);
     if (r != CTWS_OK) return r;
+    pl.from_seeds = from_seeds ? 1 : 0;
     // blocks whose inner mask is empty are skipped entirely (watershed.py:290-297); the
     // host-pointer path checks this on the host, the device path on the caller's side
     std::vector<int> todo;
@@ -1748,6 +1965,7 @@ int ctws_open(int device, ctws_handle** out) {
         h->edt_w = (v == 8 || v == 16 || v == 32) ? v : 0;
     }
     if (const char* t = std::getenv("CTWS_FRONTIER_UNROLL")) h->frontier_unroll = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_RELAX")) h->relax = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
@@ -1769,7 +1987,8 @@ void ctws_close(ctws_handle* h) {
                     w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
                     w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
                     h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p,
-                    h->edt_fh.p};
+                    h->edt_fh.p, h->rx_list0.p, h->rx_list1.p, h->rx_gen.p, h->rx_stats.p,
+                    h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);
@@ -1801,6 +2020,14 @@ int ctws_ws_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int 
 
 int ctws_ws_blocks_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks) {
     return run_blocks(h, cfg, blocks, n_blocks, true);
+}
+
+int ctws_ws_from_seeds(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks) {
+    return run_blocks(h, cfg, blocks, n_blocks, false, true);
+}
+
+int ctws_ws_from_seeds_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks) {
+    return run_blocks(h, cfg, blocks, n_blocks, true, true);
 }
 
 int ctws_last_timings(const ctws_handle* h, const char** names, float* ms, int max_entries) {

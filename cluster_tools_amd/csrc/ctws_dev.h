@@ -42,6 +42,7 @@ struct BlockDesc {
     int64_t hbase;          // pass 2: offset into the relabel hash arrays
     int64_t hcap;           // pass 2: hash capacity of this block (power of two)
     int64_t fbase;          // offset into the frontier bitmaps (Z*Y rows of ceil(X/64) words)
+    int64_t rbase;          // offset into the per-tile arrays of the LDS tile relaxation (k_relax.hip)
 };
 
 struct BlockStat {
@@ -64,6 +65,7 @@ constexpr uint32_t kErrCollision = 2u;   // pass 2 (2-D): wrapped new id == init
 constexpr uint32_t kErrLabelBits = 4u;   // auto-seeded regrow: labels beyond the 20-bit key field
 constexpr uint32_t kErrTakeDict = 8u;    // pass 2: auto-seed label without a new_to_old entry
 constexpr uint32_t kErrUnsupported = 16u; // auto-seeded regrow in a block with >= 2^20 seeds (wide keys)
+constexpr uint32_t kErrOverflow = 32u;    // WatershedFromSeeds: seed id >= 2^32 - 1 (the reference's assert)
 
 // Pointers read from the block descriptor are generic to the compiler: accesses through them
 // become flat loads, and the waits the compiler puts around flat accesses serialise a wave's
@@ -243,9 +245,23 @@ __device__ __forceinline__ uint32_t flood_label(const uint32_t* lab, const uint6
     return lab[i] & ~kFixedBit;
 }
 
+// ---- XCD-aware workgroup order -----------------------------------------------------------
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch),
+// each with its own L2: consecutive workgroup ids land on different L2s, so a stencil's
+// neighbour rows are fetched from HBM once per XCD.  The bijective remap gives the workgroups
+// that share an XCD (equal id % 8) one contiguous range of logical ids.  Speed only: any
+// placement computes the same result.  Launches using it keep gridDim.x a multiple of 8 when
+// grid.y > 1, so that id % 8 labels the XCD for every grid row.
+__device__ __forceinline__ int xcd_swizzle(int b, int n) {
+    const int xcd = b & 7, q = n >> 3, r = n & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 // ---- word tiles --------------------------------------------------------------------------
 // A wave handles one 64-voxel word of a row (lane = x - 64 * word), kWordWaves_ waves per
-// workgroup, grid-stride over the block's Z * Y * ceil(X / 64) words.  Rows whose length is
+// workgroup; each wave takes a contiguous run of the block's Z * Y * ceil(X / 64) words (the
+// rows above / below of a word were just read by the same wave: L1 / L2 hits) and the runs of
+// the workgroups on one XCD are contiguous (xcd_swizzle).  Rows whose length is
 // not a multiple of 256 keep every lane busy (a row-tile loop x += 256 runs its last pass
 // over a 576-voxel row with a quarter of the threads), x-neighbours are lane shuffles, and
 // a word is exactly one word of the frontier bitmaps.  BODY sees z, y, x, i (block C-order
@@ -256,8 +272,12 @@ __device__ __forceinline__ uint32_t flood_label(const uint32_t* lab, const uint6
         const int wpr = ((nx) + 63) >> 6;                                                                    \
         const int64_t nwords_ = (int64_t)(nz) * (ny) * wpr;                                                  \
         const int lane = threadIdx.x & 63;                                                                   \
-        for (int64_t w_ = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w_ < nwords_;        \
-             w_ += (int64_t)gridDim.x * (blockDim.x >> 6)) {                                                 \
+        const int64_t nwaves_ = (int64_t)gridDim.x * (blockDim.x >> 6);                                      \
+        const int64_t per_ = (nwords_ + nwaves_ - 1) / nwaves_;                                              \
+        const int64_t wid_ = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) +     \
+                             (threadIdx.x >> 6);                                                             \
+        const int64_t wend_ = wid_ * per_ + per_ < nwords_ ? wid_ * per_ + per_ : nwords_;                   \
+        for (int64_t w_ = wid_ * per_; w_ < wend_; ++w_) {                                                   \
             const int64_t row = w_ / wpr;                                                                    \
             const int xw = (int)(w_ - row * wpr);                                                            \
             const int z = (int)(row / (ny));                                                                 \

@@ -131,6 +131,25 @@ template <int ND, int U>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
                            const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
+// k_seeded.hip (WatershedFromSeeds)
+__global__ void k_fs_active(const BlockDesc*, BlockStat*, int);
+__global__ void k_fs_insert(const BlockDesc*, BlockStat*, uint64_t*);
+__global__ void k_fs_collect(const BlockDesc*, BlockStat*, const uint64_t*, uint32_t*);
+__global__ void k_fs_offsets(const BlockDesc*, const BlockStat*, int, int*, int*);
+__global__ void k_fs_rank(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
+__global__ void k_fs_label(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, const float*, uint32_t*,
+                           uint64_t*, uint8_t*, int);
+__global__ void k_fs_auto_label(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
+                                const float*, uint32_t*, uint64_t*, uint8_t*, int);
+__global__ void k_fs_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
+                            const uint32_t*, int);
+hipError_t fs_segmented_sort(void* tmp, size_t& bytes, const uint32_t* in, uint32_t* out, int n, int nseg,
+                             const int* beg, const int* end, hipStream_t stream);
+template <int ND>
+__global__ void k_relax_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint64_t*, uint32_t*);
+template <int ND>
+__global__ void k_tile_relax(const BlockDesc*, const float*, uint64_t*, const uint64_t*, const uint64_t*,
+                             const uint32_t*, uint64_t*, uint32_t*, uint32_t*, int, uint32_t*);
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>

@@ -10,7 +10,7 @@ import threading
 
 import numpy as np
 
-from ._abi import CtwsBlock, make_cfg, dtype_code, CTWS_OK, CTWS_BLOCK_FAILED  # noqa: F401
+from ._abi import CtwsBlock, make_cfg, dtype_code, CTWS_OK, CTWS_BLOCK_FAILED, CTWS_BLOCK_WRITTEN  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libctws.so')
@@ -43,7 +43,7 @@ def lib():
             L.ctws_close.restype = None
             L.ctws_last_error.argtypes = [C.c_void_p]
             L.ctws_last_error.restype = C.c_char_p
-            for fn in ('ctws_ws_blocks', 'ctws_ws_blocks_device'):
+            for fn in ('ctws_ws_blocks', 'ctws_ws_blocks_device', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device'):
                 getattr(L, fn).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_last_timings.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_comm_unique_id.argtypes = [C.c_void_p, C.c_void_p]
@@ -63,7 +63,7 @@ def lib():
 EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
                     'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_comm_unique_id', 'ctws_comm_init',
                     'ctws_allgather_counts', 'ctws_unique_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
-                    'ctws_debug_set_stop', 'ctws_debug_read')
+                    'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device')
 
 
 class CtwsError(RuntimeError):
@@ -218,6 +218,46 @@ class Handle:
             c.output = out.data_ptr()
         self._check(lib().ctws_ws_blocks_device(self._h, C.byref(cfg), arr, n), 'ctws_ws_blocks_device')
         return [(int(arr[i].status), int(arr[i].max_label), int(arr[i].n_ids)) for i in range(n)]
+
+    # ---- WatershedFromSeeds --------------------------------------------------------------
+    def ws_from_seeds(self, config, blocks):
+        """WatershedFromSeeds `_ws_block[_masked]` (watershed_from_seeds.py:143-199) on numpy
+        blocks: dicts with 'input' (block, 3-D or 4-D C,Z,Y,X), 'seeds' (block-shaped ids, as
+        ds_seeds[bb] returns them), optional 'mask' and 'out' (uint64, block-shaped).
+        Returns [{'output', 'status', 'max_label'}, ...]."""
+        cfg = make_cfg(config, (1, 1, 1), 0)
+        n = len(blocks)
+        arr = (CtwsBlock * n)()
+        keep, results = [], []
+        for i, b in enumerate(blocks):
+            inp = np.ascontiguousarray(b['input'])
+            shape = tuple(inp.shape[-3:])
+            c = arr[i]
+            c.input = inp.ctypes.data
+            c.input_dtype = dtype_code(inp.dtype)
+            c.n_channels = inp.shape[0] if inp.ndim == 4 else 0
+            c.outer_shape[:] = list(shape)
+            c.inner_shape[:] = list(shape)
+            seeds = np.ascontiguousarray(b['seeds'], dtype=np.uint64)
+            assert seeds.shape == shape
+            c.initial_seeds = seeds.ctypes.data
+            keep += [inp, seeds]
+            if b.get('mask') is not None:
+                m = np.ascontiguousarray(b['mask'], dtype=np.uint8)
+                keep.append(m)
+                c.mask = m.ctypes.data
+            out = b.get('out')
+            if out is None:
+                out = np.zeros(shape, dtype=np.uint64)
+            assert out.dtype == np.uint64 and out.flags.c_contiguous and out.shape == shape
+            keep.append(out)
+            c.output = out.ctypes.data
+            results.append({'output': out})
+        self._check(lib().ctws_ws_from_seeds(self._h, C.byref(cfg), arr, n), 'ctws_ws_from_seeds')
+        for i, r in enumerate(results):
+            r['status'] = int(arr[i].status)
+            r['max_label'] = int(arr[i].max_label)
+        return results
 
     # ---- RelabelWorkflow kernels ---------------------------------------------------------
     def unique_u64(self, labels):

@@ -17,6 +17,10 @@
  *       The caller does the dataset I/O (ds_in[input_bb], ds_out[output_bb] = ...) and the
  *       "processed block" log lines, exactly as the reference job entry does.
  *
+ *   ctws_ws_from_seeds / ctws_ws_from_seeds_device
+ *       the WatershedFromSeeds job loop (watershed/watershed_from_seeds.py:236-249 over
+ *       `_ws_block` / `_ws_block_masked`, :143-199).
+ *
  *   ctws_open / ctws_close / ctws_last_error
  *       process-level setup; the reference has none (vigra is stateless).  One handle per
  *       (process, GPU), as LocalTask runs one process per job (cluster_tasks.py:507-529).
@@ -148,6 +152,20 @@ int ctws_ws_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int 
  * call returns after the stream has drained.
  */
 int ctws_ws_blocks_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks);
+
+/*
+ * WatershedFromSeeds (watershed/watershed_from_seeds.py:143-199, `_ws_block` and
+ * `_ws_block_masked`): per block, input = normalize(ds_in[bb]) (4-D: channel range +
+ * agglomeration; no invert), masked voxels -> 1, seeds = `initial_seeds` (= ds_seeds[bb],
+ * uint64, the block's shape), ws = watershedsNew(input, seeds) (3-D, direct nbhd) + the
+ * size filter (cfg.size_filter), ws[~mask] = 0 -> `output` (uint64).  Blocks have no halo:
+ * inner_begin = 0, inner_shape = outer_shape.  Only threshold-independent keys of `cfg` are
+ * read (size_filter, channel_begin/end, agglomerate_channels).  A block whose seeds hold an
+ * id >= 2^32 - 1 gets CTWS_BLOCK_FAILED (the reference's "Overflow detected" assert); a block
+ * with an empty mask CTWS_BLOCK_SKIPPED_MASK (nothing written).  max_label = largest output id.
+ */
+int ctws_ws_from_seeds(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks);
+int ctws_ws_from_seeds_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks);
 
 /*
  * Stage timings of the last ctws_ws_blocks* call, measured with HIP events on the

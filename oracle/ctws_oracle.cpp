@@ -1063,4 +1063,52 @@ int orc_ws_blocks(const ctws_cfg* cfg, ctws_block* blocks, int n_blocks, OrcStag
     }
 }
 
+// WatershedFromSeeds `_ws_block` / `_ws_block_masked` (watershed/watershed_from_seeds.py:
+// 143-199) for each block: no halo (input = output = the block), `_read_data` (:125-140:
+// normalize, 4-D channel agglomeration, no invert), seeds = ds_seeds[bb] as uint32 after the
+// `max_id < uint32 max` assert (:160-163; a block failing it gets CTWS_BLOCK_FAILED),
+// vu.watershed(input, seeds, size_filter) (3-D, direct nbhd), masked voxels: input 1 before,
+// label 0 after the flood (:186-198); an empty block mask writes nothing (:178-181).
+int orc_ws_from_seeds(const ctws_cfg* cfg_in, ctws_block* blocks, int n_blocks) {
+    try {
+        ctws_cfg cfg = *cfg_in;
+        cfg.invert_inputs = 0;
+        for (int bi = 0; bi < n_blocks; ++bi) {
+            ctws_block& b = blocks[bi];
+            const int64_t* sh = b.outer_shape;
+            const int64_t n = sh[0] * sh[1] * sh[2];
+            b.status = CTWS_BLOCK_WRITTEN;
+            b.max_label = 0;
+            if (b.mask) {
+                int64_t s = 0;
+                for (int64_t i = 0; i < n; ++i) s += b.mask[i] != 0;
+                if (s == 0) {
+                    b.status = CTWS_BLOCK_SKIPPED_MASK;
+                    continue;
+                }
+            }
+            uint64_t smax = 0;
+            for (int64_t i = 0; i < n; ++i) smax = std::max(smax, b.initial_seeds[i]);
+            if (smax >= 0xFFFFFFFFull) {
+                b.status = CTWS_BLOCK_FAILED;  // AssertionError "Overflow detected"
+                continue;
+            }
+            std::vector<float> input;
+            read_data(cfg, b, input);
+            if (b.mask)
+                for (int64_t i = 0; i < n; ++i)
+                    if (!b.mask[i]) input[i] = 1.0f;
+            std::vector<uint32_t> ws(n);
+            for (int64_t i = 0; i < n; ++i) ws[i] = (uint32_t)b.initial_seeds[i];
+            const uint32_t mx = vu_watershed(input.data(), make_dims(3, sh), ws.data(), cfg.size_filter, nullptr);
+            for (int64_t i = 0; i < n; ++i) b.output[i] = (b.mask && !b.mask[i]) ? 0ull : (uint64_t)ws[i];
+            b.max_label = mx;
+        }
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 }  // extern "C"

@@ -195,3 +195,38 @@ def ws_blocks(config, block_shape, blocks, pass_id=0, with_stages=False):
         r['status'] = int(arr[i].status)
         r['max_label'] = int(arr[i].max_label)
     return results
+
+
+def ws_from_seeds(config, blocks):
+    """WatershedFromSeeds `_ws_block[_masked]` (watershed/watershed_from_seeds.py:143-199) on a
+    list of blocks: dicts with input (block ndarray, 3-D or 4-D C,Z,Y,X), seeds (block-shaped,
+    uint64 as read from ds_seeds), mask (uint8/bool or None).  Returns dicts with output
+    (uint64, block-shaped), status and max_label."""
+    cfg = make_cfg(config, (1, 1, 1), 0)
+    n = len(blocks)
+    arr = (CtwsBlock * n)()
+    keep, results = [], []
+    for i, b in enumerate(blocks):
+        inp = np.ascontiguousarray(b['input'])
+        c = arr[i]
+        c.input = inp.ctypes.data
+        c.input_dtype = dtype_code(inp.dtype)
+        c.n_channels = inp.shape[0] if inp.ndim == 4 else 0
+        c.outer_shape[:] = inp.shape[-3:]
+        c.inner_shape[:] = inp.shape[-3:]
+        s = np.ascontiguousarray(b['seeds'], dtype=np.uint64)
+        c.initial_seeds = s.ctypes.data
+        keep += [inp, s]
+        if b.get('mask') is not None:
+            m = np.ascontiguousarray(b['mask'], dtype=np.uint8)
+            keep.append(m)
+            c.mask = m.ctypes.data
+        out = np.zeros(inp.shape[-3:], dtype=np.uint64)
+        keep.append(out)
+        c.output = out.ctypes.data
+        results.append({'output': out})
+    _check(lib().orc_ws_from_seeds(C.byref(cfg), arr, n))
+    for i, r in enumerate(results):
+        r['status'] = int(arr[i].status)
+        r['max_label'] = int(arr[i].max_label)
+    return results

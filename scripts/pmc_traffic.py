@@ -9,7 +9,8 @@ import os
 import sys
 from collections import defaultdict
 
-STAGE_OF = {'k_descent_tile': 'flood', 'k_descent_init': 'flood', 'k_frontier': 'flood',
+STAGE_OF = {'k_descent_tile': 'flood', 'k_descent_init': 'flood', 'k_frontier': 'flood', 'k_flood_verify': 'flood',
+            'k_frontier_list0': 'flood',
             'k_input_minmax': 'prep_edt_x', 'k_prep_edt_x': 'prep_edt_x', 'k_prep_edt_x_reg': 'prep_edt_x',
             'k_edt_col': 'edt_yz', 'k_hist': 'size_filter', 'k_hist_zero': 'size_filter',
             'k_size_filter': 'size_filter', 'k_output': 'output'}
