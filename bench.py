@@ -278,7 +278,14 @@ def main():
     origin = (geo['g0'], 0, 0)
     gen = dict(seed=cfg['seed'], device=dev, dtype=cfg.get('dtype', 'float32'), pitch=cfg.get('pitch', (24, 24, 24)),
                origin=origin, full_shape=full)
-    vol = boundary_map_torch(geo['gshape'], **gen)
+    # generated slab by slab (per-voxel deterministic: identical to one call), with progress
+    vol = torch.empty(geo['gshape'], dtype=torch.uint8 if cfg.get('dtype') == 'uint8' else torch.float32, device=dev)
+    zs = 32
+    for z0 in range(0, geo['gshape'][0], zs):
+        z1 = min(geo['gshape'][0], z0 + zs)
+        vol[z0:z1] = boundary_map_torch((z1 - z0,) + tuple(geo['gshape'][1:]),
+                                        **dict(gen, origin=(origin[0] + z0, 0, 0)))
+        progress('synthetic input z %d..%d' % (z0, z1))
     mvol = ellipsoid_mask_torch(geo['gshape'], origin, full, device=dev) if cfg.get('mask') else None
     blist = geo['blocks']
     # two-pass: the pass-1 labels of the region (own slab + z halos from the neighbour ranks)

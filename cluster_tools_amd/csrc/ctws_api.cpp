@@ -114,6 +114,9 @@ struct ctws_handle {
     DevBuf rx_list0, rx_list1, rx_gen, rx_stats;
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
+    // evaluation (k_eval.hip): gt / seg / pair hash tables with counts, state, sums, staging
+    DevBuf ev_ka, ev_ca, ev_kb, ev_cb, ev_kp, ev_cp, ev_state, ev_out, ev_stage;
+    int64_t ev_cap_a = 0, ev_cap_b = 0, ev_cap_p = 0;
     int64_t rx_tiles = 0;  // relaxation tiles of the current batch
     // CTWS_RELAX=1: LDS tile relaxation (k_relax.hip) instead of the global-memory frontier.
     // Off by default: r02 single stream, config 3 50.3 vs 22.6 ms, config 4 64.8 vs 45.1 ms per
@@ -1289,9 +1292,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (h->verify) {
             HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
             if (pl.nd_ws == 3)
-                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
+                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
             else
-                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.lab, cc, w.counter);
+                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
             LAUNCHCHK();
             HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
@@ -1330,6 +1333,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     // ---- size filter + regrow ---------------------------------------------------------------
     std::vector<uint32_t> surv(TS, 1u);
     int n_auto_blocks = 0;
+    bool regrow_bad = false;  // the regrow's fixpoint check failed: the batch's blocks fail
     if (cfg->size_filter > 0) {
         uint32_t* counts = (uint32_t*)w.A;
         auto histogram = [&]() -> int {
@@ -1388,6 +1392,22 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2)) !=
                 CTWS_OK)
                 return r;
+            if (h->verify) {
+                // the regrow's fixpoint at the voxels it solved (the removed ones)
+                HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
+                if (pl.nd_ws == 3)
+                    k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+                else
+                    k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+                LAUNCHCHK();
+                HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
+                HIPCHK(hipStreamSynchronize(h->stream));
+                if (h->h_counter[0] && h->verify >= 2) {
+                    h->err = "regrow fixpoint check failed (CTWS_VERIFY=2)";
+                    return CTWS_EHIP;
+                }
+                regrow_bad = h->h_counter[0] != 0;
+            }
         } else {
             FilterParams fp{(uint32_t)cfg->size_filter, 0, 0, 0, w.act0};
             flood_tile_dims(pl.nd_ws, packed, &fp.tz, &fp.ty, &fp.tx);
@@ -1527,7 +1547,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const uint32_t bare = (st[i].active ? st[i]._p[0] : 1u) && desc[i].id_offset != 0;
         blocks[i].n_ids = (pl.pass2 || pl.from_seeds) ? -1 : (int32_t)((st[i].active ? st[i].n_cc : 0u) + bare);
         if (!st[i].active) continue;
-        uint32_t err = st[i].err;
+        uint32_t err = st[i].err | (regrow_bad ? kErrVerify : 0u);
         const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
         if (pl.pass2) {
             // a slice/block without any seed: watershedsNew seeds from the hmap minima and the
@@ -1545,13 +1565,14 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (err) {
             blocks[i].status = CTWS_BLOCK_FAILED;
             char msg[256];
-            std::snprintf(msg, sizeof msg, "block %lld failed (%s%s%s%s%s%s); ", (long long)blocks[i].block_id,
+            std::snprintf(msg, sizeof msg, "block %lld failed (%s%s%s%s%s%s%s); ", (long long)blocks[i].block_id,
                           (err & kErrHashFull) ? "pass-2 relabel hash table full " : "",
                           (err & kErrCollision) ? "pass-2 2-D wrapped id collision not resolved " : "",
                           (err & kErrLabelBits) ? "auto-seed labels beyond 2^20 " : "",
                           (err & kErrTakeDict) ? "takeDict: no new_to_old entry, as in the reference " : "",
                           (err & kErrUnsupported) ? "auto-seeded regrow with >= 2^20 seeds " : "",
-                          (err & kErrOverflow) ? "seed id >= 2^32 - 1: Overflow detected, as in the reference " : "");
+                          (err & kErrOverflow) ? "seed id >= 2^32 - 1: Overflow detected, as in the reference " : "",
+                          (err & kErrVerify) ? "size-filter regrow fixpoint check failed " : "");
             h->err += msg;
         }
     }
@@ -1988,7 +2009,8 @@ void ctws_close(ctws_handle* h) {
                     w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
                     h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p,
                     h->edt_fh.p, h->rx_list0.p, h->rx_list1.p, h->rx_gen.p, h->rx_stats.p,
-                    h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p};
+                    h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
+                    h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);
@@ -2020,6 +2042,115 @@ int ctws_ws_blocks(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int 
 
 int ctws_ws_blocks_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks) {
     return run_blocks(h, cfg, blocks, n_blocks, true);
+}
+
+// ---- evaluation: contingency table in HBM (k_eval.hip) ----------------------------------
+static int64_t pow2_at_least(int64_t v) {
+    int64_t c = 1024;
+    while (c < v) c <<= 1;
+    return c;
+}
+
+int ctws_eval_begin(ctws_handle* h, int64_t cap_labels, int64_t cap_pairs) {
+    if (!h || cap_labels < 0 || cap_pairs < 0) return CTWS_EINVAL;
+    h->err.clear();
+    HIPCHK(hipSetDevice(h->device));
+    const int64_t ca = pow2_at_least(2 * std::max<int64_t>(cap_labels, 1));
+    const int64_t cp = pow2_at_least(2 * std::max<int64_t>(cap_pairs, 1));
+    if (ca > (1ll << 32) || cp > (1ll << 33)) {
+        h->err = "ctws_eval_begin: capacity too large";
+        return CTWS_EINVAL;
+    }
+    int r;
+    if ((r = grow(h, h->ev_ka, 8 * (size_t)ca)) != CTWS_OK || (r = grow(h, h->ev_ca, 8 * (size_t)ca)) != CTWS_OK ||
+        (r = grow(h, h->ev_kb, 8 * (size_t)ca)) != CTWS_OK || (r = grow(h, h->ev_cb, 8 * (size_t)ca)) != CTWS_OK ||
+        (r = grow(h, h->ev_kp, 8 * (size_t)cp)) != CTWS_OK || (r = grow(h, h->ev_cp, 8 * (size_t)cp)) != CTWS_OK ||
+        (r = grow(h, h->ev_state, 16)) != CTWS_OK || (r = grow(h, h->ev_out, 6 * sizeof(double))) != CTWS_OK)
+        return r;
+    h->ev_cap_a = h->ev_cap_b = ca;
+    h->ev_cap_p = cp;
+    HIPCHK(hipMemsetAsync(h->ev_ka.p, 0xFF, 8 * (size_t)ca, h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_kb.p, 0xFF, 8 * (size_t)ca, h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_kp.p, 0xFF, 8 * (size_t)cp, h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_ca.p, 0, 8 * (size_t)ca, h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_cb.p, 0, 8 * (size_t)ca, h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_cp.p, 0, 8 * (size_t)cp, h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_state.p, 0, 16, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return CTWS_OK;
+}
+
+int ctws_eval_add(ctws_handle* h, const uint64_t* seg, const uint64_t* gt, int64_t n, int on_device, int ignore_gt_zero) {
+    if (!h || n < 0 || (n > 0 && (!seg || !gt))) return CTWS_EINVAL;
+    if (!h->ev_cap_a) {
+        h->err = "ctws_eval_add before ctws_eval_begin";
+        return CTWS_EINVAL;
+    }
+    HIPCHK(hipSetDevice(h->device));
+    auto launch = [&](const uint64_t* s, const uint64_t* g, int64_t m) -> int {
+        const unsigned grid = (unsigned)std::min<int64_t>((m + 255) / 256, 8192);
+        k_eval_add<<<grid, 256, 0, h->stream>>>(s, g, m, ignore_gt_zero, (uint64_t*)h->ev_ka.p,
+                                                 (unsigned long long*)h->ev_ca.p, h->ev_cap_a, (uint64_t*)h->ev_kb.p,
+                                                 (unsigned long long*)h->ev_cb.p, h->ev_cap_b, (uint64_t*)h->ev_kp.p,
+                                                 (unsigned long long*)h->ev_cp.p, h->ev_cap_p,
+                                                 (unsigned long long*)h->ev_state.p);
+        LAUNCHCHK();
+        return CTWS_OK;
+    };
+    int r;
+    if (on_device) {
+        if ((r = launch(seg, gt, n)) != CTWS_OK) return r;
+    } else {
+        const int64_t chunk = (int64_t)1 << 25;  // voxels per staged piece (2 x 256 MiB)
+        if ((r = grow(h, h->ev_stage, 16 * (size_t)std::min(chunk, std::max<int64_t>(n, 1)))) != CTWS_OK) return r;
+        uint64_t* ds = (uint64_t*)h->ev_stage.p;
+        for (int64_t o = 0; o < n; o += chunk) {
+            const int64_t m = std::min(chunk, n - o);
+            uint64_t* dg = ds + std::min(chunk, std::max<int64_t>(n, 1));
+            HIPCHK(hipMemcpyAsync(ds, seg + o, 8 * (size_t)m, hipMemcpyHostToDevice, h->stream));
+            HIPCHK(hipMemcpyAsync(dg, gt + o, 8 * (size_t)m, hipMemcpyHostToDevice, h->stream));
+            if ((r = launch(ds, dg, m)) != CTWS_OK) return r;
+        }
+    }
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return CTWS_OK;
+}
+
+int ctws_eval_end(ctws_handle* h, double* scores, int64_t* n_points) {
+    if (!h || !scores) return CTWS_EINVAL;
+    if (!h->ev_cap_a) {
+        h->err = "ctws_eval_end before ctws_eval_begin";
+        return CTWS_EINVAL;
+    }
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipMemsetAsync(h->ev_out.p, 0, 6 * sizeof(double), h->stream));
+    const unsigned grid = (unsigned)std::min<int64_t>((std::max(h->ev_cap_a, h->ev_cap_p) + 255) / 256, 4096);
+    k_eval_reduce<<<grid, 256, 0, h->stream>>>((const uint64_t*)h->ev_ka.p, (const unsigned long long*)h->ev_ca.p,
+                                               h->ev_cap_a, (const uint64_t*)h->ev_kb.p,
+                                               (const unsigned long long*)h->ev_cb.p, h->ev_cap_b,
+                                               (const uint64_t*)h->ev_kp.p, (const unsigned long long*)h->ev_cp.p,
+                                               h->ev_cap_p, (const unsigned long long*)h->ev_state.p,
+                                               (double*)h->ev_out.p);
+    LAUNCHCHK();
+    double v[6];
+    unsigned long long st[2];
+    HIPCHK(hipMemcpyAsync(v, h->ev_out.p, sizeof(v), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(st, h->ev_state.p, sizeof(st), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (st[1]) {
+        h->err = "contingency hash table full: call ctws_eval_begin with larger capacities";
+        return CTWS_EUNSUPPORTED;
+    }
+    const double n = (double)st[0];
+    if (n_points) *n_points = (int64_t)st[0];
+    // validation_utils.py:60-76 (a = gt, b = seg) and :178-198
+    scores[0] = v[1] - v[2];  // vi split
+    scores[1] = v[0] - v[2];  // vi merge
+    const double prec = v[4] > 0 ? v[5] / v[4] : 0.0, rec = v[3] > 0 ? v[5] / v[3] : 0.0;
+    const double ari = (prec + rec) > 0 ? 2 * prec * rec / (prec + rec) : 0.0;
+    scores[2] = 1.0 - ari;
+    scores[3] = n > 0 ? 1.0 - (v[3] + v[4] - 2 * v[5]) / (n * n) : 1.0;
+    return CTWS_OK;
 }
 
 int ctws_ws_from_seeds(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks) {

@@ -65,6 +65,7 @@ constexpr uint32_t kErrCollision = 2u;   // pass 2 (2-D): wrapped new id == init
 constexpr uint32_t kErrLabelBits = 4u;   // auto-seeded regrow: labels beyond the 20-bit key field
 constexpr uint32_t kErrTakeDict = 8u;    // pass 2: auto-seed label without a new_to_old entry
 constexpr uint32_t kErrUnsupported = 16u; // auto-seeded regrow in a block with >= 2^20 seeds (wide keys)
+constexpr uint32_t kErrVerify = 64u;     // the regrow's fixpoint check failed (CTWS_VERIFY=1): labels not written
 constexpr uint32_t kErrOverflow = 32u;    // WatershedFromSeeds: seed id >= 2^32 - 1 (the reference's assert)
 
 // Pointers read from the block descriptor are generic to the compiler: accesses through them

@@ -131,6 +131,13 @@ template <int ND, int U>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
                            const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
+// k_eval.hip (VI / Rand contingency table)
+__global__ void k_eval_add(const uint64_t*, const uint64_t*, int64_t, int, uint64_t*, unsigned long long*, int64_t,
+                           uint64_t*, unsigned long long*, int64_t, uint64_t*, unsigned long long*, int64_t,
+                           unsigned long long*);
+__global__ void k_eval_reduce(const uint64_t*, const unsigned long long*, int64_t, const uint64_t*,
+                              const unsigned long long*, int64_t, const uint64_t*, const unsigned long long*, int64_t,
+                              const unsigned long long*, double*);
 // k_seeded.hip (WatershedFromSeeds)
 __global__ void k_fs_active(const BlockDesc*, BlockStat*, int);
 __global__ void k_fs_insert(const BlockDesc*, BlockStat*, uint64_t*);
@@ -153,8 +160,8 @@ __global__ void k_tile_relax(const BlockDesc*, const float*, uint64_t*, const ui
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>
-__global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint32_t*,
-                               const uint32_t*, uint32_t*);
+__global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint64_t*,
+                               uint32_t*);
 constexpr int kWordWaves = 4;  // waves per workgroup of the word-tiled kernels
 __global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
                               uint64_t*, uint8_t*);

@@ -1067,22 +1067,25 @@ __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restr
     }
 }
 
-// fixpoint check of the packed flood: K(q) == f(min_p K(p)) for every non-seed voxel.  Word
-// tiles: a wave reads a 64-voxel row word coalesced; x-neighbours come from the neighbouring
-// lanes, the rows above / below (and the slices) are loads that the neighbouring waves'
-// own reads keep in cache.
+// fixpoint check of the packed flood: K(q) == f(min_p K(p)) at every voxel the relaxation
+// solved (the open bitmap of k_descent_init / k_regrow_init).  The descent-resolved voxels are
+// final by construction (the unique-argmin argument above) and are never written by the
+// relaxation, so words without an open voxel are skipped after one bitmap load.  Word tiles:
+// a wave reads a 64-voxel row word coalesced; x-neighbours come from the neighbouring lanes,
+// the rows above / below (and the slices) are loads the same wave's previous words keep in
+// cache.
 template <int ND>
 __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint64_t* __restrict__ key,
-                                                      const uint32_t* __restrict__ lab, const uint32_t* __restrict__ cc,
-                                                      uint32_t* __restrict__ flag) {
+                                                      const uint64_t* __restrict__ open, uint32_t* __restrict__ flag) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const uint64_t* k = key + B.base;
     const int64_t YX = (int64_t)B.Y * B.X;
-    const uint32_t* seedsrc = cc ? cc : lab;  // seed: cc != kNoParent, or lab has kFixedBit
     bool bad = false;
     WORD_TILES(B.Z, B.Y, B.X, {
+        const uint64_t ow = gbl(open)[B.fbase + w_];
+        if (ow == 0ull) continue;  // every voxel of the word descent-resolved / kept
         // every load unconditional (clamped index) so that they are all in flight together
         const int64_t ic = valid ? i : row * B.X;
         const uint64_t own0 = k[ic];
@@ -1094,7 +1097,6 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
         }
         const uint64_t kxm = k[x > 0 && valid ? ic - 1 : ic], kxp = k[x + 1 < B.X ? ic + 1 : ic];
         const float hv = h[B.base + ic];
-        const uint32_t sv = seedsrc[B.base + ic];
         const uint64_t own = valid ? own0 : kPackInf;
         uint64_t l = shfl_up_u64(own, 1), r = shfl_down_u64(own, 1);
         if (lane == 0) l = (x > 0) ? kxm : kPackInf;
@@ -1107,9 +1109,10 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
             if (z > 0) m = min(m, kzm);
             if (z + 1 < B.Z) m = min(m, kzp);
         }
-        const bool seed = cc ? sv != kNoParent : (sv & kFixedBit) != 0;
+        // an open voxel is never a seed (descent: seeds resolve to themselves; regrow: the
+        // survivors and auto seeds are taken out of the open set)
         const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(hv), m);
-        const bool b1 = valid && !seed && e != own;
+        const bool b1 = valid && ((ow >> lane) & 1ull) && e != own;
         if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
             const uint32_t slot = atomicAdd(&flag[1], 1u);
             if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + i);
@@ -1119,9 +1122,9 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 template __global__ void k_flood_verify<3>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
-                                           const uint32_t*, const uint32_t*, uint32_t*);
+                                           const uint64_t*, uint32_t*);
 template __global__ void k_flood_verify<2>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
-                                           const uint32_t*, const uint32_t*, uint32_t*);
+                                           const uint64_t*, uint32_t*);
 
 // seeds only (fallback after a failed verification)
 __global__ void __launch_bounds__(256) k_flood_reset(const BlockDesc* __restrict__ D, const BlockStat* S,

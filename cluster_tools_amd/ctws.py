@@ -43,7 +43,8 @@ def lib():
             L.ctws_close.restype = None
             L.ctws_last_error.argtypes = [C.c_void_p]
             L.ctws_last_error.restype = C.c_char_p
-            for fn in ('ctws_ws_blocks', 'ctws_ws_blocks_device', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device'):
+            for fn in ('ctws_ws_blocks', 'ctws_ws_blocks_device', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
+                    'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end'):
                 getattr(L, fn).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_last_timings.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_comm_unique_id.argtypes = [C.c_void_p, C.c_void_p]
@@ -54,6 +55,9 @@ def lib():
             L.ctws_lookup_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
                                           C.c_int64, C.POINTER(C.c_int64)]
             L.ctws_set_table_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+            L.ctws_eval_begin.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
+            L.ctws_eval_add.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
+            L.ctws_eval_end.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
             L.ctws_debug_set_stop.argtypes = [C.c_void_p, C.c_int]
             L.ctws_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_int64]
             _lib = L
@@ -63,7 +67,8 @@ def lib():
 EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
                     'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_comm_unique_id', 'ctws_comm_init',
                     'ctws_allgather_counts', 'ctws_unique_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
-                    'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device')
+                    'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
+                    'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end')
 
 
 class CtwsError(RuntimeError):
@@ -258,6 +263,46 @@ class Handle:
             r['status'] = int(arr[i].status)
             r['max_label'] = int(arr[i].max_label)
         return results
+
+    # ---- evaluation (VI / Rand) ---------------------------------------------------------
+    def eval_begin(self, cap_labels, cap_pairs):
+        """Start a contingency table for at most cap_labels distinct ids per side and
+        cap_pairs distinct (gt, seg) pairs."""
+        self._check(lib().ctws_eval_begin(self._h, int(cap_labels), int(cap_pairs)), 'ctws_eval_begin')
+
+    def eval_add(self, seg, gt, ignore_gt_zero=False):
+        """Add a block: numpy uint64 arrays, or torch tensors (int64 / uint64) on this GPU."""
+        on_dev = hasattr(seg, 'data_ptr')
+        if on_dev:
+            assert seg.is_contiguous() and gt.is_contiguous() and seg.numel() == gt.numel()
+            assert seg.element_size() == 8 and gt.element_size() == 8
+            import torch
+            torch.cuda.current_stream(seg.device).synchronize()
+            ps, pg, n = seg.data_ptr(), gt.data_ptr(), seg.numel()
+        else:
+            seg = np.ascontiguousarray(seg, dtype=np.uint64)
+            gt = np.ascontiguousarray(gt, dtype=np.uint64)
+            assert seg.size == gt.size
+            ps, pg, n = seg.ctypes.data, gt.ctypes.data, seg.size
+        self._check(lib().ctws_eval_add(self._h, ps, pg, int(n), int(on_dev), int(bool(ignore_gt_zero))),
+                    'ctws_eval_add')
+
+    def eval_end(self):
+        """{'vi-split', 'vi-merge', 'adapted-rand-error', 'rand-index', 'n_points'}."""
+        sc = (C.c_double * 4)()
+        npts = C.c_int64()
+        self._check(lib().ctws_eval_end(self._h, sc, C.byref(npts)), 'ctws_eval_end')
+        return {'vi-split': sc[0], 'vi-merge': sc[1], 'adapted-rand-error': sc[2], 'rand-index': sc[3],
+                'n_points': int(npts.value)}
+
+    def evaluate(self, seg, gt, ignore_gt_zero=False, cap_labels=None, cap_pairs=None):
+        """VI / Rand of one segmentation against one groundtruth in a single table.  Without
+        capacities the table is sized for the worst case (every voxel its own id), capped."""
+        n = int(np.prod(seg.shape))
+        cap = min(n, 1 << 26)
+        self.eval_begin(cap_labels or cap, cap_pairs or cap)
+        self.eval_add(seg, gt, ignore_gt_zero)
+        return self.eval_end()
 
     # ---- RelabelWorkflow kernels ---------------------------------------------------------
     def unique_u64(self, labels):

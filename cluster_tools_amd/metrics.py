@@ -3,22 +3,27 @@
 VI (split, merge; log2) and adapted Rand error exactly as
 cluster_tools/utils/validation_utils.py:60-76 (compute_vi_scores) and :178-198
 (compute_rand_scores), with the contingency table of validation_utils.py:9-35 computed by a
-vectorised numpy pair-count instead of nifty.ground_truth.overlap.  `seg` plays seg_a, `gt`
-plays seg_b; `ignore_gt` drops voxels whose gt label is in the list (the evaluation workflow
-ignores gt label 0 by default, evaluation/evaluation_workflow.py:53,60-67).
+vectorised numpy pair-count instead of nifty.ground_truth.overlap.  As in
+variation_of_information (validation_utils.py:79-112: contigency_table(groundtruth,
+segmentation)) and measures.py (overlaps of seg with gt), `gt` plays seg_a and `seg` plays
+seg_b, so vi_split = H(seg | gt) and vi_merge = H(gt | seg); `ignore_gt` drops voxels whose gt
+label is in the list (the evaluation workflow ignores gt label 0 by default,
+evaluation/evaluation_workflow.py:53,60-67).  Host-side check for the tests; the GPU version
+is ctws.Handle.evaluate (k_eval.hip).
 """
 import numpy as np
 
 
 def contingency(seg, gt, ignore_gt=None):
+    """(a = gt counts, b = seg counts, pair gt index, pair seg index, pair counts, n)."""
     seg = np.asarray(seg).ravel()
     gt = np.asarray(gt).ravel()
     if ignore_gt is not None:
         keep = ~np.isin(gt, ignore_gt)
         seg, gt = seg[keep], gt[keep]
     n = float(seg.size)
-    a_ids, a_inv, a_counts = np.unique(seg, return_inverse=True, return_counts=True)
-    b_ids, b_inv, b_counts = np.unique(gt, return_inverse=True, return_counts=True)
+    a_ids, a_inv, a_counts = np.unique(gt, return_inverse=True, return_counts=True)
+    b_ids, b_inv, b_counts = np.unique(seg, return_inverse=True, return_counts=True)
     pair = a_inv.astype(np.int64) * len(b_ids) + b_inv.astype(np.int64)
     p_ids, p_counts = np.unique(pair, return_counts=True)
     pa, pb = p_ids // len(b_ids), p_ids % len(b_ids)

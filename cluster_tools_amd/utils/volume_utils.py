@@ -131,6 +131,10 @@ class InterpolatedVolume:
         starts = tuple(int(floor(ind.start * sc)) for ind, sc in zip(index, self.scale))
         stops = tuple(sta + 1 if single else int(ceil(ind.stop * sc))
                       for ind, sc, sta, single in zip(index, self.scale, starts, singletons))
+        # an axis that the low-res crop collapses to one voxel while the request is longer
+        # reads one more voxel (volume_classes.py:207-212)
+        stops = tuple(b + 1 if (b - a == 1 and not single) else b
+                      for a, b, single in zip(starts, stops, singletons))
         data = self.volume[tuple(slice(a, b) for a, b in zip(starts, stops))]
         s = data.sum()
         if s == 0:

@@ -21,6 +21,10 @@
  *       the WatershedFromSeeds job loop (watershed/watershed_from_seeds.py:236-249 over
  *       `_ws_block` / `_ws_block_masked`, :143-199).
  *
+ *   ctws_eval_begin / ctws_eval_add / ctws_eval_end
+ *       EvaluationWorkflow's overlaps + Measures (evaluation/evaluation_workflow.py:53-77,
+ *       evaluation/measures.py:80-164, utils/validation_utils.py:60-76, 178-198).
+ *
  *   ctws_open / ctws_close / ctws_last_error
  *       process-level setup; the reference has none (vigra is stateless).  One handle per
  *       (process, GPU), as LocalTask runs one process per job (cluster_tasks.py:507-529).
@@ -166,6 +170,21 @@ int ctws_ws_blocks_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* block
  */
 int ctws_ws_from_seeds(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks);
 int ctws_ws_from_seeds_device(ctws_handle* h, const ctws_cfg* cfg, ctws_block* blocks, int n_blocks);
+
+/*
+ * Evaluation (evaluation/measures.py:80-164 with utils/validation_utils.py:60-76, 178-198):
+ * the seg x gt contingency table built in HBM (hash tables of gt ids, seg ids and id pairs
+ * with voxel counts), accumulated over any number of ctws_eval_add calls (blockwise), then
+ * reduced.  cap_labels / cap_pairs bound the distinct ids per side / distinct pairs; a full
+ * table makes ctws_eval_end return CTWS_EUNSUPPORTED (retry with larger capacities).
+ * ignore_gt_zero drops voxels whose gt label is 0 (EvaluationWorkflow(ignore_label=True),
+ * evaluation_workflow.py:53,60).  scores = {vi_split, vi_merge, adapted_rand_error,
+ * rand_index} (log2), exactly the keys measures() writes.
+ */
+int ctws_eval_begin(ctws_handle* h, int64_t cap_labels, int64_t cap_pairs);
+int ctws_eval_add(ctws_handle* h, const uint64_t* seg, const uint64_t* gt, int64_t n, int on_device,
+                  int ignore_gt_zero);
+int ctws_eval_end(ctws_handle* h, double* scores /* [4] */, int64_t* n_points);
 
 /*
  * Stage timings of the last ctws_ws_blocks* call, measured with HIP events on the

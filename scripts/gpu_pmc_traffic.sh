@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
 for grp in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc/$grp -o p -- python -u bench.py --config ${CONFIG:-3} --steps 1 --warmup 0 --no-cpu-baseline --no-host --streams 1 ${BENCH_ARGS:-} > gpurun_out/pmc/$grp.log 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex ctws --output-format csv -d gpurun_out/pmc/$grp -o p -- python -u bench.py --config ${CONFIG:-3} --steps 1 --warmup 0 --no-cpu-baseline --no-host --streams 1 ${BENCH_ARGS:-} > gpurun_out/pmc/$grp.log 2>&1
   rc=$?; echo "pmc $grp rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done

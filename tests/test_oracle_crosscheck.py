@@ -187,3 +187,15 @@ def test_oracle_reproduces_golden_fixtures():
             assert np.array_equal(r['input'], z['fin']), name
             assert np.array_equal(r['ws'], z['ws']), name
             assert _sha(r['dt']) == meta['dt_sha256'], name
+
+
+def test_metrics_orientation_matches_reference():
+    """validation_utils.py:60-76 with contigency_table(groundtruth, segmentation): a
+    segmentation that splits every gt object has vi-split > 0 and vi-merge = 0."""
+    from cluster_tools_amd.metrics import vi_scores
+    gt = np.repeat(np.arange(4), 16).reshape(8, 8)
+    seg = np.arange(64).reshape(8, 8) // 4
+    vs, vm = vi_scores(seg, gt)
+    assert vs > 0.5 and abs(vm) < 1e-12
+    vs2, vm2 = vi_scores(gt, seg)
+    assert abs(vs2) < 1e-12 and abs(vm2 - vs) < 1e-12

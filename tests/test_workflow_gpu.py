@@ -180,3 +180,27 @@ def test_two_pass_workflow(tmp_path, name, batch_blocks):
     vis, vim = vi_scores(res, ref)
     print('two-pass %s: VI %.2e' % (name, vis + vim))
     assert vis + vim <= 0.01, (vis, vim)
+
+
+def test_watershed_low_res_mask(tmp_path):
+    """A mask stored at half resolution goes through load_mask -> InterpolatedVolume
+    (volume_utils.py:208-218, volume_classes.py:155-232) in the job; the oracle gets the same
+    per-block masks from the same InterpolatedVolume requests."""
+    from cluster_tools_amd.watershed.watershed import WatershedLocal
+    cfg_dir, inp, x, c = _setup(tmp_path, 'ws_3d', False)
+    low = ellipsoid_mask(SHAPE)[::2, ::2, ::2]
+    with vu.file_reader(inp) as f:
+        f.create_dataset('mask_low', data=low, chunks=(10, 32, 32))
+    out = str(tmp_path / 'ws.n5')
+    ws = WatershedLocal(input_path=inp, input_key='boundaries', output_path=out, output_key='ws_raw',
+                        config_dir=cfg_dir, tmp_folder=str(tmp_path / 'tmp_ws'), max_jobs=2,
+                        mask_path=inp, mask_key='mask_low')
+    assert luigi.build([ws], local_scheduler=True)
+    with vu.file_reader(out, 'r') as f:
+        raw = f['ws_raw'][:]
+    mask = vu.load_mask(inp, 'mask_low', SHAPE)
+    assert isinstance(mask, vu.InterpolatedVolume)
+    ref = _oracle_volume(x, c, mask)
+    assert (raw == 0).any() and ((raw == 0) == (ref == 0)).all()
+    vis, vim = vi_scores(raw, ref, [0])
+    assert vis + vim <= 0.01, (vis, vim)
