@@ -689,7 +689,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
         for (int k = 0; k < PER; ++k) {
             const uint32_t v = sv[k];
             const bool need = cc && v != kNoParent && !(v & kRootBit) && ((seedm >> k) & 1u);
-            rl[k] = gbl(cc ? cc : lab)[B.base + (need ? v : 0u)];
+            rl[k] = gbl(cc ? cc : lab)[B.base + (need ? v : 0u)];  // unconditional: all in flight
         }
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
@@ -743,30 +743,60 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     uint32_t cnt_open = 0;  // statistics (CTWS_TRACE): voxels left to the relaxation
-    // word tiles: a wave's ballot is exactly one word of the open / changed bitmaps
-    WORD_TILES(B.Z, B.Y, B.X, {
-        const int64_t gi = B.base + (valid ? i : 0);
-        const uint32_t e0 = gbl(par)[gi];
-        const float hv = gbl(h)[gi];
-        uint32_t e = valid ? e0 : kDescRes;
+    // word tiles (a wave's ballot is exactly one word of the open / changed bitmaps), U words
+    // per step: the U chains of a lane hop together, so U dependent-load latencies overlap
+    constexpr int U = 4;
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
+        int64_t gi[U];
+        bool valid[U];
+        uint32_t e[U];
+        float hv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t wu = w0 + u;
+            const int64_t row = wu / wpr;
+            const int x = (int)(wu - row * wpr) * 64 + lane;
+            valid[u] = wu < wend && x < B.X;
+            gi[u] = B.base + (valid[u] ? row * B.X + x : 0);
+            e[u] = gbl(par)[gi[u]];
+            hv[u] = gbl(h)[gi[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (!valid[u]) e[u] = kDescRes;
         for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
-            if (e & kDescRes) break;
-            e = par[B.base + e];
+            bool more = false;
+#pragma unroll
+            for (int u = 0; u < U; ++u) more |= !(e[u] & kDescRes);
+            if (!more) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (!(e[u] & kDescRes)) e[u] = gbl(par)[B.base + e[u]];
         }
-        const uint32_t lr = e & ~kDescRes;
-        const bool res = lr != 0;
-        if (valid) {
-            key[gi] = res ? (((uint64_t)ordf(hv) << 32) | (uint64_t)lr) : kPackInf;
-            fixedv[gi] = res ? 1 : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t lr = e[u] & ~kDescRes;
+            const bool res = lr != 0;
+            if (valid[u]) {
+                key[gi[u]] = res ? (((uint64_t)ordf(hv[u]) << 32) | (uint64_t)lr) : kPackInf;
+                fixedv[gi[u]] = res ? 1 : 0;
+            }
+            const uint64_t op = __ballot(valid[u] && !res);
+            const uint64_t fi = __ballot(valid[u] && res);
+            if (lane == 0 && w0 + u < wend) {
+                open[B.fbase + w0 + u] = op;
+                chg[B.fbase + w0 + u] = fi;
+            }
+            cnt_open += lane == 0 ? (uint32_t)__popcll(op) : 0u;
         }
-        const uint64_t op = __ballot(valid && !res);
-        const uint64_t fi = __ballot(valid && res);
-        if (lane == 0) {
-            open[B.fbase + w_] = op;
-            chg[B.fbase + w_] = fi;
-        }
-        cnt_open += lane == 0 ? (uint32_t)__popcll(op) : 0u;
-    })
+    }
     if (nopen) {
         cnt_open = wg_reduce_u32(cnt_open, OpAdd());
         if (threadIdx.x == 0 && cnt_open) atomicAdd(&nopen[blockIdx.y], cnt_open);
