@@ -186,42 +186,73 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     constexpr uint64_t kLab = (1ull << 20) - 1ull;
-    // word tiles: a wave's ballot is exactly one word of the open / changed bitmaps
-    WORD_TILES(B.Z, B.Y, B.X, {
-        // loads unconditional (clamped index): key, seed flag and height together, then the
-        // label's count
-        const int64_t gi = B.base + (valid ? i : row * B.X);
-        const uint64_t kv0 = key[gi];
-        const uint8_t fx0 = fixedv[gi];
-        const float hv = h[gi];
-        const uint64_t kv = valid ? kv0 : kInfKey;
-        const uint8_t fx = valid ? fx0 : 0;
-        const uint32_t l = kv == kInfKey ? 0u : (uint32_t)(kv & kLab);
-        const uint32_t cnt = counts[B.base + l];
-        const bool ex = excl ? excl[B.base + l] != 0 : false;
-        const bool keep = l != 0 && (cnt >= size_filter || ex);
-        if (valid) {
-            if (keep) {
-                if (!fx) {
-                    key[gi] = ((uint64_t)ordf(hv) << 32) | (uint64_t)l;
-                    fixedv[gi] = 1;
+    // word tiles (a wave's ballot is exactly one word of the open / changed bitmaps), U words per
+    // step: the loads of the U words, then their dependent count loads, in flight together
+    constexpr int U = 4;
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
+        int64_t gi[U];
+        bool valid[U];
+        int zs[U];
+        uint64_t kv[U];
+        uint8_t fx[U];
+        float hv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = (w0 + u) / wpr;
+            const int x = (int)(w0 + u - row * wpr) * 64 + lane;
+            valid[u] = w0 + u < wend && x < B.X;
+            zs[u] = (int)(row / B.Y);
+            // loads unconditional (clamped index): key, seed flag and height together
+            gi[u] = B.base + (valid[u] ? row * B.X + x : 0);
+            kv[u] = key[gi[u]];
+            fx[u] = fixedv[gi[u]];
+            hv[u] = h[gi[u]];
+        }
+        uint32_t lb[U], cnt[U];
+        bool ex[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!valid[u]) {
+                kv[u] = kInfKey;
+                fx[u] = 0;
+            }
+            lb[u] = kv[u] == kInfKey ? 0u : (uint32_t)(kv[u] & kLab);
+            cnt[u] = counts[B.base + lb[u]];
+            ex[u] = excl ? excl[B.base + lb[u]] != 0 : false;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool keep = lb[u] != 0 && (cnt[u] >= size_filter || ex[u]);
+            if (valid[u]) {
+                if (keep) {
+                    if (!fx[u]) {
+                        key[gi[u]] = ((uint64_t)ordf(hv[u]) << 32) | (uint64_t)lb[u];
+                        fixedv[gi[u]] = 1;
+                    }
+                } else {
+                    if (kv[u] != kInfKey) key[gi[u]] = kInfKey;
+                    if (fx[u]) fixedv[gi[u]] = 0;
                 }
-            } else {
-                if (kv != kInfKey) key[gi] = kInfKey;
-                if (fx) fixedv[gi] = 0;
+            }
+            const uint64_t op = __ballot(valid[u] && !keep);
+            const uint64_t kp = __ballot(valid[u] && keep);
+            if (lane == 0 && w0 + u < wend) {
+                open[B.fbase + w0 + u] = op;
+                chg[B.fbase + w0 + u] = kp;
+                if (kp) {
+                    uint32_t* sv = survivors + B.sbase + (B.nd_ws == 2 ? zs[u] : 0);
+                    if (!*sv) *sv = 1;
+                }
             }
         }
-        const uint64_t op = __ballot(valid && !keep);
-        const uint64_t kp = __ballot(valid && keep);
-        if (lane == 0) {
-            open[B.fbase + w_] = op;
-            chg[B.fbase + w_] = kp;
-            if (kp) {
-                uint32_t* sv = survivors + B.sbase + (B.nd_ws == 2 ? z : 0);
-                if (!*sv) *sv = 1;
-            }
-        }
-    })
+    }
 }
 
 // Auto-seeded regrow: a slice (2-D) / block (3-D) whose every segment was removed leaves
