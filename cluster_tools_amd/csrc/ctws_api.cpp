@@ -137,7 +137,9 @@ struct ctws_handle {
     int host_batch_blocks = 0;  // CTWS_HOST_BATCH_BLOCKS: cap on blocks per host-path batch (0: voxel cap)
     int64_t host_batch_voxels = (int64_t)256 << 20;  // CTWS_HOST_BATCH_VOXELS: smaller batches pipeline better  // CTWS_HOST_THREADS: memcpy threads per direction of the host path  // CTWS_D2H_WGS: workgroups of the device-to-host copy kernel (0: hipMemcpyAsync)  // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
-    int frontier_unroll = 1;  // CTWS_FRONTIER_UNROLL (1, 2, 4, 8): list entries per lane in flight
+    // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words)
+    int fchunk2[3] = {1, 64, 1};
+    int fchunk3[3] = {1, 8, 8};
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
@@ -209,7 +211,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(Bf, vox);
         ALLOC(sm, vox);
         ALLOC(hm, vox);
-        ALLOC(cls, vox);
+        ALLOC(cls, vox + 16);  // k_plateau_flag reads aligned 16-byte groups
         ALLOC(P, vox);
         ALLOC(PF, vox);
         ALLOC(lab, vox);
@@ -493,6 +495,16 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
 
 // ---- flood rounds until no tile is active -----------------------------------------------
 // tile extents of k_flood_packed (PTile) and k_flood (FloodTile)
+// frontier chunk bricks instantiated in k_flood.hip (CTWS_FRONTIER_SHAPES below): index or -1
+int frontier_chunk_kind(int nd, int cw, int cy, int cz) {
+    static const int shapes[9][4] = {{2, 1, 64, 1}, {2, 2, 32, 1}, {2, 4, 16, 1}, {2, 8, 8, 1}, {3, 1, 8, 8},
+                                     {3, 2, 8, 4},  {3, 1, 16, 4}, {3, 4, 4, 4},  {3, 8, 8, 1}};
+    for (int k = 0; k < 9; ++k)
+        if (shapes[k][0] == nd && shapes[k][1] == cw && shapes[k][2] == cy && shapes[k][3] == cz) return k;
+    return -1;
+}
+bool frontier_chunk_ok(int nd, int cw, int cy, int cz) { return frontier_chunk_kind(nd, cw, cy, cz) >= 0; }
+
 void flood_tile_dims(int nd, bool packed, int* tz, int* ty, int* tx) {
     *tz = nd == 3 ? (packed ? 16 : 4) : (packed ? 4 : 1);
     *ty = nd == 3 ? (packed ? 16 : 8) : 32;
@@ -586,7 +598,15 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     // iteration 0: every chunk with an open voxel
     const dim3 lg((unsigned)std::min<int64_t>((TF / nb + 64 * 64 * kFrontierWavesHost - 1) / (64 * 64 * kFrontierWavesHost) + 1,
                                               1024), nb);
-    k_frontier_list0<<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt);
+    const int* fc = pl.nd_ws == 3 ? h->fchunk3 : h->fchunk2;
+    const int fkind = frontier_chunk_kind(pl.nd_ws, fc[0], fc[1], fc[2]);
+#define CTWS_FRONTIER_SHAPES(X) \
+    X(0, 2, 1, 64, 1) X(1, 2, 2, 32, 1) X(2, 2, 4, 16, 1) X(3, 2, 8, 8, 1) X(4, 3, 1, 8, 8) X(5, 3, 2, 8, 4) \
+    X(6, 3, 1, 16, 4) X(7, 3, 4, 4, 4) X(8, 3, 8, 8, 1)
+#define CTWS_LIST0(K, ND, CW, CY, CZ) \
+    case K: k_frontier_list0<CW, CY, CZ><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt); break;
+    switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_LIST0) default: h->err = "bad frontier chunk"; return CTWS_EINVAL; }
+#undef CTWS_LIST0
     LAUNCHCHK();
     // one wave per list entry; the largest list is every chunk of the batch
     const unsigned fg = (unsigned)std::min<int64_t>((nch + kFrontierWavesHost - 1) / kFrontierWavesHost, 2048);
@@ -603,21 +623,14 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
         }
         for (int k = 0; k < nl; ++k) {
             const int it = it0 + k;
-#define CTWS_FRONTIER(ND, U)                                                                                       \
-    k_frontier<ND, U><<<fg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], \
-                                                 gen[(it + 1) & 1], gen[it & 1], it, wl[it & 1], w.wlcnt + it,      \
-                                                 wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen,                        \
-                                                 fst ? fst + nb : nullptr, h->frontier_reps)
-            const int fu = h->frontier_unroll;
-            if (pl.nd_ws == 3) {
-                if (fu == 2) CTWS_FRONTIER(3, 2);
-                else if (fu == 4) CTWS_FRONTIER(3, 4);
-                else CTWS_FRONTIER(3, 1);
-            } else {
-                if (fu == 2) CTWS_FRONTIER(2, 2);
-                else if (fu == 4) CTWS_FRONTIER(2, 4);
-                else CTWS_FRONTIER(2, 1);
-            }
+#define CTWS_FRONTIER(K, ND, CW, CY, CZ)                                                                            \
+    case K:                                                                                                         \
+        k_frontier<ND, CW, CY, CZ><<<fg, 256, 0, h->stream>>>(                                                      \
+            w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
+            wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
+            h->frontier_reps);                                                                                      \
+        break;
+            switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_FRONTIER) }
 #undef CTWS_FRONTIER
             if (h->trace) hipEventRecord(tev[k + 1], h->stream);
         }
@@ -643,6 +656,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
             }
         }
     }
+#undef CTWS_FRONTIER_SHAPES
     *iters_out += fiters;
     if (!converged) {
         int TZ, TY, TX;
@@ -886,9 +900,14 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             d.rbase = TR;
             TR += (int64_t)((d.Z + rz - 1) / rz) * ((d.Y + ry - 1) / ry) * ((d.X + rx - 1) / rx);
         }
-        // frontier bitmaps: rows padded to a multiple of 64, so that the block's chunks (64 rows
-        // x one word column, k_frontier) are exactly its words / 64
-        TF += (((int64_t)d.Z * d.Y + 63) / 64) * 64 * ((d.X + 63) / 64);
+        // frontier bitmaps: rows padded to a multiple of 64, and at least 64 words per frontier
+        // chunk brick (k_frontier), so that the per-chunk arrays can be indexed at fbase / 64
+        {
+            const int* fc = pl.nd_ws == 3 ? h->fchunk3 : h->fchunk2;
+            const int64_t wpr = (d.X + 63) / 64;
+            const int64_t nch = ((wpr + fc[0] - 1) / fc[0]) * ((d.Y + fc[1] - 1) / fc[1]) * ((d.Z + fc[2] - 1) / fc[2]);
+            TF += std::max((((int64_t)d.Z * d.Y + 63) / 64) * 64 * wpr, nch * 64);
+        }
         T += d.N;
         TI += d.NI;
         TW += words_of(d.N);
@@ -1156,7 +1175,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
     {
-        k_localmax<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
+        k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
         LAUNCHCHK();
         // plateaus (equal-valued maxima candidates) and the seed CC: LDS tile union-find
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
@@ -1181,7 +1200,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         LAUNCHCHK();
     }
     HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-    k_flatten_roots<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
+    k_flatten_roots<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
     k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
@@ -1260,8 +1279,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
             const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
             const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
-            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
-            else k_descent_tile<2><<<dg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
+            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
+            else k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
             LAUNCHCHK();
         }
         mark("descent_tile");
@@ -1489,7 +1508,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 k_tile_merge<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             }
             HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-            k_flatten_roots<<<rig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
+            k_flatten_roots<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
             k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
             k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
             k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
@@ -1985,7 +2004,16 @@ int ctws_open(int device, ctws_handle** out) {
         const int v = std::atoi(t);
         h->edt_w = (v == 8 || v == 16 || v == 32) ? v : 0;
     }
-    if (const char* t = std::getenv("CTWS_FRONTIER_UNROLL")) h->frontier_unroll = std::atoi(t);
+    auto parse_chunk = [](const char* t, int* c, bool three_d) {
+        int a = 0, b = 0, d = 0;
+        if (std::sscanf(t, "%dx%dx%d", &a, &b, &d) == 3 && frontier_chunk_ok(three_d ? 3 : 2, a, b, d)) {
+            c[0] = a;
+            c[1] = b;
+            c[2] = d;
+        }
+    };
+    if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK2D")) parse_chunk(t, h->fchunk2, false);
+    if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK3D")) parse_chunk(t, h->fchunk3, true);
     if (const char* t = std::getenv("CTWS_RELAX")) h->relax = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||

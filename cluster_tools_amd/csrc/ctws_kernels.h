@@ -127,7 +127,7 @@ __global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*,
                                uint32_t*);
 __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint8_t*,
                                uint64_t*, uint64_t*, uint32_t*);
-template <int ND, int U>
+template <int ND, int CW, int CY, int CZ>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
                            const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
@@ -157,6 +157,7 @@ __global__ void k_relax_list0(const BlockDesc*, const BlockStat*, const uint64_t
 template <int ND>
 __global__ void k_tile_relax(const BlockDesc*, const float*, uint64_t*, const uint64_t*, const uint64_t*,
                              const uint32_t*, uint64_t*, uint32_t*, uint32_t*, int, uint32_t*);
+template <int CW, int CY, int CZ>
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>

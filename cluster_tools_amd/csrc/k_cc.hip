@@ -47,60 +47,121 @@ namespace ctws {
 // ---- local maxima classification ---------------------------------------------------------
 // cls bit0: a neighbour is strictly greater; bit1: a neighbour is equal (plateau voxel).
 // Neighbourhood: 6 (3-D ws) or 8 in-plane (2-D ws), as localMaxima3D / localMaxima.
+// Word tiles (wtg grid): a wave classifies 64 consecutive voxels of a row per word, U words
+// per step with every load of the step in flight together (clamped positions, no branches
+// between them).  The x neighbours come from the neighbouring lanes; lane 0 / 63 fetch the
+// voxel left / right of the word with one extra load per row.
+template <int ND>
+__device__ __forceinline__ void localmax_words(const BlockDesc& B, const float* __restrict__ p, uint8_t* __restrict__ cl,
+                                               uint32_t& nplat) {
+    constexpr int U = 4;
+    const int Y = B.Y, X = B.X, Z = B.Z;
+    const int64_t YX = (int64_t)Y * X;
+    const int wpr = (X + 63) >> 6;
+    const int64_t nwords = (int64_t)Z * Y * wpr;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    const float NEG = -__builtin_huge_valf();
+    const gptr_t<float> gp = gbl(p);
+    constexpr int NR = ND == 3 ? 1 : 3;  // rows whose x neighbours are needed: y-1, y, y+1 (2-D)
+    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
+        float c[U], up[U], dn[U], zm[U], zp[U], e[U][NR];
+        int64_t ii[U];
+        bool valid[U], yl[U], yh[U], zl[U], zh[U];
+        int xx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t wu = min(w0 + u, wend - 1);
+            const int64_t row = wu / wpr;
+            const int xw = (int)(wu - row * wpr);
+            const int z = (int)(row / Y), y = (int)(row - (int64_t)z * Y);
+            const int x = xw * 64 + lane;
+            valid[u] = w0 + u < wend && x < X;
+            const int xc = min(x, X - 1);
+            xx[u] = x;
+            const int64_t i = row * X + xc;
+            ii[u] = i;
+            yl[u] = y > 0;
+            yh[u] = y + 1 < Y;
+            zl[u] = z > 0;
+            zh[u] = z + 1 < Z;
+            c[u] = gp[i];
+            up[u] = gp[i - (yl[u] ? X : 0)];
+            dn[u] = gp[i + (yh[u] ? X : 0)];
+            if (ND == 3) {
+                zm[u] = gp[i - (zl[u] ? YX : 0)];
+                zp[u] = gp[i + (zh[u] ? YX : 0)];
+            }
+            // lane 0: the voxel left of the word, every other lane: right of it (lane 63's is
+            // the only one used); clamped into the row
+            const int64_t ie = row * X + (lane == 0 ? max(xc - 1, 0) : min(xc + 1, X - 1));
+            e[u][0] = gp[ie];
+            if (ND == 2) {
+                e[u][1] = gp[ie - (yl[u] ? X : 0)];
+                e[u][2] = gp[ie + (yh[u] ? X : 0)];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int x = xx[u];
+            const bool xl = x > 0, xh = x + 1 < X;
+            // x neighbours of row r (centre, up, down): lanes +-1, the word edges from e[]
+            auto left = [&](float v, float ev) {
+                const float t = __shfl(v, (lane + 63) & 63);
+                return lane == 0 ? ev : t;
+            };
+            auto right = [&](float v, float ev) {
+                const float t = __shfl(v, (lane + 1) & 63);
+                return lane == 63 ? __shfl(ev, 63) : t;
+            };
+            const float cc = c[u];
+            float w[8];
+            if (ND == 3) {
+                w[0] = zl[u] ? zm[u] : NEG;
+                w[1] = zh[u] ? zp[u] : NEG;
+                w[2] = yl[u] ? up[u] : NEG;
+                w[3] = yh[u] ? dn[u] : NEG;
+                const float l = left(cc, e[u][0]), r = right(cc, __shfl(e[u][0], 63));
+                w[4] = xl ? l : NEG;
+                w[5] = xh ? r : NEG;
+                w[6] = w[7] = NEG;
+            } else {
+                const float lc = left(cc, e[u][0]), rc = right(cc, e[u][0]);
+                const float lu = left(up[u], e[u][1]), ru = right(up[u], e[u][1]);
+                const float ld = left(dn[u], e[u][2]), rd = right(dn[u], e[u][2]);
+                w[0] = yl[u] && xl ? lu : NEG;
+                w[1] = yl[u] ? up[u] : NEG;
+                w[2] = yl[u] && xh ? ru : NEG;
+                w[3] = xl ? lc : NEG;
+                w[4] = xh ? rc : NEG;
+                w[5] = yh[u] && xl ? ld : NEG;
+                w[6] = yh[u] ? dn[u] : NEG;
+                w[7] = yh[u] && xh ? rd : NEG;
+            }
+            bool gt = false, eq = false;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                gt |= w[k] > cc;
+                eq |= w[k] == cc;
+            }
+            if (valid[u]) cl[ii[u]] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
+            nplat += valid[u] && eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ D, BlockStat* S,
                                                   const float* __restrict__ v, uint8_t* __restrict__ cls,
                                                   uint32_t* __restrict__ Pp) {
+    (void)Pp;
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const int Y = B.Y, X = B.X, Z = B.Z;
-    const int64_t YX = (int64_t)Y * X;
-    const float* __restrict__ p = v + B.base;
-    uint8_t* __restrict__ cl = cls + B.base;
     uint32_t nplat = 0;
-    const float NEG = -__builtin_huge_valf();
-    const gptr_t<float> gp = gbl(p);
-    ROW_TILES(Z, Y, X, {
-        // neighbour loads at clamped positions (unconditional: all in flight together), the
-        // positions outside the block selected away
-        const int64_t ic = i;
-        const int xq = x;
-        const bool valid = true;
-        const float c = gp[ic];
-        float w[8];
-        const bool yl = y > 0, yh = y + 1 < Y, xl = xq > 0, xh = xq + 1 < X;
-        const int64_t dym = yl ? X : 0, dyp = yh ? X : 0;
-        const int64_t dxm = xl ? 1 : 0, dxp = xh ? 1 : 0;
-        if (B.nd_ws == 3) {
-            const bool zl = z > 0, zh = z + 1 < Z;
-            const float a0 = gp[ic - (zl ? YX : 0)], a1 = gp[ic + (zh ? YX : 0)];
-            const float a2 = gp[ic - dym], a3 = gp[ic + dyp], a4 = gp[ic - dxm], a5 = gp[ic + dxp];
-            w[0] = zl ? a0 : NEG;
-            w[1] = zh ? a1 : NEG;
-            w[2] = yl ? a2 : NEG;
-            w[3] = yh ? a3 : NEG;
-            w[4] = xl ? a4 : NEG;
-            w[5] = xh ? a5 : NEG;
-            w[6] = w[7] = NEG;
-        } else {
-            const float a0 = gp[ic - dym - dxm], a1 = gp[ic - dym], a2 = gp[ic - dym + dxp], a3 = gp[ic - dxm];
-            const float a4 = gp[ic + dxp], a5 = gp[ic + dyp - dxm], a6 = gp[ic + dyp], a7 = gp[ic + dyp + dxp];
-            w[0] = yl && xl ? a0 : NEG;
-            w[1] = yl ? a1 : NEG;
-            w[2] = yl && xh ? a2 : NEG;
-            w[3] = xl ? a3 : NEG;
-            w[4] = xh ? a4 : NEG;
-            w[5] = yh && xl ? a5 : NEG;
-            w[6] = yh ? a6 : NEG;
-            w[7] = yh && xh ? a7 : NEG;
-        }
-        bool gt = false, eq = false;
-        _Pragma("unroll") for (int k = 0; k < 8; ++k) {
-            gt |= w[k] > c;
-            eq |= w[k] == c;
-        }
-        if (valid) cl[i] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
-        nplat += valid && eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
-    })
+    if (B.nd_ws == 3) localmax_words<3>(B, v + B.base, cls + B.base, nplat);
+    else localmax_words<2>(B, v + B.base, cls + B.base, nplat);
     nplat = wg_reduce_u32(nplat, OpAdd());
     if (threadIdx.x == 0 && nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
 }
@@ -112,11 +173,25 @@ __global__ void __launch_bounds__(256) k_plateau_flag(const BlockDesc* __restric
     if (!S[blockIdx.y].active || !S[blockIdx.y].plateau) return;
     uint8_t* cl = cls + B.base;
     uint32_t* P = Pg + B.base;
-    BLOCK_LOOP(i, B) {
-        const uint8_t c = cl[i];
-        if ((c & 3) == 3) {
-            const uint32_t r = uf_find_compress(P, (uint32_t)i);
-            cl[r] |= 4;  // benign race: every writer sets the same bit
+    // 16 classes per thread: aligned 16-byte loads over the block's byte range (plateau voxels
+    // are rare, so nearly every load is the whole work)
+    const int64_t a0 = B.base >> 4, a1 = (B.base + B.N + 15) >> 4;
+    const uint4* c16 = reinterpret_cast<const uint4*>(cls);
+    for (int64_t a = a0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < a1; a += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 q = c16[a];
+        const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // bytes with both bit 0 and bit 1 set
+            uint32_t m = wv[k] & (wv[k] >> 1) & 0x01010101u;
+            while (m) {
+                const int b = __builtin_ctz(m) >> 3;
+                m &= m - 1u;
+                const int64_t i = a * 16 + k * 4 + b - B.base;
+                if (i < 0 || i >= B.N) continue;
+                const uint32_t r = uf_find_compress(P, (uint32_t)i);
+                cl[r] |= 4;  // benign race: every writer sets the same bit
+            }
         }
     }
 }
@@ -334,7 +409,9 @@ __global__ void __launch_bounds__(256) k_count_ids(const BlockDesc* __restrict__
 }
 
 // point every element of a union-find forest directly at its root; roots set their scan-key
-// bit in the root bitmap W (zeroed beforehand)
+// bit in the root bitmap W (zeroed beforehand).  Word tiles (wtg / wtig grid), U words per
+// step with their parent loads in flight together; most voxels are kNoParent or point at
+// their root already and cost the one load.
 __global__ void __launch_bounds__(256) k_flatten_roots(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
                                                        uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg) {
     const BlockDesc& B = D[blockIdx.y];
@@ -342,15 +419,45 @@ __global__ void __launch_bounds__(256) k_flatten_roots(const BlockDesc* __restri
     uint32_t* P = PFg + (inner ? B.ibase : B.base);
     uint64_t* W = Wg + B.wbase;
     const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
-    ROW_TILES(nz, ny, nx, {
-        const uint32_t p = gbl(P)[i];
-        if (p == (uint32_t)i) {
-            const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
-            atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
-        } else if (p != kNoParent) {
-            P[i] = uf_find(P, p);
+    constexpr int U = 4;
+    const int wpr = (nx + 63) >> 6;
+    const int64_t nwords = (int64_t)nz * ny * wpr;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
+        uint32_t pv[U];
+        int64_t ii[U];
+        int xx[U], yy[U], zz[U];
+        bool valid[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t wu = min(w0 + u, wend - 1);
+            const int64_t row = wu / wpr;
+            const int xw = (int)(wu - row * wpr);
+            zz[u] = (int)(row / ny);
+            yy[u] = (int)(row - (int64_t)zz[u] * ny);
+            xx[u] = xw * 64 + lane;
+            valid[u] = w0 + u < wend && xx[u] < nx;
+            ii[u] = row * nx + min(xx[u], nx - 1);
+            pv[u] = gbl(P)[ii[u]];
         }
-    })
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!valid[u]) continue;
+            const uint32_t p = pv[u];
+            if (p == (uint32_t)ii[u]) {
+                const int z = zz[u], y = yy[u], x = xx[u];
+                const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
+                atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
+            } else if (p != kNoParent) {
+                const uint32_t r = uf_find(P, p);
+                if (r != p) P[ii[u]] = r;
+            }
+        }
+    }
 }
 
 }  // namespace ctws

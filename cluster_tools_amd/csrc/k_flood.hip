@@ -549,6 +549,9 @@ __device__ __forceinline__ uint32_t seed_label(const uint32_t* lab, const uint32
     return (l & kFixedBit) ? (l & ~kFixedBit) : 0u;
 }
 
+// threads per descent tile (4096 voxels): 512 keeps the per-thread arrays at 8 voxels
+constexpr int kDescThreads = 512;
+
 template <int ND>
 struct DTile;
 template <>
@@ -561,7 +564,7 @@ struct DTile<2> {
 };
 
 template <int ND>
-__global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restrict__ D, const BlockStat* S,
+__global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_eu(ND == 2 ? 8 : 6, 8))) k_descent_tile(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint32_t* __restrict__ lab,
                                                       const uint32_t* __restrict__ cc, uint32_t* __restrict__ exitp) {
     using T = DTile<ND>;
@@ -582,8 +585,8 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
     const int64_t YX = (int64_t)B.Y * B.X;
     const float* hb = h + B.base;
-    constexpr int PER = TN / 256;  // voxels per thread: c = threadIdx.x + k * 256
-    static_assert(TN % 256 == 0 && PER <= 32, "");
+    constexpr int NT = kDescThreads, PER = TN / NT;  // voxels per thread: c = threadIdx.x + k * NT
+    static_assert(TN % NT == 0 && PER <= 32, "");
     // seed entries of the thread's voxels (cc parent or lab), then the halo heights: every load
     // unconditional (clamped index, global address space) so that all of them are in flight
     // together; out-of-block values are selected away afterwards
@@ -592,18 +595,18 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     uint32_t sv[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const int c = threadIdx.x + k * 256;
+        const int c = threadIdx.x + k * NT;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = min(z0 + lz, B.Z - 1), gy = min(y0 + ly, B.Y - 1), gx = min(x0 + lx, B.X - 1);
         inm |= ((z0 + lz < B.Z && y0 + ly < B.Y && x0 + lx < B.X) ? 1u : 0u) << k;
         sv[k] = gbl(sdsrc)[B.base + gz * YX + (int64_t)gy * B.X + gx];
     }
     {
-        constexpr int NH = (HN + 255) / 256;
+        constexpr int NH = (HN + NT - 1) / NT;
         uint32_t hv[NH];
 #pragma unroll
         for (int k = 0; k < NH; ++k) {
-            const int c = min((int)threadIdx.x + k * 256, HN - 1);
+            const int c = min((int)threadIdx.x + k * NT, HN - 1);
             const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
             const int gz = z0 + hz - ZOFF, gy = y0 + hy - 1, gx = x0 + hx - 1;
             const int cz = min(max(gz, 0), B.Z - 1), cy = min(max(gy, 0), B.Y - 1), cx = min(max(gx, 0), B.X - 1);
@@ -611,7 +614,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
         }
 #pragma unroll
         for (int k = 0; k < NH; ++k) {
-            const int c = (int)threadIdx.x + k * 256;
+            const int c = (int)threadIdx.x + k * NT;
             if (c < HN) {
                 const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
                 const int gz = z0 + hz - ZOFF, gy = y0 + hy - 1, gx = x0 + hx - 1;
@@ -629,7 +632,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     // parents
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const int c = threadIdx.x + k * 256;
+        const int c = threadIdx.x + k * NT;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         int p = c;
         if (((inm & ~seedm) >> k) & 1u) {
@@ -668,7 +671,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
         bool moved = false;
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int c = threadIdx.x + k * 256;
+            const int c = threadIdx.x + k * NT;
             const int p = sp[c];
             if (p < TN) {
                 const int pp = sp[p];
@@ -693,7 +696,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
         }
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int c = threadIdx.x + k * 256;
+            const int c = threadIdx.x + k * NT;
             const uint32_t v = sv[k];
             uint32_t l = 0u;
             if ((seedm >> k) & 1u) {
@@ -708,7 +711,7 @@ __global__ void __launch_bounds__(256) k_descent_tile(const BlockDesc* __restric
     // index of the first voxel outside the tile (k_descent_init follows it)
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        const int c = threadIdx.x + k * 256;
+        const int c = threadIdx.x + k * NT;
         if (!((inm >> k) & 1u)) continue;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
@@ -806,17 +809,42 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
 // One iteration of the frontier relaxation.  frontier = (neighbours of the voxels changed in
 // the previous iteration) & open; every frontier voxel recomputes K = f(min of its
 // neighbours' keys) in place (a stale read is repaired by the next iteration, as the
-// neighbour's change is recorded).  Work is a list of 64-word chunks (one wave per entry):
-// the chunks that contain open voxels in iteration 0, afterwards the chunks next to a chunk
-// that changed in the previous iteration — so a late iteration with a handful of active
-// chunks costs a handful of waves, not a pass over every chunk of the batch.  A wave builds
-// its chunk's frontier from the previous changed bitmap, expands the set bits into an LDS
-// list and relaxes 64 voxels per step, one per lane; its changed bits collect in LDS and are
-// stored whole.  Chunk generations instead of cleared flags: gen[it & 1][ch] = it + 1 when
-// chunk ch changed in iteration it, so a word of the previous changed bitmap is valid iff
-// gen[(it + 1) & 1][ch] == it; qgen[ch] = it + 1 when ch is queued for iteration it + 1.
+// neighbour's change is recorded).
+//
+// Work unit: a *chunk*, a brick of 64 bitmap words (one per lane) — CW words along x, CY rows
+// along y, CZ slices along z (FChunk; 2-D ws: CZ = 1) — so that a front crosses up to 64
+// voxels in x and CY / CZ in y / z inside one launch.  The list holds the chunks that contain
+// open voxels in iteration 0, afterwards the chunks next to a chunk change, so a late
+// iteration with a handful of active chunks costs a handful of waves.  A wave builds its
+// chunk's frontier from the previous changed bitmap, expands the set bits into an LDS list and
+// relaxes 64 voxels per step, one per lane; then it sweeps locally (the in-chunk neighbours of
+// this sweep's changes) until nothing changes or `reps` sweeps are done.  Its changed bits
+// collect in LDS and are stored whole.
+//
+// Chunk generations instead of cleared flags: gen[it & 1][ch] = (it + 1) | kGenConv? when
+// chunk ch changed in iteration it, so a word of the previous changed bitmap is valid iff its
+// chunk's generation is it.  kGenConv marks a chunk whose local sweeps converged: every
+// in-chunk neighbour of each of its changes was re-evaluated after that change by the same
+// wave, so the chunk neither queues itself nor rebuilds its own frontier from its own words
+// (its words still feed the neighbouring chunks).  qgen[ch] = it + 1 when ch is queued for
+// iteration it + 1.  Neighbour chunks are queued only when a change lies on the shared face.
 constexpr int kFrontierWaves = 4;
 constexpr uint32_t kWlChunkBits = 20;  // list entry = block << 20 | chunk
+constexpr uint32_t kGenConv = 0x80000000u;
+
+// chunk grid of a block (words along x, rows, slices) for brick CW x CY x CZ
+template <int CW, int CY, int CZ>
+struct FChunk {
+    static_assert(CW * CY * CZ == 64, "a chunk is 64 words");
+    int wpr, ncx, ncy, ncz;
+    __device__ FChunk(const BlockDesc& B) {
+        wpr = (B.X + 63) >> 6;
+        ncx = (wpr + CW - 1) / CW;
+        ncy = (B.Y + CY - 1) / CY;
+        ncz = (B.Z + CZ - 1) / CZ;
+    }
+    __device__ int64_t count() const { return (int64_t)ncx * ncy * ncz; }
+};
 
 // position of the k-th (0-based) set bit of w (k < popcount(w))
 __device__ __forceinline__ int kth_set_bit(uint64_t w, int k) {
@@ -837,24 +865,34 @@ __device__ __forceinline__ int kth_set_bit(uint64_t w, int k) {
 }
 
 // iteration-0 list: every chunk holding an open voxel.  A wave takes 64 consecutive chunks,
-// reads each one's 64 words coalesced (one word per lane) and appends the non-empty ones with
-// one atomic.
+// reads each one's 64 words (one word per lane) and appends the non-empty ones with one atomic.
+template <int CW, int CY, int CZ>
 __global__ void __launch_bounds__(256) k_frontier_list0(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                         const uint64_t* __restrict__ open, uint32_t* __restrict__ list,
                                                         uint32_t* __restrict__ cnt) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int lane = threadIdx.x & 63;
-    const int64_t nwords = (int64_t)B.Z * B.Y * ((B.X + 63) >> 6);
-    const int64_t nch = (nwords + 63) >> 6;
+    const int lx = lane % CW, ly = (lane / CW) % CY, lz = lane / (CW * CY);
+    const FChunk<CW, CY, CZ> G(B);
+    const int64_t nch = G.count();
     const uint64_t* op = open + B.fbase;
     for (int64_t c0 = ((int64_t)blockIdx.x * kFrontierWaves + (threadIdx.x >> 6)) * 64; c0 < nch;
          c0 += (int64_t)gridDim.x * kFrontierWaves * 64) {
         uint64_t m = 0ull;  // bit k: chunk c0 + k holds an open voxel
+        int cx = (int)(c0 % G.ncx), cy = (int)((c0 / G.ncx) % G.ncy), cz = (int)(c0 / ((int64_t)G.ncx * G.ncy));
         for (int k = 0; k < 64 && c0 + k < nch; ++k) {
-            const int64_t wi = (c0 + k) * 64 + lane;
-            const bool any = __ballot(wi < nwords && op[wi] != 0ull) != 0ull;
+            const int xw = cx * CW + lx, y = cy * CY + ly, z = cz * CZ + lz;
+            const bool ok = xw < G.wpr && y < B.Y && z < B.Z;
+            const bool any = __ballot(ok && op[((int64_t)z * B.Y + y) * G.wpr + xw] != 0ull) != 0ull;
             m |= (any ? 1ull : 0ull) << k;
+            if (++cx == G.ncx) {
+                cx = 0;
+                if (++cy == G.ncy) {
+                    cy = 0;
+                    ++cz;
+                }
+            }
         }
         if (!m) continue;
         uint32_t base = 0;
@@ -865,7 +903,7 @@ __global__ void __launch_bounds__(256) k_frontier_list0(const BlockDesc* __restr
     }
 }
 
-template <int ND, int kFrontierUnroll>
+template <int ND, int CW, int CY, int CZ>
 __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                   const float* __restrict__ h, uint64_t* __restrict__ key,
                                                   const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
@@ -874,22 +912,26 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                                   const uint32_t* __restrict__ cnt, uint32_t* __restrict__ list_next,
                                                   uint32_t* __restrict__ cnt_next, uint32_t* __restrict__ qgen,
                                                   uint32_t* __restrict__ nvisit, int reps) {
+    static_assert(ND == 3 || CZ == 1, "2-D ws: slices are independent, chunks are one slice deep");
     __shared__ uint64_t schg[kFrontierWaves][64];
     __shared__ uint64_t sfw[kFrontierWaves][64];
     __shared__ int spre[kFrontierWaves][64];
     __shared__ int srow[kFrontierWaves][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lx = lane % CW, ly = (lane / CW) % CY, lz = lane / (CW * CY);
     const uint32_t n_entries = *cnt;
-    const uint32_t prev_gen = (uint32_t)it;  // gprev[ch] == it: changed in iteration it - 1
+    const uint32_t prev_gen = (uint32_t)it;  // gprev[ch] & ~kGenConv == it: changed in iteration it - 1
     for (uint32_t e0 = blockIdx.x * kFrontierWaves + wv; e0 < n_entries; e0 += gridDim.x * kFrontierWaves) {
         const uint32_t ent = list[e0];
         const int bi = (int)(ent >> kWlChunkBits);
-        const int64_t ch0 = ent & ((1u << kWlChunkBits) - 1u);
+        // word and chunk indices fit 32 bits (Z * Y * wpr < 2^27, chunks < 2^20)
+        const int ch0 = (int)(ent & ((1u << kWlChunkBits) - 1u));
         const BlockDesc& B = D[bi];
-        const int wpr = (B.X + 63) >> 6;
-        const int64_t ws = (int64_t)B.Y * wpr;
-        const int64_t nwords = (int64_t)B.Z * ws;
+        const FChunk<CW, CY, CZ> G(B);
+        const int wpr = G.wpr;
+        const int ws = B.Y * wpr;
         const int64_t YX = (int64_t)B.Y * B.X;
+        const int cplane = G.ncx * G.ncy;
         const uint64_t* cp = cprev + B.fbase;
         const uint64_t* op = open + B.fbase;
         uint64_t* cn = cnext + B.fbase;
@@ -898,52 +940,60 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
         const uint32_t* gp = gprev + (B.fbase >> 6);
         uint32_t* gn = gnext + (B.fbase >> 6);
         uint32_t* qg = qgen + (B.fbase >> 6);
-        const int64_t nchunks = (nwords + 63) >> 6;
-        // word w of the previous changed bitmap (0 unless its chunk changed in iteration it - 1).
-        // All generation and word loads are unconditional (clamped word index, global address
+        const int cx = (int)(ch0 % G.ncx), cy = (int)((ch0 / G.ncx) % G.ncy), cz = (int)(ch0 / cplane);
+        const int xw = cx * CW + lx, yy = cy * CY + ly, zz = cz * CZ + lz;
+        const bool wok = xw < wpr && yy < B.Y && zz < B.Z;
+        const int wc = wok ? (zz * B.Y + yy) * wpr + xw : 0;
+        const int row = zz * B.Y + yy;
+        // word k of the lane's neighbourhood and the chunk holding it; previous changed words
+        // count only when their chunk changed in iteration it - 1 (own chunk: and did not
+        // converge).  All generation and word loads are unconditional (clamped, global address
         // space) and issued together; the neighbours outside the block are selected away.
-        const int64_t w0 = ch0 * 64;
-        const int64_t wl = w0 + lane;
-        const bool wok = wl < nwords;
-        const int64_t wc = wok ? wl : nwords - 1;
-        const int row = (int)(wc / wpr);
-        const int xw = (int)(wc - (int64_t)row * wpr);
-        const int zz = row / B.Y, yy = row - zz * B.Y;
         constexpr int NW = ND == 3 ? 7 : 5;
-        int64_t wi[NW];
+        int wi[NW], ci[NW];
         bool ok[NW];
         wi[0] = wc;
+        ci[0] = ch0;
         ok[0] = wok;
         wi[1] = wc - 1;
+        ci[1] = lx == 0 ? ch0 - 1 : ch0;
         ok[1] = wok && xw > 0;
         wi[2] = wc + 1;
+        ci[2] = lx == CW - 1 ? ch0 + 1 : ch0;
         ok[2] = wok && xw + 1 < wpr;
         wi[3] = wc - wpr;
+        ci[3] = ly == 0 ? ch0 - G.ncx : ch0;
         ok[3] = wok && yy > 0;
         wi[4] = wc + wpr;
+        ci[4] = ly == CY - 1 ? ch0 + G.ncx : ch0;
         ok[4] = wok && yy + 1 < B.Y;
         if (ND == 3) {
             wi[5] = wc - ws;
+            ci[5] = lz == 0 ? ch0 - cplane : ch0;
             ok[5] = wok && zz > 0;
             wi[6] = wc + ws;
+            ci[6] = lz == CZ - 1 ? ch0 + cplane : ch0;
             ok[6] = wok && zz + 1 < B.Z;
         }
         uint32_t gv[NW];
         uint64_t cv[NW];
 #pragma unroll
         for (int k = 0; k < NW; ++k) {
-            const int64_t w = ok[k] ? wi[k] : wc;
-            gv[k] = gbl(gp)[w >> 6];
-            cv[k] = gbl(cp)[w];
+            gv[k] = gbl(gp)[ok[k] ? ci[k] : ch0];
+            cv[k] = gbl(cp)[ok[k] ? wi[k] : wc];
         }
         const uint64_t opw = wok ? gbl(op)[wc] : 0ull;
 #pragma unroll
-        for (int k = 0; k < NW; ++k) cv[k] = (ok[k] && gv[k] == prev_gen) ? cv[k] : 0ull;
+        for (int k = 0; k < NW; ++k) {
+            const bool own = ci[k] == ch0;
+            const bool valid = own ? gv[k] == prev_gen : (gv[k] & ~kGenConv) == prev_gen;
+            cv[k] = (ok[k] && valid) ? cv[k] : 0ull;
+        }
         uint64_t f = (cv[0] << 1) | (cv[0] >> 1) | (cv[1] >> 63) | (cv[2] << 63) | cv[3] | cv[4];
         if (ND == 3) f |= cv[5] | cv[6];
         f &= opw;  // open voxels only (their x < X)
-        const int y0 = yy;
         uint64_t acc = 0ull;  // changed bits of this word over all local sweeps
+        bool conv = true;     // the local sweeps ended without a pending change
         for (int rep = 0;; ++rep) {
             // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list
             // is bit (e - pre[j]) of word j, the last j with pre[j] <= e
@@ -962,57 +1012,39 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             srow[wv][lane] = row * 64 + xw;  // row < 2^25 (Z * Y <= 2^22)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            for (int t0 = 0; t0 < total; t0 += 64 * kFrontierUnroll) {
-                int64_t vi[kFrontierUnroll];
-                int vj[kFrontierUnroll], vb[kFrontierUnroll];
-                uint64_t nb[kFrontierUnroll][6];
-                uint64_t own[kFrontierUnroll];
-                float hv[kFrontierUnroll];
+            for (int t0 = 0; t0 < total; t0 += 64) {
+                const int e = t0 + lane;
+                if (e < total) {
+                    int j = 0;
 #pragma unroll
-                for (int u = 0; u < kFrontierUnroll; ++u) {
-                    const int e = t0 + u * 64 + lane;
-                    vi[u] = -1;
-                    vj[u] = 0;
-                    vb[u] = 0;
+                    for (int step = 32; step > 0; step >>= 1)
+                        if (spre[wv][j + step] <= e) j += step;
+                    const int b = kth_set_bit(sfw[wv][j], e - spre[wv][j]);
+                    const int rx = srow[wv][j];
+                    const int r = rx >> 6, xq = rx & 63;
+                    const int z = r / B.Y, y = r - z * B.Y;
+                    const int x = xq * 64 + b;
+                    const int64_t i = (int64_t)r * B.X + x;
+                    uint64_t nb[6];
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) nb[u][k] = kPackInf;
-                    own[u] = kPackInf;
-                    hv[u] = 0.0f;
-                    if (e < total) {
-                        int j = 0;
-#pragma unroll
-                        for (int step = 32; step > 0; step >>= 1)
-                            if (spre[wv][j + step] <= e) j += step;
-                        const int b = kth_set_bit(sfw[wv][j], e - spre[wv][j]);
-                        const int rx = srow[wv][j];
-                        const int r = rx >> 6, xq = rx & 63;
-                        const int z = r / B.Y, y = r - z * B.Y;
-                        const int x = xq * 64 + b;
-                        const int64_t i = (int64_t)r * B.X + x;
-                        vi[u] = i;
-                        vj[u] = j;
-                        vb[u] = b;
-                        if (ND == 3) {
-                            if (z > 0) nb[u][0] = kb[i - YX];
-                            if (z + 1 < B.Z) nb[u][1] = kb[i + YX];
-                        }
-                        if (y > 0) nb[u][2] = kb[i - B.X];
-                        if (y + 1 < B.Y) nb[u][3] = kb[i + B.X];
-                        if (x > 0) nb[u][4] = kb[i - 1];
-                        if (x + 1 < B.X) nb[u][5] = kb[i + 1];
-                        own[u] = kb[i];
-                        hv[u] = hb[i];
+                    for (int k = 0; k < 6; ++k) nb[k] = kPackInf;
+                    if (ND == 3) {
+                        if (z > 0) nb[0] = kb[i - YX];
+                        if (z + 1 < B.Z) nb[1] = kb[i + YX];
                     }
-                }
-#pragma unroll
-                for (int u = 0; u < kFrontierUnroll; ++u) {
-                    if (vi[u] < 0) continue;
-                    uint64_t m = min(min(min(nb[u][0], nb[u][1]), min(nb[u][2], nb[u][3])), min(nb[u][4], nb[u][5]));
-                    if (m == kPackInf) continue;
-                    const uint64_t k = f_packed(ordf(hv[u]), m);
-                    if (k != own[u]) {
-                        kb[vi[u]] = k;
-                        atomicOr((unsigned long long*)&schg[wv][vj[u]], 1ull << vb[u]);
+                    if (y > 0) nb[2] = kb[i - B.X];
+                    if (y + 1 < B.Y) nb[3] = kb[i + B.X];
+                    if (x > 0) nb[4] = kb[i - 1];
+                    if (x + 1 < B.X) nb[5] = kb[i + 1];
+                    const uint64_t own = kb[i];
+                    const float hv = hb[i];
+                    const uint64_t m = min(min(min(nb[0], nb[1]), min(nb[2], nb[3])), min(nb[4], nb[5]));
+                    if (m != kPackInf) {
+                        const uint64_t k = f_packed(ordf(hv), m);
+                        if (k != own) {
+                            kb[i] = k;
+                            atomicOr((unsigned long long*)&schg[wv][j], 1ull << b);
+                        }
                     }
                 }
             }
@@ -1020,58 +1052,87 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             __builtin_amdgcn_wave_barrier();
             const uint64_t c = schg[wv][lane];
             acc |= c;
-            if (__ballot(c != 0ull) == 0ull || rep + 1 >= reps) break;
-            // local sweep: the neighbours of this sweep's changes that lie in the same chunk
-            // (x within the row's words, y within the chunk's rows); changes are also in acc, so
-            // the neighbours outside the chunk see them in the next launch
+            if (__ballot(c != 0ull) == 0ull) break;
+            if (rep + 1 >= reps) {
+                conv = false;
+                break;
+            }
+            // local sweep: the neighbours of this sweep's changes inside the chunk; changes are
+            // also in acc, so the neighbours outside the chunk see them in the next launch
             f = (c << 1) | (c >> 1);
-            const uint64_t cxm = __shfl(c, (lane + 63) & 63), cxp = __shfl(c, (lane + 1) & 63);
-            if (xw > 0 && lane > 0) f |= cxm >> 63;
-            if (xw + 1 < wpr && lane < 63) f |= cxp << 63;
-            const uint64_t cym = __shfl(c, lane >= wpr ? lane - wpr : lane);
-            const uint64_t cyp = __shfl(c, lane + wpr < 64 ? lane + wpr : lane);
-            if (y0 > 0 && lane >= wpr) f |= cym;
-            if (y0 + 1 < B.Y && lane + wpr < 64) f |= cyp;
+            const uint64_t cxm = __shfl(c, lx > 0 ? lane - 1 : lane);
+            const uint64_t cxp = __shfl(c, lx < CW - 1 ? lane + 1 : lane);
+            if (lx > 0) f |= cxm >> 63;
+            if (lx < CW - 1 && xw + 1 < wpr) f |= cxp << 63;
+            const uint64_t cym = __shfl(c, ly > 0 ? lane - CW : lane);
+            const uint64_t cyp = __shfl(c, ly < CY - 1 ? lane + CW : lane);
+            if (ly > 0) f |= cym;
+            if (ly < CY - 1 && yy + 1 < B.Y) f |= cyp;
+            if (ND == 3 && CZ > 1) {
+                const uint64_t czm = __shfl(c, lz > 0 ? lane - CW * CY : lane);
+                const uint64_t czp = __shfl(c, lz < CZ - 1 ? lane + CW * CY : lane);
+                if (lz > 0) f |= czm;
+                if (lz < CZ - 1 && zz + 1 < B.Z) f |= czp;
+            }
             f &= opw;
         }
         if (__ballot(acc != 0ull) == 0ull) continue;
-        // the chunk changed: publish its changed words and queue the chunks whose frontier can
-        // hold a neighbour of a changed voxel (x / y: the adjacent chunks; 3-D z: the chunks
-        // of the words +- one slice)
-        if (wl < nwords) cn[wl] = acc;
-        if (lane == 0) gn[ch0] = (uint32_t)it + 1u;
-        int64_t cand = -1;
-        if (lane == 0) cand = ch0;
-        else if (lane == 1 && ch0 > 0) cand = ch0 - 1;
-        else if (lane == 2 && ch0 + 1 < nchunks) cand = ch0 + 1;
-        // (a chunk straddling a slice boundary reaches the previous / next slice with part of
-        // its words only: the word range is clamped, not dropped)
-        else if (ND == 3 && lane == 3 && w0 + 63 - ws >= 0) cand = max((int64_t)0, w0 - ws) >> 6;
-        else if (ND == 3 && lane == 4 && w0 + 63 - ws >= 0) cand = min(nwords - 1, w0 + 63 - ws) >> 6;
-        else if (ND == 3 && lane == 5 && w0 + ws < nwords) cand = (w0 + ws) >> 6;
-        else if (ND == 3 && lane == 6 && w0 + ws < nwords) cand = min(nwords - 1, w0 + 63 + ws) >> 6;
+        // the chunk changed: publish its changed words and queue the chunks that hold a
+        // neighbour of a change (faces), and itself unless its local sweeps converged
+        if (wok) cn[wc] = acc;
+        if (lane == 0) gn[ch0] = ((uint32_t)it + 1u) | (conv ? kGenConv : 0u);
+        const bool fxm = __ballot(lx == 0 && (acc & 1ull)) != 0ull;
+        const bool fxp = __ballot(lx == CW - 1 && (acc >> 63)) != 0ull;
+        const bool fym = __ballot(ly == 0 && acc != 0ull) != 0ull;
+        const bool fyp = __ballot(ly == CY - 1 && acc != 0ull) != 0ull;
+        const bool fzm = ND == 3 && __ballot(lz == 0 && acc != 0ull) != 0ull;
+        const bool fzp = ND == 3 && __ballot(lz == CZ - 1 && acc != 0ull) != 0ull;
+        int cand = -1;
+        if (lane == 0 && !conv) cand = ch0;
+        else if (lane == 1 && fxm && cx > 0) cand = ch0 - 1;
+        else if (lane == 2 && fxp && cx + 1 < G.ncx) cand = ch0 + 1;
+        else if (lane == 3 && fym && cy > 0) cand = ch0 - G.ncx;
+        else if (lane == 4 && fyp && cy + 1 < G.ncy) cand = ch0 + G.ncx;
+        else if (lane == 5 && fzm && cz > 0) cand = ch0 - cplane;
+        else if (lane == 6 && fzp && cz + 1 < G.ncz) cand = ch0 + cplane;
         bool push = false;
         if (cand >= 0) push = atomicMax(&qg[cand], (uint32_t)it + 1u) < (uint32_t)it + 1u;
         const uint64_t pm = __ballot(push);
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(cnt_next, (uint32_t)__popcll(pm));
+        if (lane == 0 && pm) base = atomicAdd(cnt_next, (uint32_t)__popcll(pm));
         base = (uint32_t)__shfl((int)base, 0);
         if (push)
             list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
     }
 }
-#define CTWS_FRONTIER_INST(ND, U)                                                                                 \
-    template __global__ void k_frontier<ND, U>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,        \
-                                               const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,        \
-                                               uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, \
-                                               uint32_t*, uint32_t*, int);
-CTWS_FRONTIER_INST(3, 1)
-CTWS_FRONTIER_INST(2, 1)
-CTWS_FRONTIER_INST(3, 2)
-CTWS_FRONTIER_INST(2, 2)
-CTWS_FRONTIER_INST(3, 4)
-CTWS_FRONTIER_INST(2, 4)
+// chunk bricks: 2-D ws (CZ = 1) and 3-D; CTWS_FRONTIER_CHUNK selects one (frontier_chunk_dims)
+#define CTWS_FRONTIER_INST(ND, CW, CY, CZ)                                                                           \
+    template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
+                                                        const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,  \
+                                                        uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*,   \
+                                                        uint32_t*, uint32_t*, uint32_t*, int);
+#define CTWS_LIST0_INST(CW, CY, CZ)                                                                             \
+    template __global__ void k_frontier_list0<CW, CY, CZ>(const BlockDesc*, const BlockStat*, const uint64_t*, \
+                                                          uint32_t*, uint32_t*);
+CTWS_FRONTIER_INST(2, 1, 64, 1)
+CTWS_FRONTIER_INST(2, 2, 32, 1)
+CTWS_FRONTIER_INST(2, 4, 16, 1)
+CTWS_FRONTIER_INST(2, 8, 8, 1)
+CTWS_FRONTIER_INST(3, 1, 8, 8)
+CTWS_FRONTIER_INST(3, 2, 8, 4)
+CTWS_FRONTIER_INST(3, 1, 16, 4)
+CTWS_FRONTIER_INST(3, 4, 4, 4)
+CTWS_FRONTIER_INST(3, 8, 8, 1)
+CTWS_LIST0_INST(1, 64, 1)
+CTWS_LIST0_INST(2, 32, 1)
+CTWS_LIST0_INST(4, 16, 1)
+CTWS_LIST0_INST(8, 8, 1)
+CTWS_LIST0_INST(1, 8, 8)
+CTWS_LIST0_INST(2, 8, 4)
+CTWS_LIST0_INST(1, 16, 4)
+CTWS_LIST0_INST(4, 4, 4)
 #undef CTWS_FRONTIER_INST
+#undef CTWS_LIST0_INST
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
@@ -1100,55 +1161,90 @@ __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restr
 // fixpoint check of the packed flood: K(q) == f(min_p K(p)) at every voxel the relaxation
 // solved (the open bitmap of k_descent_init / k_regrow_init).  The descent-resolved voxels are
 // final by construction (the unique-argmin argument above) and are never written by the
-// relaxation, so words without an open voxel are skipped after one bitmap load.  Word tiles:
-// a wave reads a 64-voxel row word coalesced; x-neighbours come from the neighbouring lanes,
-// the rows above / below (and the slices) are loads the same wave's previous words keep in
-// cache.
+// relaxation, so a group of words without an open voxel is skipped after its bitmap loads.
+// Word tiles, U words per step with all their loads in flight together: a wave reads a
+// 64-voxel row word coalesced; x-neighbours come from the neighbouring lanes, lane 0 / 63
+// fetch the key left / right of the word.
 template <int ND>
 __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint64_t* __restrict__ key,
                                                       const uint64_t* __restrict__ open, uint32_t* __restrict__ flag) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const uint64_t* k = key + B.base;
+    constexpr int U = 4;
+    const gptr_t<uint64_t> k = gbl(key + B.base);
+    const gptr_t<float> hb = gbl(h + B.base);
     const int64_t YX = (int64_t)B.Y * B.X;
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
     bool bad = false;
-    WORD_TILES(B.Z, B.Y, B.X, {
-        const uint64_t ow = gbl(open)[B.fbase + w_];
-        if (ow == 0ull) continue;  // every voxel of the word descent-resolved / kept
-        // every load unconditional (clamped index) so that they are all in flight together
-        const int64_t ic = valid ? i : row * B.X;
-        const uint64_t own0 = k[ic];
-        const uint64_t kym = k[y > 0 ? ic - B.X : ic], kyp = k[y + 1 < B.Y ? ic + B.X : ic];
-        uint64_t kzm = kPackInf, kzp = kPackInf;
-        if (ND == 3) {
-            kzm = k[z > 0 ? ic - YX : ic];
-            kzp = k[z + 1 < B.Z ? ic + YX : ic];
+    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
+        uint64_t ow[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) ow[u] = w0 + u < wend ? gbl(open)[B.fbase + w0 + u] : 0ull;
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) any |= ow[u] != 0ull;
+        if (!any) continue;  // every voxel of the group descent-resolved / kept
+        uint64_t own[U], kym[U], kyp[U], kzm[U], kzp[U], ke[U];
+        float hv[U];
+        int xx[U], yy[U], zz[U];
+        bool valid[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t wu = min(w0 + u, wend - 1);
+            const int64_t row = wu / wpr;
+            const int xw = (int)(wu - row * wpr);
+            const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
+            const int x = xw * 64 + lane;
+            valid[u] = x < B.X;
+            xx[u] = x;
+            yy[u] = y;
+            zz[u] = z;
+            const int xc = min(x, B.X - 1);
+            const int64_t ic = row * B.X + xc;
+            own[u] = k[ic];
+            kym[u] = k[y > 0 ? ic - B.X : ic];
+            kyp[u] = k[y + 1 < B.Y ? ic + B.X : ic];
+            if (ND == 3) {
+                kzm[u] = k[z > 0 ? ic - YX : ic];
+                kzp[u] = k[z + 1 < B.Z ? ic + YX : ic];
+            }
+            ke[u] = k[row * B.X + (lane == 0 ? max(xc - 1, 0) : min(xc + 1, B.X - 1))];
+            hv[u] = hb[ic];
         }
-        const uint64_t kxm = k[x > 0 && valid ? ic - 1 : ic], kxp = k[x + 1 < B.X ? ic + 1 : ic];
-        const float hv = h[B.base + ic];
-        const uint64_t own = valid ? own0 : kPackInf;
-        uint64_t l = shfl_up_u64(own, 1), r = shfl_down_u64(own, 1);
-        if (lane == 0) l = (x > 0) ? kxm : kPackInf;
-        if (lane == 63) r = (x + 1 < B.X) ? kxp : kPackInf;
-        if (x + 1 >= B.X) r = kPackInf;
-        uint64_t m = min(l, r);
-        if (y > 0) m = min(m, kym);
-        if (y + 1 < B.Y) m = min(m, kyp);
-        if (ND == 3) {
-            if (z > 0) m = min(m, kzm);
-            if (z + 1 < B.Z) m = min(m, kzp);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int x = xx[u], y = yy[u], z = zz[u];
+            const uint64_t o = valid[u] ? own[u] : kPackInf;
+            uint64_t l = shfl_up_u64(o, 1), r = shfl_down_u64(o, 1);
+            const uint64_t ker = shfl_u64(ke[u], 63);
+            if (lane == 0) l = (x > 0) ? ke[u] : kPackInf;
+            if (lane == 63) r = ker;
+            if (x + 1 >= B.X) r = kPackInf;
+            uint64_t m = min(l, r);
+            if (y > 0) m = min(m, kym[u]);
+            if (y + 1 < B.Y) m = min(m, kyp[u]);
+            if (ND == 3) {
+                if (z > 0) m = min(m, kzm[u]);
+                if (z + 1 < B.Z) m = min(m, kzp[u]);
+            }
+            // an open voxel is never a seed (descent: seeds resolve to themselves; regrow: the
+            // survivors and auto seeds are taken out of the open set)
+            const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(hv[u]), m);
+            const bool b1 = valid[u] && ((ow[u] >> lane) & 1ull) && e != o;
+            if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
+                const uint32_t slot = atomicAdd(&flag[1], 1u);
+                if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + (int64_t)(z * B.Y + y) * B.X + x);
+            }
+            bad |= b1;
         }
-        // an open voxel is never a seed (descent: seeds resolve to themselves; regrow: the
-        // survivors and auto seeds are taken out of the open set)
-        const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(hv), m);
-        const bool b1 = valid && ((ow >> lane) & 1ull) && e != own;
-        if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
-            const uint32_t slot = atomicAdd(&flag[1], 1u);
-            if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + i);
-        }
-        bad |= b1;
-    })
+    }
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 template __global__ void k_flood_verify<3>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,

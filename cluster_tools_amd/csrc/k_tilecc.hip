@@ -194,6 +194,14 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             vv[j] = ((inm >> j) & 1u) ? v : kLNone;
         }
     }
+    if (MODE == CC_PLATEAU) {
+        // a tile without plateau voxels writes nothing: P is read only at plateau voxels
+        // (cc_is_max, k_plateau_flag, k_tile_merge checks cls first)
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) any |= vv[j] != kLNone;
+        if (!__syncthreads_or(any)) return;
+    }
 #pragma unroll
     for (int j = 0; j < PER; ++j) sv[threadIdx.x + j * 256] = vv[j];
     __syncthreads();
@@ -301,7 +309,9 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                 const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
                 if (z < nz && y < ny && x < nx) {
                     const int64_t i = ((int64_t)z * ny + y) * nx + x;
-                    const uint32_t pi = P[i];
+                    // PLATEAU: tiles without plateau voxels leave P unwritten
+                    const bool mi = MODE != CC_PLATEAU || (a.cls[B.base + i] & 2);
+                    const uint32_t pi = mi ? P[i] : kNoParent;
                     if (pi != kNoParent) {
                         // the backward neighbours of (z, y, x) that leave the tile through face f
                         // (a diagonal through the tile corner belongs to the y face)
@@ -313,6 +323,7 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                             const int qz = z + dz, qy = y + dy, qx = x + dx;
                             if (!out || qz < 0 || qy < 0 || qx < 0 || qx >= nx) continue;
                             const int64_t q = ((int64_t)qz * ny + qy) * nx + qx;
+                            if (MODE == CC_PLATEAU && !(a.cls[B.base + q] & 2)) continue;
                             const uint32_t pq = P[q];
                             if (pq == kNoParent) continue;
                             if (MODE != CC_SEED &&
@@ -347,6 +358,7 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
             if (ly == 0 || z >= nz || y >= ny || x + 1 >= nx) continue;
             const int64_t i = ((int64_t)z * ny + y) * nx + x;
             const int64_t q = i - nx + 1;
+            if (!(a.cls[B.base + i] & 2) || !(a.cls[B.base + q] & 2)) continue;
             const uint32_t pi = P[i], pq = P[q];
             if (pi == kNoParent || pq == kNoParent) continue;
             if (cc_value<MODE>(B, a, true, z, y, x) != cc_value<MODE>(B, a, true, z, y - 1, x + 1)) continue;
