@@ -140,6 +140,7 @@ struct ctws_handle {
     // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words)
     int fchunk2[3] = {1, 64, 1};
     int fchunk3[3] = {1, 8, 8};
+    int frontier_grid = 2048;  // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4)
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
@@ -609,7 +610,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
 #undef CTWS_LIST0
     LAUNCHCHK();
     // one wave per list entry; the largest list is every chunk of the batch
-    const unsigned fg = (unsigned)std::min<int64_t>((nch + kFrontierWavesHost - 1) / kFrontierWavesHost, 2048);
+    const unsigned fg = (unsigned)std::min<int64_t>((nch + kFrontierWavesHost - 1) / kFrontierWavesHost, h->frontier_grid);
     bool converged = false;
     int fiters = 0;
     while (fiters < h->frontier_max_iters && !converged) {
@@ -2015,6 +2016,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK2D")) parse_chunk(t, h->fchunk2, false);
     if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK3D")) parse_chunk(t, h->fchunk3, true);
     if (const char* t = std::getenv("CTWS_RELAX")) h->relax = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||

@@ -921,7 +921,10 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     const int lx = lane % CW, ly = (lane / CW) % CY, lz = lane / (CW * CY);
     const uint32_t n_entries = *cnt;
     const uint32_t prev_gen = (uint32_t)it;  // gprev[ch] & ~kGenConv == it: changed in iteration it - 1
-    for (uint32_t e0 = blockIdx.x * kFrontierWaves + wv; e0 < n_entries; e0 += gridDim.x * kFrontierWaves) {
+    // XCD-contiguous entries: the workgroups of one XCD take neighbouring chunks, so the lines
+    // two adjacent chunks share stay in one L2
+    const uint32_t wg = (uint32_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+    for (uint32_t e0 = wg * kFrontierWaves + wv; e0 < n_entries; e0 += gridDim.x * kFrontierWaves) {
         const uint32_t ent = list[e0];
         const int bi = (int)(ent >> kWlChunkBits);
         // word and chunk indices fit 32 bits (Z * Y * wpr < 2^27, chunks < 2^20)
@@ -994,6 +997,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
         f &= opw;  // open voxels only (their x < X)
         uint64_t acc = 0ull;  // changed bits of this word over all local sweeps
         bool conv = true;     // the local sweeps ended without a pending change
+        uint32_t vis = 0;     // statistics (CTWS_TRACE): voxels visited
         for (int rep = 0;; ++rep) {
             // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list
             // is bit (e - pre[j]) of word j, the last j with pre[j] <= e
@@ -1005,7 +1009,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             }
             const int total = __shfl(incl, 63);
             if (total == 0) break;
-            if (nvisit && lane == 0) atomicAdd(&nvisit[bi], (uint32_t)total);
+            vis += (uint32_t)total;
             schg[wv][lane] = 0ull;
             sfw[wv][lane] = f;
             spre[wv][lane] = incl - cnt_bits;
@@ -1076,6 +1080,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             }
             f &= opw;
         }
+        if (nvisit && lane == 0 && vis) atomicAdd(&nvisit[bi], vis);
         if (__ballot(acc != 0ull) == 0ull) continue;
         // the chunk changed: publish its changed words and queue the chunks that hold a
         // neighbour of a change (faces), and itself unless its local sweeps converged
