@@ -140,6 +140,7 @@ struct ctws_handle {
     // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words)
     int fchunk2[3] = {1, 64, 1};
     int fchunk3[3] = {1, 8, 8};
+    int frontier_stage = 0;    // CTWS_FRONTIER_STAGE=1: iteration 0 in LDS (k_frontier_stage; measured slower, opt-in)
     int frontier_grid = 2048;  // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4)
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
@@ -611,6 +612,8 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     LAUNCHCHK();
     // one wave per list entry; the largest list is every chunk of the batch
     const unsigned fg = (unsigned)std::min<int64_t>((nch + kFrontierWavesHost - 1) / kFrontierWavesHost, h->frontier_grid);
+    // k_frontier_stage: one workgroup per chunk, grid-stride (a multiple of 8 for xcd_swizzle)
+    const unsigned sg = (unsigned)std::min<int64_t>(nch, 2048);
     bool converged = false;
     int fiters = 0;
     while (fiters < h->frontier_max_iters && !converged) {
@@ -631,7 +634,19 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             h->frontier_reps);                                                                                      \
         break;
-            switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_FRONTIER) }
+#define CTWS_STAGE(K, ND, CW, CY, CZ)                                                                             \
+    case K:                                                                                                       \
+        k_frontier_stage<ND, CW, CY, CZ><<<sg, 256, 0, h->stream>>>(                                              \
+            w.desc, w.hm, w.key, w.fopen, fb[1], gen[0], wl[0], w.wlcnt, wl[1], w.wlcnt + 1, w.qgen,              \
+            fst ? fst + nb : nullptr, h->frontier_reps);                                                          \
+        break;
+            if (it == 0 && h->frontier_stage) {
+                // iteration 0 with the chunks staged in LDS (k_frontier_stage)
+                switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_STAGE) }
+            } else {
+                switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_FRONTIER) }
+            }
+#undef CTWS_STAGE
 #undef CTWS_FRONTIER
             if (h->trace) hipEventRecord(tev[k + 1], h->stream);
         }
@@ -2016,6 +2031,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK2D")) parse_chunk(t, h->fchunk2, false);
     if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK3D")) parse_chunk(t, h->fchunk3, true);
     if (const char* t = std::getenv("CTWS_RELAX")) h->relax = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FRONTIER_STAGE")) h->frontier_stage = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
