@@ -10,9 +10,9 @@
 //
 // A global union-find over every voxel (one atomicCAS chain per neighbour pair through HBM)
 // costs ~100x a streaming pass on large components.  Here a workgroup first solves its tile
-// (3-D: 4x16x32, 2-D: 1x32x64) completely in LDS: parents are tile-local *order keys*, so
-// linking the larger key under the smaller (atomicCAS in LDS) leaves every tile component
-// rooted at its smallest key.  For SEED/CROP the order key is the local F-order index
+// (3-D: 4x16x32, 2-D: 1x32x64) completely in LDS: parents are tile-local positions and a
+// union links the root with the larger *order key* under the smaller (atomicCAS in LDS), so
+// every tile component is rooted at its smallest key.  For SEED/CROP the order key is the local F-order index
 // (x most significant, then y, then z — vigra scan order, A.0), so the tile root is the
 // component's first voxel in scan order within the tile; for PLATEAU the C-order index.
 // The tile writes each member's global parent = its tile root (C-order block index), non-
@@ -43,13 +43,16 @@ __device__ __forceinline__ uint32_t lds_find(uint32_t* sp, uint32_t a) {
     }
     return a;
 }
-__device__ __forceinline__ void lds_union(uint32_t* sp, uint32_t a, uint32_t b) {
-    // link the root with the larger key under the one with the smaller
+// link the root with the larger order key under the one with the smaller; parents are indexed
+// by tile C-order position (consecutive lanes: consecutive LDS words, no bank conflicts), the
+// order key of a position is key(position)
+template <typename Key>
+__device__ __forceinline__ void lds_union(uint32_t* sp, uint32_t a, uint32_t b, Key key) {
     while (true) {
         a = lds_find(sp, a);
         b = lds_find(sp, b);
         if (a == b) return;
-        if (a > b) {
+        if (key(a) > key(b)) {
             const uint32_t t = a;
             a = b;
             b = t;
@@ -127,7 +130,7 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, TN = TZ * TY * TX, PER = TN / 256;
     static_assert(TN % 256 == 0, "");
     __shared__ uint32_t sv[TN];  // values, C-layout c = (lz * TY + ly) * TX + lx
-    __shared__ uint32_t sp[TN];  // parents by order key
+    __shared__ uint32_t sp[TN];  // parents, C-layout like sv
     const BlockDesc& B = D[blockIdx.y];
     const BlockStat& st = S[blockIdx.y];
     if (!st.active) return;
@@ -141,9 +144,10 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
     if (t >= ntx * nty * ntz) return;
     const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
     const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
-    auto ordk = [&](int c) -> uint32_t {
-        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-        return MODE == CC_PLATEAU ? (uint32_t)c : fkey_local<TZ, TY>(lz, ly, lx);
+    // order key of tile position c: the C index (PLATEAU) or the vigra scan key (SEED, CROP)
+    auto ordk = [&](uint32_t c) -> uint32_t {
+        const int lx = (int)(c % TX), ly = (int)((c / TX) % TY), lz = (int)(c / (TX * TY));
+        return MODE == CC_PLATEAU ? c : fkey_local<TZ, TY>(lz, ly, lx);
     };
     // load values: every load unconditional (position clamped into the domain, global address
     // space) so that all of a thread's loads are in flight together; non-members and positions
@@ -220,7 +224,8 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
         const uint64_t starts = __ballot(!cont);
         const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
         const int s0 = 63 - __builtin_clzll(starts & upto);
-        sp[ordk(c)] = vv[j] == kLNone ? kLNone : ordk(c - (lane - s0));
+        // (the run start has the smallest x, so the smallest scan key of the run)
+        sp[c] = vv[j] == kLNone ? kLNone : (uint32_t)(c - (lane - s0));
     }
     __syncthreads();
     // unions with the other backward neighbours; a y / z pair is redundant when both voxels
@@ -240,7 +245,7 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             const int cq = (qz * TY + qy) * TX + qx;
             if (!conn(sv[cq], vv[j])) continue;
             if (dx == 0 && ((contm >> j) & 1u) && conn(sv[cq - 1], sv[cq])) continue;
-            lds_union(sp, ordk(c), ordk(cq));
+            lds_union(sp, (uint32_t)c, (uint32_t)cq, ordk);
         }
     }
     __syncthreads();
@@ -254,17 +259,8 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
         if (z >= nz || y >= ny || x >= nx) continue;
         uint32_t g = kNoParent;
         if (vv[j] != kLNone) {
-            const uint32_t r = lds_find(sp, ordk(c));
-            int rz, ry, rx;
-            if (MODE == CC_PLATEAU) {
-                rx = (int)(r % TX);
-                ry = (int)((r / TX) % TY);
-                rz = (int)(r / (TX * TY));
-            } else {
-                rz = (int)(r % TZ);
-                ry = (int)((r / TZ) % TY);
-                rx = (int)(r / (TZ * TY));
-            }
+            const uint32_t r = lds_find(sp, (uint32_t)c);
+            const int rx = (int)(r % TX), ry = (int)((r / TX) % TY), rz = (int)(r / (TX * TY));
             g = (uint32_t)(((int64_t)(z0 + rz) * ny + (y0 + ry)) * nx + (x0 + rx));
         }
         P[((int64_t)z * ny + y) * nx + x] = g;
