@@ -184,6 +184,27 @@ class BaseClusterTask(luigi.Task):
     def clean_up_for_retry(self, block_list, prefix=None):
         pass
 
+    # -- the blockwise schedule every task of the path shares
+    def blocks_to_process(self, shape, block_shape, roi_begin=None, roi_end=None, block_list_path=None,
+                          job_prefix=None):
+        """First attempt: the blocks of the volume (or of its roi / the given block list).  A
+        retry: the blocks no job of the previous attempt processed, after the task's clean-up."""
+        if self.n_retries > 0:
+            self.clean_up_for_retry(self.block_list, job_prefix)
+            return self.block_list
+        from cluster_tools_amd.utils.volume_utils import blocks_in_volume
+        return blocks_in_volume(shape, block_shape, roi_begin, roi_end, block_list_path=block_list_path)
+
+    def run_jobs(self, n_jobs, block_list, config, job_prefix=None, consecutive_blocks=False):
+        """Write the job configs, submit, wait and check (retrying failed blocks per the global
+        config); block_list None = one job that gets the config as is."""
+        if block_list is not None:
+            self._write_log('scheduling %i blocks to be processed' % len(block_list))
+        self.prepare_jobs(n_jobs, block_list, config, job_prefix, consecutive_blocks)
+        self.submit_jobs(n_jobs, job_prefix)
+        self.wait_for_jobs(job_prefix)
+        self.check_jobs(n_jobs, job_prefix)
+
     # -- results and retry
     @staticmethod
     def parse_jobs(log_prefix, max_jobs):

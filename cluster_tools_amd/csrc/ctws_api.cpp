@@ -214,8 +214,8 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(sm, vox);
         ALLOC(hm, vox);
         ALLOC(cls, vox + 16);  // k_plateau_flag reads aligned 16-byte groups
-        ALLOC(P, vox);
-        ALLOC(PF, vox);
+        ALLOC(P, vox + 4);   // + 4: 16-byte group reads (k_flatten_roots)
+        ALLOC(PF, vox + 4);
         ALLOC(lab, vox);
         ALLOC(key, vox);
         w.cap_vox = vox;
@@ -1023,6 +1023,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     const dim3 vg((unsigned)std::min<int64_t>((maxN + 255) / 256, 4096), nb);
     const dim3 ig((unsigned)std::min<int64_t>((maxNI + 255) / 256, 4096), nb);
+    // 4 voxels per thread (16-byte groups)
+    const dim3 vg4((unsigned)std::min<int64_t>((maxN / 4 + 256) / 256, 4096), nb);
     const dim3 wg((unsigned)((words_of(maxN) + 255) / 256), nb);
     // row-tile kernels: kRows rows (z, y) per workgroup iteration
     const dim3 rg((unsigned)std::min<int64_t>((maxRows + kRows - 1) / kRows, 16384), nb);
@@ -1216,7 +1218,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         LAUNCHCHK();
     }
     HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-    k_flatten_roots<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
+    k_flatten_roots<<<vg4, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
     k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
@@ -1524,7 +1526,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 k_tile_merge<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             }
             HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-            k_flatten_roots<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
+            k_flatten_roots_w<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
             k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
             k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
             k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);

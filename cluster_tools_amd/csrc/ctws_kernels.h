@@ -76,6 +76,7 @@ __global__ void k_gauss_yx(const BlockDesc*, const BlockStat*, int, HmapParams, 
 __global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, uint32_t*);
 __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uint32_t*);
 __global__ void k_flatten_roots(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
+__global__ void k_flatten_roots_w(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
 __global__ void k_bitmap_csum(const BlockDesc*, const BlockStat*, int, const uint64_t*, uint32_t*);
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
 __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uint64_t*, const uint32_t*, uint32_t*);

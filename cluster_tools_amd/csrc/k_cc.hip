@@ -409,10 +409,49 @@ __global__ void __launch_bounds__(256) k_count_ids(const BlockDesc* __restrict__
 }
 
 // point every element of a union-find forest directly at its root; roots set their scan-key
+// bit in the root bitmap W (zeroed beforehand).  Most entries are kNoParent or point at their
+// root already and cost only their load, so the pass streams the parent array 16 bytes per
+// lane: a thread takes an aligned group of 4 entries (global index), the entries outside the
+// block are skipped.
+__global__ void __launch_bounds__(256) k_flatten_roots(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
+                                                       uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active || (inner && !B.crop)) return;
+    const int64_t base = inner ? B.ibase : B.base;
+    const int64_t n = inner ? B.NI : B.N;
+    uint32_t* P = PFg + base;
+    uint64_t* W = Wg + B.wbase;
+    const int ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
+    const int64_t g0 = base >> 2, g1 = (base + n + 3) >> 2;
+    const uint4* P4 = reinterpret_cast<const uint4*>(PFg);
+    for (int64_t g = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < g1; g += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 q = P4[g];
+        const uint32_t pv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = g * 4 + k - base;  // block index
+            const uint32_t p = pv[k];
+            if (i < 0 || i >= n || p == kNoParent) continue;
+            if (p == (uint32_t)i) {
+                const int64_t row = i / nx;
+                const int x = (int)(i - row * nx), z = (int)(row / ny), y = (int)(row - (int64_t)z * ny);
+                const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
+                atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
+            } else {
+                const uint32_t r = uf_find(P, p);
+                if (r != p) P[i] = r;
+            }
+        }
+    }
+}
+
+// k_flatten_roots for dense forests (the crop CC: nearly every voxel a member, so nearly
+// every entry a find): word tiles, more threads in flight per voxel.  Points every element at
+// its root; roots set their scan-key
 // bit in the root bitmap W (zeroed beforehand).  Word tiles (wtg / wtig grid), U words per
 // step with their parent loads in flight together; most voxels are kNoParent or point at
 // their root already and cost the one load.
-__global__ void __launch_bounds__(256) k_flatten_roots(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
+__global__ void __launch_bounds__(256) k_flatten_roots_w(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
                                                        uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || (inner && !B.crop)) return;

@@ -209,11 +209,10 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
             const int x = (int)(w0 + u - row * wpr) * 64 + lane;
             valid[u] = w0 + u < wend && x < B.X;
             zs[u] = (int)(row / B.Y);
-            // loads unconditional (clamped index): key, seed flag and height together
+            // loads unconditional (clamped index): key and seed flag together
             gi[u] = B.base + (valid[u] ? row * B.X + x : 0);
             kv[u] = key[gi[u]];
             fx[u] = fixedv[gi[u]];
-            hv[u] = h[gi[u]];
         }
         uint32_t lb[U], cnt[U];
         bool ex[U];
@@ -226,6 +225,9 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
             lb[u] = kv[u] == kInfKey ? 0u : (uint32_t)(kv[u] & kLab);
             cnt[u] = counts[B.base + lb[u]];
             ex[u] = excl ? excl[B.base + lb[u]] != 0 : false;
+            // the height only where a relaxed voxel may become a seed (descent-resolved voxels
+            // are seeds already; ~10 % of the voxels on config 3): words without one skip it
+            hv[u] = __ballot(valid[u] && !fx[u] && lb[u] != 0) ? h[gi[u]] : 0.0f;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {

@@ -51,10 +51,7 @@ class GpuMeasuresBase(luigi.Task):
         config.update({'seg_path': self.seg_path, 'seg_key': self.seg_key, 'gt_path': self.gt_path,
                        'gt_key': self.gt_key, 'output_path': self.output_path,
                        'ignore_label': bool(self.ignore_label), 'block_shape': block_shape})
-        self.prepare_jobs(1, None, config)
-        self.submit_jobs(1)
-        self.wait_for_jobs()
-        self.check_jobs(1)
+        self.run_jobs(1, None, config)
 
 
 class GpuMeasuresLocal(GpuMeasuresBase, LocalTask):

@@ -33,14 +33,11 @@ class FindLabelingBase(luigi.Task):
         self.init(shebang)
         shape = vu.get_shape(self.input_path, self.input_key)
         block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end)
-        n_jobs = min(len(block_list), self.max_jobs)
-        config = self.get_task_config()
-        config.update({'shape': list(shape), 'assignment_path': self.assignment_path,
-                       'assignment_key': self.assignment_key, 'tmp_folder': self.tmp_folder, 'n_jobs': n_jobs})
-        self.prepare_jobs(1, None, config)
-        self.submit_jobs(1)
-        self.wait_for_jobs()
-        self.check_jobs(1)
+        # one job merges the find_uniques results of the n_jobs jobs of the previous task
+        cfg = dict(self.get_task_config(), shape=list(shape), assignment_path=self.assignment_path,
+                   assignment_key=self.assignment_key, tmp_folder=self.tmp_folder,
+                   n_jobs=min(len(block_list), self.max_jobs))
+        self.run_jobs(1, None, cfg)
 
 
 class FindLabelingLocal(FindLabelingBase, LocalTask):

@@ -30,20 +30,11 @@ class FindUniquesBase(luigi.Task):
     def run_impl(self):
         shebang, block_shape, roi_begin, roi_end = self.global_config_values()
         self.init(shebang)
-        shape = vu.get_shape(self.input_path, self.input_key)
-        if self.n_retries == 0:
-            block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end)
-        else:
-            block_list = self.block_list
-            self.clean_up_for_retry(block_list)
-        n_jobs = min(len(block_list), self.max_jobs)
-        config = {"input_path": self.input_path, "input_key": self.input_key, "block_shape": block_shape,
-                  "tmp_folder": self.tmp_folder, "return_counts": self.return_counts}
-        self._write_log('scheduling %i blocks to be processed' % len(block_list))
-        self.prepare_jobs(n_jobs, block_list, config)
-        self.submit_jobs(n_jobs)
-        self.wait_for_jobs()
-        self.check_jobs(n_jobs)
+        blocks = self.blocks_to_process(vu.get_shape(self.input_path, self.input_key), block_shape,
+                                        roi_begin, roi_end)
+        self.run_jobs(min(len(blocks), self.max_jobs), blocks,
+                      dict(input_path=self.input_path, input_key=self.input_key, block_shape=block_shape,
+                           tmp_folder=self.tmp_folder, return_counts=self.return_counts))
 
 
 class FindUniquesLocal(FindUniquesBase, LocalTask):

@@ -48,37 +48,28 @@ class WatershedBase(luigi.Task):
                        'invert_inputs': False, 'non_maximum_suppression': False})
         return config
 
-    def clean_up_for_retry(self, block_list, prefix=None):
-        super().clean_up_for_retry(block_list)
-
     def run_impl(self):
         shebang, block_shape, roi_begin, roi_end, block_list_path = self.global_config_values(True)
         self.init(shebang)
-        shape = vu.get_shape(self.input_path, self.input_key)
-        if len(shape) == 4:
-            shape = shape[1:]
-        ws_config = self.get_task_config()
-        chunks = tuple(bs // 2 for bs in block_shape)
-        with vu.file_reader(self.output_path) as f:
-            f.require_dataset(self.output_key, shape=shape, chunks=chunks, compression='gzip', dtype='uint64')
-        ws_config.update({'input_path': self.input_path, 'input_key': self.input_key,
-                          'output_path': self.output_path, 'output_key': self.output_key,
-                          'block_shape': block_shape})
-        if self.mask_path != '':
-            assert self.mask_key != ''
-            ws_config.update({'mask_path': self.mask_path, 'mask_key': self.mask_key})
-        if self.n_retries == 0:
-            block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end,
-                                             block_list_path=block_list_path)
-        else:
-            block_list = self.block_list
-            self.clean_up_for_retry(block_list)
-        self._write_log('scheduling %i blocks to be processed' % len(block_list))
-        n_jobs = min(len(block_list), self.max_jobs)
-        self.prepare_jobs(n_jobs, block_list, ws_config)
-        self.submit_jobs(n_jobs)
-        self.wait_for_jobs()
-        self.check_jobs(n_jobs)
+        shape, ws_config = ws_task_setup(self, block_shape)
+        blocks = self.blocks_to_process(shape, block_shape, roi_begin, roi_end, block_list_path)
+        self.run_jobs(min(len(blocks), self.max_jobs), blocks, ws_config)
+
+
+def ws_task_setup(task, block_shape):
+    """Shared by the watershed tasks: the 3-D output shape (a 4-D input's channel axis dropped),
+    the gzip uint64 output dataset with half-block chunks, and the job config = task config +
+    paths (+ mask)."""
+    shape = tuple(vu.get_shape(task.input_path, task.input_key))[-3:]
+    with vu.file_reader(task.output_path) as f:
+        f.require_dataset(task.output_key, shape=shape, chunks=tuple(b // 2 for b in block_shape),
+                          compression='gzip', dtype='uint64')
+    cfg = dict(task.get_task_config(), input_path=task.input_path, input_key=task.input_key,
+               output_path=task.output_path, output_key=task.output_key, block_shape=block_shape)
+    if task.mask_path != '':
+        assert task.mask_key != ''
+        cfg.update(mask_path=task.mask_path, mask_key=task.mask_key)
+    return shape, cfg
 
 
 class WatershedLocal(WatershedBase, LocalTask):
@@ -228,27 +219,26 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
             pending_write.result()
 
 
-def watershed(job_id, config_path):
+def run_job(job_id, config_path, pass_id=None):
+    """Job entry shared by the watershed tasks: the job's blocks through run_blocks, pass 0
+    (`_ws_block`) unless the config's 'pass' says 1 (`_ws_pass2`)."""
     fu.log("start processing job %i" % job_id)
     fu.log("reading config from %s" % config_path)
     with open(config_path) as f:
         config = json.load(f)
-    input_path, input_key = config['input_path'], config['input_key']
-    shape = list(vu.get_shape(input_path, input_key))
-    if len(shape) == 4:
-        shape = shape[1:]
-    block_shape = list(config['block_shape'])
-    block_list = config['block_list']
-    output_path, output_key = config['output_path'], config['output_key']
-    blocking = Blocking([0, 0, 0], shape, block_shape)
-    with vu.file_reader(input_path, 'r') as f_in, vu.file_reader(output_path) as f_out:
-        ds_in = f_in[input_key]
-        assert ds_in.ndim in (3, 4)
-        ds_out = f_out[output_key]
-        assert ds_out.ndim == 3
+    pass_id = config.get('pass', 0) if pass_id is None else pass_id
+    shape = list(vu.get_shape(config['input_path'], config['input_key']))[-3:]
+    blocking = Blocking([0, 0, 0], shape, list(config['block_shape']))
+    with vu.file_reader(config['input_path'], 'r') as fi, vu.file_reader(config['output_path']) as fo:
+        ds_in, ds_out = fi[config['input_key']], fo[config['output_key']]
+        assert ds_in.ndim in (3, 4) and ds_out.ndim == 3, (ds_in.ndim, ds_out.ndim)
         mask = vu.load_mask(config['mask_path'], config['mask_key'], shape) if 'mask_path' in config else None
-        run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0)
+        run_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, pass_id=pass_id)
     fu.log_job_success(job_id)
+
+
+def watershed(job_id, config_path):
+    run_job(job_id, config_path, pass_id=0)
 
 
 if __name__ == '__main__':

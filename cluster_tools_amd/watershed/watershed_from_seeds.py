@@ -48,9 +48,6 @@ class WatershedFromSeedsBase(luigi.Task):
         config.update({'channel_begin': 0, 'channel_end': None, 'agglomerate_channels': 'mean', 'size_filter': 0})
         return config
 
-    def clean_up_for_retry(self, block_list):
-        super().clean_up_for_retry(block_list)
-
     def run_impl(self):
         shebang, block_shape, roi_begin, roi_end = self.global_config_values()
         self.init(shebang)
@@ -69,17 +66,8 @@ class WatershedFromSeedsBase(luigi.Task):
         if self.mask_path != '':
             assert self.mask_key != ''
             config.update({'mask_path': self.mask_path, 'mask_key': self.mask_key})
-        if self.n_retries == 0:
-            block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end)
-        else:
-            block_list = self.block_list
-            self.clean_up_for_retry(block_list)
-        n_jobs = min(len(block_list), self.max_jobs)
-        self._write_log('scheduling %i blocks to be processed' % len(block_list))
-        self.prepare_jobs(n_jobs, block_list, config)
-        self.submit_jobs(n_jobs)
-        self.wait_for_jobs()
-        self.check_jobs(n_jobs)
+        blocks = self.blocks_to_process(shape, block_shape, roi_begin, roi_end)
+        self.run_jobs(min(len(blocks), self.max_jobs), blocks, config)
 
 
 class WatershedFromSeedsLocal(WatershedFromSeedsBase, LocalTask):

@@ -62,17 +62,8 @@ class WriteBase(luigi.Task):
             config.update({'offset_path': self.offset_path})
         if not in_place:
             config.update({'output_path': self.output_path, 'output_key': self.output_key})
-        if self.n_retries == 0:
-            block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end)
-        else:
-            block_list = self.block_list
-            self.clean_up_for_retry(block_list, self.identifier)
-        self._write_log('scheduling %i blocks to be processed' % len(block_list))
-        n_jobs = min(len(block_list), self.max_jobs)
-        self.prepare_jobs(n_jobs, block_list, config, self.identifier)
-        self.submit_jobs(n_jobs, self.identifier)
-        self.wait_for_jobs(self.identifier)
-        self.check_jobs(n_jobs, self.identifier)
+        blocks = self.blocks_to_process(shape, block_shape, roi_begin, roi_end, job_prefix=self.identifier)
+        self.run_jobs(min(len(blocks), self.max_jobs), blocks, config, self.identifier)
 
     def output(self):
         return luigi.LocalTarget(os.path.join(self.tmp_folder, '%s_%s.log' % (self.task_name, self.identifier)))
