@@ -1193,7 +1193,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
     {
-        k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.P);
+        k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.smax);
         LAUNCHCHK();
         // plateaus (equal-valued maxima candidates) and the seed CC: LDS tile union-find
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device

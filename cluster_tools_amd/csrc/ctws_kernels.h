@@ -73,7 +73,7 @@ __global__ void k_gauss_yx(const BlockDesc*, const BlockStat*, int, HmapParams, 
                            const float*, const float*, const uint32_t*, const uint32_t*, float*);
 
 // k_cc.hip
-__global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, uint32_t*);
+__global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, const uint32_t*);
 __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uint32_t*);
 __global__ void k_flatten_roots(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
 __global__ void k_flatten_roots_w(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);

@@ -51,9 +51,18 @@ namespace ctws {
 // per step with every load of the step in flight together (clamped positions, no branches
 // between them).  The x neighbours come from the neighbouring lanes; lane 0 / 63 fetch the
 // voxel left / right of the word with one extra load per row.
+//
+// Zero short cut: the seed map is >= 0 (a distance transform, Gaussian-smoothed with positive
+// taps), so 0 is its minimum, and a slice (2-D ws) / block (3-D ws) whose dt has a positive
+// value has a positive seed-map voxel (at the same position).  On the connected grid every
+// zero component then touches a strictly greater voxel: no zero voxel is a maximum, whatever
+// its neighbours.  Those voxels are classified "greater neighbour" outright and stay out of
+// the plateau union-find (the masked region of a masked block — fin = 1, dt = 0 — is one
+// huge zero plateau otherwise).  pos: the slice's / block's dt maximum > 0.
 template <int ND>
-__device__ __forceinline__ void localmax_words(const BlockDesc& B, const float* __restrict__ p, uint8_t* __restrict__ cl,
-                                               uint32_t& nplat) {
+__device__ __forceinline__ void localmax_words(const BlockDesc& B, const BlockStat& st, const uint32_t* __restrict__ smax,
+                                               const float* __restrict__ p, uint8_t* __restrict__ cl, uint32_t& nplat) {
+    const uint32_t ord0 = 0x80000000u;  // ordf(+0.0f)
     constexpr int U = 4;
     const int Y = B.Y, X = B.X, Z = B.Z;
     const int64_t YX = (int64_t)Y * X;
@@ -147,6 +156,14 @@ __device__ __forceinline__ void localmax_words(const BlockDesc& B, const float* 
                 gt |= w[k] > cc;
                 eq |= w[k] == cc;
             }
+            if (cc == 0.0f) {
+                const int z = (int)(ii[u] / ((int64_t)B.Y * B.X));
+                const bool pos = (ND == 2 ? smax[B.sbase + z] : st.dt_max) > ord0;
+                if (pos) {
+                    gt = true;
+                    eq = false;
+                }
+            }
             if (valid[u]) cl[ii[u]] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
             nplat += valid[u] && eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
         }
@@ -155,13 +172,12 @@ __device__ __forceinline__ void localmax_words(const BlockDesc& B, const float* 
 
 __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ D, BlockStat* S,
                                                   const float* __restrict__ v, uint8_t* __restrict__ cls,
-                                                  uint32_t* __restrict__ Pp) {
-    (void)Pp;
+                                                  const uint32_t* __restrict__ smax) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     uint32_t nplat = 0;
-    if (B.nd_ws == 3) localmax_words<3>(B, v + B.base, cls + B.base, nplat);
-    else localmax_words<2>(B, v + B.base, cls + B.base, nplat);
+    if (B.nd_ws == 3) localmax_words<3>(B, S[blockIdx.y], smax, v + B.base, cls + B.base, nplat);
+    else localmax_words<2>(B, S[blockIdx.y], smax, v + B.base, cls + B.base, nplat);
     nplat = wg_reduce_u32(nplat, OpAdd());
     if (threadIdx.x == 0 && nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
 }

@@ -1,0 +1,65 @@
+"""The frontier relaxation's schedule knobs change the order of work, never the result.
+
+The flood's fixpoint (K = f(min of the neighbours' keys), k_flood.hip) is unique, so every
+chunk brick (CTWS_FRONTIER_CHUNK2D / _3D), the LDS-staged iteration 0 (CTWS_FRONTIER_STAGE=1)
+and a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
+non-converged re-queue path runs) must reproduce the oracle's flood model bit for bit on every
+parity case, as the default schedule does (test_gpu_parity.py::test_flood_matches_model_exactly).
+The knobs are read when a handle is opened.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from cases import make_cases, BLOCK_SHAPE
+
+pytestmark = pytest.mark.gpu
+
+CASES = make_cases()
+VARIANTS = {
+    'stage_lds': {'CTWS_FRONTIER_STAGE': '1'},
+    'bricks_a': {'CTWS_FRONTIER_CHUNK2D': '4x16x1', 'CTWS_FRONTIER_CHUNK3D': '2x8x4'},
+    'bricks_b': {'CTWS_FRONTIER_CHUNK2D': '8x8x1', 'CTWS_FRONTIER_CHUNK3D': '4x4x4'},
+    'bricks_c': {'CTWS_FRONTIER_CHUNK2D': '2x32x1', 'CTWS_FRONTIER_CHUNK3D': '1x16x4'},
+    'rows_3d_one_sweep': {'CTWS_FRONTIER_CHUNK3D': '8x8x1', 'CTWS_FRONTIER_REPS': '1'},
+}
+
+
+@pytest.fixture(scope='module', params=sorted(VARIANTS))
+def variant_handle(request):
+    from cluster_tools_amd import ctws
+    env = VARIANTS[request.param]
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        h = ctws.Handle(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    yield h
+    h.close()
+
+
+_REF = {}
+
+
+def _model(name):
+    if name not in _REF:
+        config, block = CASES[name]
+        with O.flood_model():
+            _REF[name] = O.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=3)])[0]
+    return _REF[name]
+
+
+@pytest.mark.parametrize('name', sorted(CASES))
+def test_variant_matches_model(variant_handle, name):
+    config, block = CASES[name]
+    ref = _model(name)
+    res = variant_handle.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=3)])[0]
+    assert res['status'] == ref['status']
+    np.testing.assert_array_equal(res['output'], ref['output'])
