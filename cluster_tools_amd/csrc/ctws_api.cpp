@@ -137,9 +137,15 @@ struct ctws_handle {
     int host_batch_blocks = 0;  // CTWS_HOST_BATCH_BLOCKS: cap on blocks per host-path batch (0: voxel cap)
     int64_t host_batch_voxels = (int64_t)256 << 20;  // CTWS_HOST_BATCH_VOXELS: smaller batches pipeline better  // CTWS_HOST_THREADS: memcpy threads per direction of the host path  // CTWS_D2H_WGS: workgroups of the device-to-host copy kernel (0: hipMemcpyAsync)  // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
-    // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words)
+    // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words).
+    // 3-D batches with a mask default to 1x32x2 instead of 1x8x8: a masked region is one flat
+    // plateau (fin = 1) that the flood crosses hop by hop, and wider bricks in y cut the launches
+    // (config 5: 104 -> 72 ms of relaxation, 156 -> 82 launches; unmasked config 4: 33 vs 41 ms)
     int fchunk2[3] = {1, 64, 1};
     int fchunk3[3] = {1, 8, 8};
+    int fchunk3_masked[3] = {1, 32, 2};
+    int fchunk3_env = 0;  // CTWS_FRONTIER_CHUNK3D given: used for every 3-D batch
+    int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
     int frontier_stage = 0;    // CTWS_FRONTIER_STAGE=1: iteration 0 in LDS (k_frontier_stage; measured slower, opt-in)
     int frontier_grid = 2048;  // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4)
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
@@ -499,9 +505,9 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
 // tile extents of k_flood_packed (PTile) and k_flood (FloodTile)
 // frontier chunk bricks instantiated in k_flood.hip (CTWS_FRONTIER_SHAPES below): index or -1
 int frontier_chunk_kind(int nd, int cw, int cy, int cz) {
-    static const int shapes[9][4] = {{2, 1, 64, 1}, {2, 2, 32, 1}, {2, 4, 16, 1}, {2, 8, 8, 1}, {3, 1, 8, 8},
-                                     {3, 2, 8, 4},  {3, 1, 16, 4}, {3, 4, 4, 4},  {3, 8, 8, 1}};
-    for (int k = 0; k < 9; ++k)
+    static const int shapes[10][4] = {{2, 1, 64, 1}, {2, 2, 32, 1}, {2, 4, 16, 1}, {2, 8, 8, 1}, {3, 1, 8, 8},
+                                      {3, 2, 8, 4},  {3, 1, 16, 4}, {3, 4, 4, 4},  {3, 8, 8, 1}, {3, 1, 32, 2}};
+    for (int k = 0; k < 10; ++k)
         if (shapes[k][0] == nd && shapes[k][1] == cw && shapes[k][2] == cy && shapes[k][3] == cz) return k;
     return -1;
 }
@@ -600,11 +606,11 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     // iteration 0: every chunk with an open voxel
     const dim3 lg((unsigned)std::min<int64_t>((TF / nb + 64 * 64 * kFrontierWavesHost - 1) / (64 * 64 * kFrontierWavesHost) + 1,
                                               1024), nb);
-    const int* fc = pl.nd_ws == 3 ? h->fchunk3 : h->fchunk2;
+    const int* fc = h->fc_cur;
     const int fkind = frontier_chunk_kind(pl.nd_ws, fc[0], fc[1], fc[2]);
 #define CTWS_FRONTIER_SHAPES(X) \
     X(0, 2, 1, 64, 1) X(1, 2, 2, 32, 1) X(2, 2, 4, 16, 1) X(3, 2, 8, 8, 1) X(4, 3, 1, 8, 8) X(5, 3, 2, 8, 4) \
-    X(6, 3, 1, 16, 4) X(7, 3, 4, 4, 4) X(8, 3, 8, 8, 1)
+    X(6, 3, 1, 16, 4) X(7, 3, 4, 4, 4) X(8, 3, 8, 8, 1) X(9, 3, 1, 32, 2)
 #define CTWS_LIST0(K, ND, CW, CY, CZ) \
     case K: k_frontier_list0<CW, CY, CZ><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt); break;
     switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_LIST0) default: h->err = "bad frontier chunk"; return CTWS_EINVAL; }
@@ -851,6 +857,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int64_t maxN = 0, maxNI = 0;
     int maxIZ = 0, maxIY = 0, maxIX = 0;
     const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
+    {
+        bool any_mask = false;
+        for (int i = 0; i < nb; ++i) any_mask |= io[i].mask != nullptr;
+        const int* fc = pl.nd_ws == 2 ? h->fchunk2 : (any_mask && !h->fchunk3_env ? h->fchunk3_masked : h->fchunk3);
+        std::memcpy(h->fc_cur, fc, sizeof(h->fc_cur));
+    }
     for (int i = 0; i < nb; ++i) {
         const ctws_block& b = blocks[i];
         BlockDesc& d = desc[i];
@@ -919,7 +931,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // frontier bitmaps: rows padded to a multiple of 64, and at least 64 words per frontier
         // chunk brick (k_frontier), so that the per-chunk arrays can be indexed at fbase / 64
         {
-            const int* fc = pl.nd_ws == 3 ? h->fchunk3 : h->fchunk2;
+            const int* fc = h->fc_cur;
             const int64_t wpr = (d.X + 63) / 64;
             const int64_t nch = ((wpr + fc[0] - 1) / fc[0]) * ((d.Y + fc[1] - 1) / fc[1]) * ((d.Z + fc[2] - 1) / fc[2]);
             TF += std::max((((int64_t)d.Z * d.Y + 63) / 64) * 64 * wpr, nch * 64);
@@ -2031,7 +2043,10 @@ int ctws_open(int device, ctws_handle** out) {
         }
     };
     if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK2D")) parse_chunk(t, h->fchunk2, false);
-    if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK3D")) parse_chunk(t, h->fchunk3, true);
+    if (const char* t = std::getenv("CTWS_FRONTIER_CHUNK3D")) {
+        parse_chunk(t, h->fchunk3, true);
+        h->fchunk3_env = 1;
+    }
     if (const char* t = std::getenv("CTWS_RELAX")) h->relax = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_STAGE")) h->frontier_stage = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));

@@ -1349,6 +1349,7 @@ CTWS_FRONTIER_INST(3, 2, 8, 4)
 CTWS_FRONTIER_INST(3, 1, 16, 4)
 CTWS_FRONTIER_INST(3, 4, 4, 4)
 CTWS_FRONTIER_INST(3, 8, 8, 1)
+CTWS_FRONTIER_INST(3, 1, 32, 2)
 CTWS_STAGE_INST(2, 1, 64, 1)
 CTWS_STAGE_INST(2, 2, 32, 1)
 CTWS_STAGE_INST(2, 4, 16, 1)
@@ -1358,6 +1359,7 @@ CTWS_STAGE_INST(3, 2, 8, 4)
 CTWS_STAGE_INST(3, 1, 16, 4)
 CTWS_STAGE_INST(3, 4, 4, 4)
 CTWS_STAGE_INST(3, 8, 8, 1)
+CTWS_STAGE_INST(3, 1, 32, 2)
 CTWS_LIST0_INST(1, 64, 1)
 CTWS_LIST0_INST(2, 32, 1)
 CTWS_LIST0_INST(4, 16, 1)
@@ -1366,6 +1368,7 @@ CTWS_LIST0_INST(1, 8, 8)
 CTWS_LIST0_INST(2, 8, 4)
 CTWS_LIST0_INST(1, 16, 4)
 CTWS_LIST0_INST(4, 4, 4)
+CTWS_LIST0_INST(1, 32, 2)
 #undef CTWS_FRONTIER_INST
 #undef CTWS_LIST0_INST
 #undef CTWS_STAGE_INST
