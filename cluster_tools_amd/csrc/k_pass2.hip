@@ -109,8 +109,12 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
     }
 }
 
-// insert keys whose scan-order predecessor holds a different key (only those can be the
-// first appearance); the table keeps the smallest scan key per value
+// insert the keys of the voxels none of whose backward neighbours along the scan axes (3-D:
+// z - 1, y - 1, x - 1; 2-D: y - 1, x - 1 in the slice) holds the same key: a voxel with such a
+// neighbour has a smaller scan key with its value, so it cannot be the first appearance, and
+// the first appearance itself passes (every voxel of smaller scan key that is a neighbour has
+// a smaller key along some axis).  Only a few corner voxels per segment reach the atomics; the
+// table keeps the smallest scan key per value.
 __global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__ D, BlockStat* S,
                                                    const uint64_t* __restrict__ vkey, uint64_t* __restrict__ hkey,
                                                    uint32_t* __restrict__ hpos) {
@@ -125,11 +129,9 @@ __global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__
         if (k == kEmptyKey) continue;
         int z, y, x;
         inner_to_zyx(i, YX, B.X, z, y, x);
-        // predecessor in scan order: z - 1 (3-D) / y - 1 (2-D)
-        if (B.nd_ws == 3 ? z > 0 : y > 0) {
-            const int64_t j = (B.nd_ws == 3) ? i - YX : i - B.X;
-            if (vkey[B.base + j] == k) continue;
-        }
+        if (B.nd_ws == 3 && z > 0 && vkey[B.base + i - YX] == k) continue;
+        if (y > 0 && vkey[B.base + i - B.X] == k) continue;
+        if (x > 0 && vkey[B.base + i - 1] == k) continue;
         const uint32_t f = scan_key(B, z, y, x);
         int64_t s = (int64_t)(mix64(k) & (uint64_t)(cap - 1));
         bool done = false;
@@ -171,16 +173,33 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
-    BLOCK_LOOP(i, B) {
-        const uint64_t k = key[B.base + i];
+    const int lane = threadIdx.x & 63;
+    // every lane of the wave runs the loop body to the shuffles (uniform trip count)
+    const int64_t nfull = (B.N + blockDim.x - 1) / blockDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nfull; i0 += (int64_t)gridDim.x * blockDim.x) {
+        const bool in = i0 < B.N;
+        const int64_t i = in ? i0 : B.N - 1;
+        const uint64_t k = in ? key[B.base + i] : kEmptyKey;
+        // the 64 lanes hold consecutive voxels: only the first lane of each run of equal keys
+        // probes the table and ranks the bitmap, the others take its result
+        const uint64_t kprev = shfl_up_u64(k, 1);
+        const bool start = lane == 0 || kprev != k;
+        const uint64_t starts = __ballot(start);
+        const int s0 = 63 - __builtin_clzll(starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
+        uint32_t pos = 0u, l = 0u;
+        if (start && k != kEmptyKey) {
+            const int64_t s = hash_find(hkey + B.hbase, B.hcap, k);
+            pos = s >= 0 ? hpos[B.hbase + s] : 0u;  // s < 0 cannot happen after insert
+            l = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, pos) + 1u;
+        }
+        pos = (uint32_t)__shfl((int)pos, s0);
+        l = (uint32_t)__shfl((int)l, s0);
+        if (!in) continue;
         if (k == kEmptyKey) {
             lab[B.base + i] = 0;
             fixedv[B.base + i] = 0;
             continue;  // key stays kEmptyKey == kInfKey
         }
-        const int64_t s = hash_find(hkey + B.hbase, B.hcap, k);
-        const uint32_t pos = s >= 0 ? hpos[B.hbase + s] : 0u;  // s < 0 cannot happen after insert
-        const uint32_t l = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, pos) + 1u;
         lab[B.base + i] = l | kFixedBit;
         key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
         fixedv[B.base + i] = 1;
