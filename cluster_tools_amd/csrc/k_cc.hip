@@ -47,10 +47,12 @@ namespace ctws {
 // ---- local maxima classification ---------------------------------------------------------
 // cls bit0: a neighbour is strictly greater; bit1: a neighbour is equal (plateau voxel).
 // Neighbourhood: 6 (3-D ws) or 8 in-plane (2-D ws), as localMaxima3D / localMaxima.
-// Word tiles (wtg grid): a wave classifies 64 consecutive voxels of a row per word, U words
-// per step with every load of the step in flight together (clamped positions, no branches
-// between them).  The x neighbours come from the neighbouring lanes; lane 0 / 63 fetch the
-// voxel left / right of the word with one extra load per row.
+// Word columns (wtg grid): the unit of work is U vertically adjacent words (rows y0 .. y0+U-1
+// of one 64-voxel column of a slice); a wave takes a contiguous range of units and loads the
+// U + 2 rows y0-1 .. y0+U once (every load of the unit in flight together, clamped positions),
+// so each row serves as centre, upper and lower row from registers.  The x neighbours come
+// from the neighbouring lanes; lane 0 / 63 fetch the voxel left / right of the word with one
+// extra load per row (3-D: z neighbours are one load each).
 //
 // Zero short cut: the seed map is >= 0 (a distance transform, Gaussian-smoothed with positive
 // taps), so 0 is its minimum, and a slice (2-D ws) / block (3-D ws) whose dt has a positive
@@ -63,109 +65,102 @@ template <int ND>
 __device__ __forceinline__ void localmax_words(const BlockDesc& B, const BlockStat& st, const uint32_t* __restrict__ smax,
                                                const float* __restrict__ p, uint8_t* __restrict__ cl, uint32_t& nplat) {
     const uint32_t ord0 = 0x80000000u;  // ordf(+0.0f)
-    constexpr int U = 4;
+    constexpr int U = 4, R = U + 2;
     const int Y = B.Y, X = B.X, Z = B.Z;
     const int64_t YX = (int64_t)Y * X;
     const int wpr = (X + 63) >> 6;
-    const int64_t nwords = (int64_t)Z * Y * wpr;
+    const int ngy = (Y + U - 1) / U;
+    const int64_t nunits = (int64_t)Z * wpr * ngy;  // unit = (z, xw, y group), y group fastest
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t per = (nunits + nwaves - 1) / nwaves;
     const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    const int64_t ubeg = wid * per, uend = min(nunits, ubeg + per);
     const float NEG = -__builtin_huge_valf();
     const gptr_t<float> gp = gbl(p);
-    constexpr int NR = ND == 3 ? 1 : 3;  // rows whose x neighbours are needed: y-1, y, y+1 (2-D)
-    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
-        float c[U], up[U], dn[U], zm[U], zp[U], e[U][NR];
-        int64_t ii[U];
-        bool valid[U], yl[U], yh[U], zl[U], zh[U];
-        int xx[U];
+    for (int64_t un = ubeg; un < uend; ++un) {
+        const int gy = (int)(un % ngy);
+        const int64_t strip = un / ngy;
+        const int xw = (int)(strip % wpr), z = (int)(strip / wpr);
+        const int y0 = gy * U;
+        const int x = xw * 64 + lane;
+        const int xc = min(x, X - 1);
+        const int xe = lane == 0 ? max(xc - 1, 0) : min(xc + 1, X - 1);  // lane 0: left, others: right
+        const int64_t zb = (int64_t)z * YX;
+        float rc[R], re[R];  // rows y0-1 .. y0+U (clamped): centre word and edge voxel
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t wu = min(w0 + u, wend - 1);
-            const int64_t row = wu / wpr;
-            const int xw = (int)(wu - row * wpr);
-            const int z = (int)(row / Y), y = (int)(row - (int64_t)z * Y);
-            const int x = xw * 64 + lane;
-            valid[u] = w0 + u < wend && x < X;
-            const int xc = min(x, X - 1);
-            xx[u] = x;
-            const int64_t i = row * X + xc;
-            ii[u] = i;
-            yl[u] = y > 0;
-            yh[u] = y + 1 < Y;
-            zl[u] = z > 0;
-            zh[u] = z + 1 < Z;
-            c[u] = gp[i];
-            up[u] = gp[i - (yl[u] ? X : 0)];
-            dn[u] = gp[i + (yh[u] ? X : 0)];
-            if (ND == 3) {
-                zm[u] = gp[i - (zl[u] ? YX : 0)];
-                zp[u] = gp[i + (zh[u] ? YX : 0)];
+        for (int k = 0; k < R; ++k) {
+            const int yy = min(max(y0 - 1 + k, 0), Y - 1);
+            rc[k] = gp[zb + (int64_t)yy * X + xc];
+            re[k] = gp[zb + (int64_t)yy * X + xe];
+        }
+        float zm[U], zp[U];
+        if (ND == 3) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int yy = min(y0 + u, Y - 1);
+                const int64_t i = zb + (int64_t)yy * X + xc;
+                zm[u] = gp[i - (z > 0 ? YX : 0)];
+                zp[u] = gp[i + (z + 1 < Z ? YX : 0)];
             }
-            // lane 0: the voxel left of the word, every other lane: right of it (lane 63's is
-            // the only one used); clamped into the row
-            const int64_t ie = row * X + (lane == 0 ? max(xc - 1, 0) : min(xc + 1, X - 1));
-            e[u][0] = gp[ie];
-            if (ND == 2) {
-                e[u][1] = gp[ie - (yl[u] ? X : 0)];
-                e[u][2] = gp[ie + (yh[u] ? X : 0)];
+        }
+        const bool xl = x > 0, xh = x + 1 < X;
+        const bool pos = (ND == 2 ? smax[B.sbase + z] : st.dt_max) > ord0;
+        auto left = [&](float v, float ev) {
+            const float t = __shfl(v, (lane + 63) & 63);
+            return lane == 0 ? ev : t;
+        };
+        auto right = [&](float v, float ev) {
+            const float t = __shfl(v, (lane + 1) & 63);
+            const float e63 = __shfl(ev, 63);
+            return lane == 63 ? e63 : t;
+        };
+        float lft[R], rgt[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            if (ND == 2 || (k >= 1 && k <= U)) {
+                lft[k] = left(rc[k], re[k]);
+                rgt[k] = right(rc[k], re[k]);
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int x = xx[u];
-            const bool xl = x > 0, xh = x + 1 < X;
-            // x neighbours of row r (centre, up, down): lanes +-1, the word edges from e[]
-            auto left = [&](float v, float ev) {
-                const float t = __shfl(v, (lane + 63) & 63);
-                return lane == 0 ? ev : t;
-            };
-            auto right = [&](float v, float ev) {
-                const float t = __shfl(v, (lane + 1) & 63);
-                return lane == 63 ? __shfl(ev, 63) : t;
-            };
-            const float cc = c[u];
+            const int y = y0 + u;
+            const int k = u + 1;  // row y in the window
+            const bool yl = y > 0, yh = y + 1 < Y;
+            const float cc = rc[k];
             float w[8];
             if (ND == 3) {
-                w[0] = zl[u] ? zm[u] : NEG;
-                w[1] = zh[u] ? zp[u] : NEG;
-                w[2] = yl[u] ? up[u] : NEG;
-                w[3] = yh[u] ? dn[u] : NEG;
-                const float l = left(cc, e[u][0]), r = right(cc, __shfl(e[u][0], 63));
-                w[4] = xl ? l : NEG;
-                w[5] = xh ? r : NEG;
+                w[0] = z > 0 ? zm[u] : NEG;
+                w[1] = z + 1 < Z ? zp[u] : NEG;
+                w[2] = yl ? rc[k - 1] : NEG;
+                w[3] = yh ? rc[k + 1] : NEG;
+                w[4] = xl ? lft[k] : NEG;
+                w[5] = xh ? rgt[k] : NEG;
                 w[6] = w[7] = NEG;
             } else {
-                const float lc = left(cc, e[u][0]), rc = right(cc, e[u][0]);
-                const float lu = left(up[u], e[u][1]), ru = right(up[u], e[u][1]);
-                const float ld = left(dn[u], e[u][2]), rd = right(dn[u], e[u][2]);
-                w[0] = yl[u] && xl ? lu : NEG;
-                w[1] = yl[u] ? up[u] : NEG;
-                w[2] = yl[u] && xh ? ru : NEG;
-                w[3] = xl ? lc : NEG;
-                w[4] = xh ? rc : NEG;
-                w[5] = yh[u] && xl ? ld : NEG;
-                w[6] = yh[u] ? dn[u] : NEG;
-                w[7] = yh[u] && xh ? rd : NEG;
+                w[0] = yl && xl ? lft[k - 1] : NEG;
+                w[1] = yl ? rc[k - 1] : NEG;
+                w[2] = yl && xh ? rgt[k - 1] : NEG;
+                w[3] = xl ? lft[k] : NEG;
+                w[4] = xh ? rgt[k] : NEG;
+                w[5] = yh && xl ? lft[k + 1] : NEG;
+                w[6] = yh ? rc[k + 1] : NEG;
+                w[7] = yh && xh ? rgt[k + 1] : NEG;
             }
             bool gt = false, eq = false;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                gt |= w[k] > cc;
-                eq |= w[k] == cc;
+            for (int q = 0; q < 8; ++q) {
+                gt |= w[q] > cc;
+                eq |= w[q] == cc;
             }
-            if (cc == 0.0f) {
-                const int z = (int)(ii[u] / ((int64_t)B.Y * B.X));
-                const bool pos = (ND == 2 ? smax[B.sbase + z] : st.dt_max) > ord0;
-                if (pos) {
-                    gt = true;
-                    eq = false;
-                }
+            if (cc == 0.0f && pos) {
+                gt = true;
+                eq = false;
             }
-            if (valid[u]) cl[ii[u]] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
-            nplat += valid[u] && eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
+            const bool valid = y < Y && x < X;
+            if (valid) cl[zb + (int64_t)y * X + x] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
+            nplat += valid && eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
         }
     }
 }

@@ -1400,75 +1400,80 @@ __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restr
 // fixpoint check of the packed flood: K(q) == f(min_p K(p)) at every voxel the relaxation
 // solved (the open bitmap of k_descent_init / k_regrow_init).  The descent-resolved voxels are
 // final by construction (the unique-argmin argument above) and are never written by the
-// relaxation, so a group of words without an open voxel is skipped after its bitmap loads.
-// Word tiles, U words per step with all their loads in flight together: a wave reads a
-// 64-voxel row word coalesced; x-neighbours come from the neighbouring lanes, lane 0 / 63
-// fetch the key left / right of the word.
+// relaxation, so a unit without an open voxel is skipped after its bitmap loads.  Word columns
+// as k_localmax: a unit is U vertically adjacent words of one 64-voxel column, whose U + 2 key
+// rows are loaded once (all loads of the unit in flight together) and serve as centre, upper
+// and lower rows; x-neighbours come from the neighbouring lanes, lane 0 / 63 fetch the key
+// left / right of the word.
 template <int ND>
 __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint64_t* __restrict__ key,
                                                       const uint64_t* __restrict__ open, uint32_t* __restrict__ flag) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    constexpr int U = 4;
+    constexpr int U = 4, R = U + 2;
     const gptr_t<uint64_t> k = gbl(key + B.base);
     const gptr_t<float> hb = gbl(h + B.base);
     const int64_t YX = (int64_t)B.Y * B.X;
     const int wpr = (B.X + 63) >> 6;
-    const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
+    const int ngy = (B.Y + U - 1) / U;
+    const int64_t nunits = (int64_t)B.Z * wpr * ngy;
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t per = (nunits + nwaves - 1) / nwaves;
     const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    const int64_t ubeg = wid * per, uend = min(nunits, ubeg + per);
     bool bad = false;
-    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
+    for (int64_t un = ubeg; un < uend; ++un) {
+        const int gy = (int)(un % ngy);
+        const int64_t strip = un / ngy;
+        const int xw = (int)(strip % wpr), z = (int)(strip / wpr);
+        const int y0 = gy * U;
+        // open words of the unit's rows
         uint64_t ow[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) ow[u] = w0 + u < wend ? gbl(open)[B.fbase + w0 + u] : 0ull;
+        for (int u = 0; u < U; ++u)
+            ow[u] = y0 + u < B.Y ? gbl(open)[B.fbase + ((int64_t)z * B.Y + y0 + u) * wpr + xw] : 0ull;
         bool any = false;
 #pragma unroll
         for (int u = 0; u < U; ++u) any |= ow[u] != 0ull;
-        if (!any) continue;  // every voxel of the group descent-resolved / kept
-        uint64_t own[U], kym[U], kyp[U], kzm[U], kzp[U], ke[U];
+        if (!any) continue;  // every voxel of the unit descent-resolved / kept
+        const int x = xw * 64 + lane;
+        const int xc = min(x, B.X - 1);
+        const int xe = lane == 0 ? max(xc - 1, 0) : min(xc + 1, B.X - 1);
+        const int64_t zb = (int64_t)z * YX;
+        uint64_t rk[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int yy = min(max(y0 - 1 + q, 0), B.Y - 1);
+            rk[q] = k[zb + (int64_t)yy * B.X + xc];
+        }
+        uint64_t ke[U], kzm[U], kzp[U];
         float hv[U];
-        int xx[U], yy[U], zz[U];
-        bool valid[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t wu = min(w0 + u, wend - 1);
-            const int64_t row = wu / wpr;
-            const int xw = (int)(wu - row * wpr);
-            const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
-            const int x = xw * 64 + lane;
-            valid[u] = x < B.X;
-            xx[u] = x;
-            yy[u] = y;
-            zz[u] = z;
-            const int xc = min(x, B.X - 1);
-            const int64_t ic = row * B.X + xc;
-            own[u] = k[ic];
-            kym[u] = k[y > 0 ? ic - B.X : ic];
-            kyp[u] = k[y + 1 < B.Y ? ic + B.X : ic];
+            const int yy = min(y0 + u, B.Y - 1);
+            const int64_t ic = zb + (int64_t)yy * B.X + xc;
+            ke[u] = k[zb + (int64_t)yy * B.X + xe];
+            hv[u] = hb[ic];
             if (ND == 3) {
                 kzm[u] = k[z > 0 ? ic - YX : ic];
                 kzp[u] = k[z + 1 < B.Z ? ic + YX : ic];
             }
-            ke[u] = k[row * B.X + (lane == 0 ? max(xc - 1, 0) : min(xc + 1, B.X - 1))];
-            hv[u] = hb[ic];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int x = xx[u], y = yy[u], z = zz[u];
-            const uint64_t o = valid[u] ? own[u] : kPackInf;
+            const int y = y0 + u;
+            const bool valid = y < B.Y && x < B.X;
+            const uint64_t o = valid ? rk[u + 1] : kPackInf;
             uint64_t l = shfl_up_u64(o, 1), r = shfl_down_u64(o, 1);
             const uint64_t ker = shfl_u64(ke[u], 63);
             if (lane == 0) l = (x > 0) ? ke[u] : kPackInf;
             if (lane == 63) r = ker;
             if (x + 1 >= B.X) r = kPackInf;
             uint64_t m = min(l, r);
-            if (y > 0) m = min(m, kym[u]);
-            if (y + 1 < B.Y) m = min(m, kyp[u]);
+            if (y > 0) m = min(m, rk[u]);
+            if (y + 1 < B.Y) m = min(m, rk[u + 2]);
             if (ND == 3) {
                 if (z > 0) m = min(m, kzm[u]);
                 if (z + 1 < B.Z) m = min(m, kzp[u]);
@@ -1476,10 +1481,10 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
             // an open voxel is never a seed (descent: seeds resolve to themselves; regrow: the
             // survivors and auto seeds are taken out of the open set)
             const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(hv[u]), m);
-            const bool b1 = valid[u] && ((ow[u] >> lane) & 1ull) && e != o;
+            const bool b1 = valid && ((ow[u] >> lane) & 1ull) && e != o;
             if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
                 const uint32_t slot = atomicAdd(&flag[1], 1u);
-                if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + (int64_t)(z * B.Y + y) * B.X + x);
+                if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + zb + (int64_t)y * B.X + x);
             }
             bad |= b1;
         }
