@@ -1214,18 +1214,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             using T = CcTile<3>;
             const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
             k_tile_cc<3, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
-            k_tile_merge<3, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
+            k_tile_merge<3, CC_PLATEAU><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
             k_tile_cc<3, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
-            k_tile_merge<3, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            k_tile_merge<3, CC_SEED><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
         } else {
             using T = CcTile<2>;
             const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
             k_tile_cc<2, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
-            k_tile_merge<2, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
+            k_tile_merge<2, CC_PLATEAU><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
             k_tile_cc<2, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
-            k_tile_merge<2, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            k_tile_merge<2, CC_SEED><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
         }
         LAUNCHCHK();
     }
@@ -1530,12 +1530,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 using T = CcTile<3>;
                 const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
                 k_tile_cc<3, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
-                k_tile_merge<3, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+                k_tile_merge<3, CC_CROP><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             } else {
                 using T = CcTile<2>;
                 const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
                 k_tile_cc<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
-                k_tile_merge<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+                k_tile_merge<2, CC_CROP><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             }
             HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
             k_flatten_roots_w<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);

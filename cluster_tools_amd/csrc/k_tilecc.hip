@@ -282,8 +282,9 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
     int nz, ny, nx;
     domain_dims<MODE>(B, nz, ny, nx);
     const int ntx = (nx + TX - 1) / TX, nty = (ny + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
-    const int t = blockIdx.x;
-    if (t >= ntx * nty * ntz) return;
+    // a workgroup walks several tiles (a face is only a few hundred voxels: one workgroup per
+    // tile would make the dispatch of ~10^5 workgroups the cost)
+    for (int t = blockIdx.x; t < ntx * nty * ntz; t += gridDim.x) {
     const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
     const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
     uint32_t* P = Pg + (MODE == CC_CROP ? B.ibase : B.base);
@@ -361,6 +362,7 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
             uf_union(P, pi, pq);
         }
     }
+    }  // tiles
 }
 
 #define CTWS_TILECC_INST(ND, MODE)                                                                   \
