@@ -129,13 +129,13 @@ struct ctws_handle {
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
-    int gauss_w = 0;  // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
-    int gauss_yx = 1;
-    int words_per_wave = 32;
-    int d2h_wgs = 32;
-    int host_threads = 8;
+    int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
+    int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
+    int words_per_wave = 32;    // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels
+    int d2h_wgs = 32;           // CTWS_D2H_WGS: workgroups of the device-to-host copy kernel (0: hipMemcpyAsync)
+    int host_threads = 8;       // CTWS_HOST_THREADS: memcpy threads per direction of the host path
     int host_batch_blocks = 0;  // CTWS_HOST_BATCH_BLOCKS: cap on blocks per host-path batch (0: voxel cap)
-    int64_t host_batch_voxels = (int64_t)256 << 20;  // CTWS_HOST_BATCH_VOXELS: smaller batches pipeline better  // CTWS_HOST_THREADS: memcpy threads per direction of the host path  // CTWS_D2H_WGS: workgroups of the device-to-host copy kernel (0: hipMemcpyAsync)  // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels  // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
+    int64_t host_batch_voxels = (int64_t)256 << 20;  // CTWS_HOST_BATCH_VOXELS: smaller batches pipeline better
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words).
     // 3-D batches with a mask default to 1x32x2 instead of 1x8x8: a masked region is one flat
