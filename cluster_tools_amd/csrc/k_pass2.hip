@@ -173,33 +173,16 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
-    const int lane = threadIdx.x & 63;
-    // every lane of the wave runs the loop body to the shuffles (uniform trip count)
-    const int64_t nfull = (B.N + blockDim.x - 1) / blockDim.x * blockDim.x;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nfull; i0 += (int64_t)gridDim.x * blockDim.x) {
-        const bool in = i0 < B.N;
-        const int64_t i = in ? i0 : B.N - 1;
-        const uint64_t k = in ? key[B.base + i] : kEmptyKey;
-        // the 64 lanes hold consecutive voxels: only the first lane of each run of equal keys
-        // probes the table and ranks the bitmap, the others take its result
-        const uint64_t kprev = shfl_up_u64(k, 1);
-        const bool start = lane == 0 || kprev != k;
-        const uint64_t starts = __ballot(start);
-        const int s0 = 63 - __builtin_clzll(starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
-        uint32_t pos = 0u, l = 0u;
-        if (start && k != kEmptyKey) {
-            const int64_t s = hash_find(hkey + B.hbase, B.hcap, k);
-            pos = s >= 0 ? hpos[B.hbase + s] : 0u;  // s < 0 cannot happen after insert
-            l = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, pos) + 1u;
-        }
-        pos = (uint32_t)__shfl((int)pos, s0);
-        l = (uint32_t)__shfl((int)l, s0);
-        if (!in) continue;
+    BLOCK_LOOP(i, B) {
+        const uint64_t k = key[B.base + i];
         if (k == kEmptyKey) {
             lab[B.base + i] = 0;
             fixedv[B.base + i] = 0;
             continue;  // key stays kEmptyKey == kInfKey
         }
+        const int64_t s = hash_find(hkey + B.hbase, B.hcap, k);
+        const uint32_t pos = s >= 0 ? hpos[B.hbase + s] : 0u;  // s < 0 cannot happen after insert
+        const uint32_t l = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, pos) + 1u;
         lab[B.base + i] = l | kFixedBit;
         key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
         fixedv[B.base + i] = 1;
