@@ -110,18 +110,11 @@ struct ctws_handle {
     int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
     // EDT: counters (64 B) + columns queued for the lower-envelope pass (k_edt_col_fh)
     DevBuf edt_fh;
-    // LDS tile relaxation (k_relax.hip): tile worklists, queued generation per tile, statistics
-    DevBuf rx_list0, rx_list1, rx_gen, rx_stats;
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
     // evaluation (k_eval.hip): gt / seg / pair hash tables with counts, state, sums, staging
     DevBuf ev_ka, ev_ca, ev_kb, ev_cb, ev_kp, ev_cp, ev_state, ev_out, ev_stage;
     int64_t ev_cap_a = 0, ev_cap_b = 0, ev_cap_p = 0;
-    int64_t rx_tiles = 0;  // relaxation tiles of the current batch
-    // CTWS_RELAX=1: LDS tile relaxation (k_relax.hip) instead of the global-memory frontier.
-    // Off by default: r02 single stream, config 3 50.3 vs 22.6 ms, config 4 64.8 vs 45.1 ms per
-    // step (every tile re-solved ~3x: its halo is stale until the neighbours converged)
-    int relax = 0;
     // test hooks
     int stop_after = 0;
     int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
@@ -146,7 +139,6 @@ struct ctws_handle {
     int fchunk3_masked[3] = {1, 32, 2};
     int fchunk3_env = 0;  // CTWS_FRONTIER_CHUNK3D given: used for every 3-D batch
     int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
-    int frontier_stage = 0;    // CTWS_FRONTIER_STAGE=1: iteration 0 in LDS (k_frontier_stage; measured slower, opt-in)
     int frontier_grid = 2048;  // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4)
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
@@ -588,12 +580,8 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 // key changes.  Batches of kFrontierBatch launches run between host checks of their flags; if
 // it has not converged after frontier_max_iters iterations (very long equal-height paths) the
 // tile flood finishes from the current keys.
-int run_relax(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
-              uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out);
-
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
                  uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
-    if (h->relax) return run_relax(h, pl, nb, TF, max_tiles, TT, packed, fst, iters_out, rounds_out, kms_out);
     Workspace& w = h->ws;
     const int64_t nch = TF / 64 + 1;
     uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
@@ -618,8 +606,6 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     LAUNCHCHK();
     // one wave per list entry; the largest list is every chunk of the batch
     const unsigned fg = (unsigned)std::min<int64_t>((nch + kFrontierWavesHost - 1) / kFrontierWavesHost, h->frontier_grid);
-    // k_frontier_stage: one workgroup per chunk, grid-stride (a multiple of 8 for xcd_swizzle)
-    const unsigned sg = (unsigned)std::min<int64_t>(nch, 2048);
     bool converged = false;
     int fiters = 0;
     while (fiters < h->frontier_max_iters && !converged) {
@@ -640,19 +626,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             h->frontier_reps);                                                                                      \
         break;
-#define CTWS_STAGE(K, ND, CW, CY, CZ)                                                                             \
-    case K:                                                                                                       \
-        k_frontier_stage<ND, CW, CY, CZ><<<sg, 256, 0, h->stream>>>(                                              \
-            w.desc, w.hm, w.key, w.fopen, fb[1], gen[0], wl[0], w.wlcnt, wl[1], w.wlcnt + 1, w.qgen,              \
-            fst ? fst + nb : nullptr, h->frontier_reps);                                                          \
-        break;
-            if (it == 0 && h->frontier_stage) {
-                // iteration 0 with the chunks staged in LDS (k_frontier_stage)
-                switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_STAGE) }
-            } else {
-                switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_FRONTIER) }
-            }
-#undef CTWS_STAGE
+            switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_FRONTIER) }
 #undef CTWS_FRONTIER
             if (h->trace) hipEventRecord(tev[k + 1], h->stream);
         }
@@ -680,88 +654,6 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     }
 #undef CTWS_FRONTIER_SHAPES
     *iters_out += fiters;
-    if (!converged) {
-        int TZ, TY, TX;
-        flood_tile_dims(pl.nd_ws, packed, &TZ, &TY, &TX);
-        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-        k_frontier_tiles<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0,
-                           h->stream>>>(w.desc, w.stat, w.fopen, w.act0, TZ, TY, TX);
-        LAUNCHCHK();
-        int rounds = 0;
-        float kms = 0.f;
-        int r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds, &kms);
-        if (r != CTWS_OK) return r;
-        *rounds_out += rounds;
-        *kms_out += kms;
-    }
-    return CTWS_OK;
-}
-
-// Relaxation of the open voxels in LDS tiles (k_relax.hip): iteration 0 solves every tile
-// that holds an open voxel, later iterations the tiles whose halo changed, until no tile is
-// queued.  Same contract as the frontier loop above (the open bitmap in w.fopen; keys of the
-// other voxels final), same fallback to the tile flood after frontier_max_iters launches.
-int run_relax(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
-              uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
-    Workspace& w = h->ws;
-    const int64_t TR = h->rx_tiles;
-    uint64_t* wl[2] = {(uint64_t*)h->rx_list0.p, (uint64_t*)h->rx_list1.p};
-    uint32_t* tgen = (uint32_t*)h->rx_gen.p;
-    uint32_t* rst = fst ? (uint32_t*)h->rx_stats.p : nullptr;
-    HIPCHK(hipMemsetAsync(tgen, 0, sizeof(uint32_t) * (size_t)TR, h->stream));
-    HIPCHK(hipMemsetAsync(w.wlcnt, 0, sizeof(uint32_t) * (size_t)(h->frontier_max_iters + 2), h->stream));
-    if (rst) HIPCHK(hipMemsetAsync(rst, 0, sizeof(uint32_t) * 128, h->stream));
-    const dim3 lg((unsigned)std::min<int64_t>((TR / nb + 255) / 256 + 1, 1024), nb);
-    if (pl.nd_ws == 3) k_relax_list0<3><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt);
-    else k_relax_list0<2><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt);
-    LAUNCHCHK();
-    // a wave per queued tile (4 per workgroup), grid-stride over the list (its length is on the device)
-    const unsigned rg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((TR + 3) / 4, 2048));
-    bool converged = false;
-    int iters = 0;
-    while (iters < h->frontier_max_iters && !converged) {
-        const int it0 = iters;
-        const int nl = std::min(kFrontierBatch, h->frontier_max_iters - it0);
-        for (int k = 0; k < nl; ++k) {
-            const int it = it0 + k;
-            if (pl.nd_ws == 3)
-                k_tile_relax<3><<<rg, 256, 0, h->stream>>>(w.desc, w.hm, w.key, w.fopen, wl[it & 1], w.wlcnt + it,
-                                                           wl[(it + 1) & 1], w.wlcnt + it + 1, tgen, it, rst);
-            else
-                k_tile_relax<2><<<rg, 256, 0, h->stream>>>(w.desc, w.hm, w.key, w.fopen, wl[it & 1], w.wlcnt + it,
-                                                           wl[(it + 1) & 1], w.wlcnt + it + 1, tgen, it, rst);
-        }
-        LAUNCHCHK();
-        HIPCHK(hipMemcpyAsync(h->h_counter, w.wlcnt + it0, sizeof(uint32_t) * (nl + 1), hipMemcpyDeviceToHost,
-                              h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-        if (h->trace)
-            for (int k = 0; k < nl; ++k) {
-                std::fprintf(stderr, "[ctws] relax it %d: %u tiles\n", it0 + k, h->h_counter[k]);
-                if (!h->h_counter[k + 1]) break;
-            }
-        for (int k = 0; k < nl; ++k) {
-            ++iters;
-            if (!h->h_counter[k + 1]) {  // nothing queued for the next iteration
-                converged = true;
-                break;
-            }
-        }
-    }
-    *iters_out += iters;
-    if (rst) {
-        uint32_t hs[128];
-        HIPCHK(hipMemcpy(hs, rst, sizeof(hs), hipMemcpyDeviceToHost));
-        double v = 0, rr = 0;
-        for (int k = 0; k < 64; ++k) {
-            v += hs[2 * k];
-            rr += hs[2 * k + 1];
-        }
-        // fst[nb..2nb): frontier visits per block (summed over the batch into block 0's slot)
-        uint32_t vv = (uint32_t)std::min(v, 4.0e9);
-        HIPCHK(hipMemcpy(fst + nb, &vv, sizeof(uint32_t), hipMemcpyHostToDevice));
-        if (h->trace) std::fprintf(stderr, "[ctws] relax: %.0f visits, %.0f tile rounds\n", v, rr);
-    }
     if (!converged) {
         int TZ, TY, TX;
         flood_tile_dims(pl.nd_ws, packed, &TZ, &TY, &TX);
@@ -851,7 +743,7 @@ int fs_seeds(ctws_handle* h, const std::vector<BlockDesc>& desc, int nb, int64_t
 int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* blocks, const BlockIO* io, int nb) {
     Workspace& w = h->ws;
     std::vector<BlockDesc> desc(nb);
-    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0, TH = 0, TF = 0, TR = 0;
+    int64_t T = 0, TI = 0, TW = 0, TC = 0, TS = 0, TT = 0, TH = 0, TF = 0;
     int64_t maxH = 0, maxRows = 0, maxIRows = 0;
     int maxZ = 0, maxY = 0, maxX = 0, max_tiles = 0;
     int64_t maxN = 0, maxNI = 0;
@@ -922,12 +814,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
                             (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
         d.fbase = TF;
-        {
-            // LDS relaxation tiles (RTile, k_relax.hip): 1 x 32 x 32 (2-D ws) or 8 x 8 x 16
-            const int rz = pl.nd_ws == 3 ? 8 : 1, ry = pl.nd_ws == 3 ? 8 : 32, rx = pl.nd_ws == 3 ? 16 : 32;
-            d.rbase = TR;
-            TR += (int64_t)((d.Z + rz - 1) / rz) * ((d.Y + ry - 1) / ry) * ((d.X + rx - 1) / rx);
-        }
         // frontier bitmaps: rows padded to a multiple of 64, and at least 64 words per frontier
         // chunk brick (k_frontier), so that the per-chunk arrays can be indexed at fbase / 64
         {
@@ -1014,11 +900,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     set_tiles(true);
     int r;
     if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb, TH, TF)) != CTWS_OK) return r;
-    if ((r = grow(h, h->rx_list0, sizeof(uint64_t) * (size_t)TR)) != CTWS_OK) return r;
-    if ((r = grow(h, h->rx_list1, sizeof(uint64_t) * (size_t)TR)) != CTWS_OK) return r;
-    if ((r = grow(h, h->rx_gen, sizeof(uint32_t) * (size_t)TR)) != CTWS_OK) return r;
-    if ((r = grow(h, h->rx_stats, sizeof(uint32_t) * 128)) != CTWS_OK) return r;
-    h->rx_tiles = TR;
     HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
     h->last_desc = desc;
     std::vector<BlockStat> st(nb);
@@ -2047,8 +1928,6 @@ int ctws_open(int device, ctws_handle** out) {
         parse_chunk(t, h->fchunk3, true);
         h->fchunk3_env = 1;
     }
-    if (const char* t = std::getenv("CTWS_RELAX")) h->relax = std::atoi(t);
-    if (const char* t = std::getenv("CTWS_FRONTIER_STAGE")) h->frontier_stage = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -2071,7 +1950,7 @@ void ctws_close(ctws_handle* h) {
                     w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
                     w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
                     h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p,
-                    h->edt_fh.p, h->rx_list0.p, h->rx_list1.p, h->rx_gen.p, h->rx_stats.p,
+                    h->edt_fh.p,
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
                     h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p};
     for (void* p : ptrs)

@@ -42,7 +42,7 @@ struct BlockDesc {
     int64_t hbase;          // pass 2: offset into the relabel hash arrays
     int64_t hcap;           // pass 2: hash capacity of this block (power of two)
     int64_t fbase;          // offset into the frontier bitmaps (Z*Y rows of ceil(X/64) words)
-    int64_t rbase;          // offset into the per-tile arrays of the LDS tile relaxation (k_relax.hip)
+    int64_t _r0;
 };
 
 struct BlockStat {

@@ -153,14 +153,6 @@ __global__ void k_fs_output(const BlockDesc*, BlockStat*, const uint32_t*, const
                             const uint32_t*, int);
 hipError_t fs_segmented_sort(void* tmp, size_t& bytes, const uint32_t* in, uint32_t* out, int n, int nseg,
                              const int* beg, const int* end, hipStream_t stream);
-template <int ND>
-__global__ void k_relax_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint64_t*, uint32_t*);
-template <int ND>
-__global__ void k_tile_relax(const BlockDesc*, const float*, uint64_t*, const uint64_t*, const uint64_t*,
-                             const uint32_t*, uint64_t*, uint32_t*, uint32_t*, int, uint32_t*);
-template <int ND, int CW, int CY, int CZ>
-__global__ void k_frontier_stage(const BlockDesc*, const float*, uint64_t*, const uint64_t*, uint64_t*, uint32_t*,
-                                 const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 template <int CW, int CY, int CZ>
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);

@@ -1110,233 +1110,12 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
     }
 }
-// Iteration 0 of the frontier relaxation with the chunk staged in LDS.  In iteration 0 every
-// chunk holding an open voxel is active and does most of the relaxation's work in its local
-// sweeps; with keys gathered from HBM every visit touches four or six scattered lines, so the
-// sweeps are bound by line traffic (measured: the launch is ~80 % of the relaxation).  Here
-// one workgroup per chunk loads the chunk's keys with a one-voxel halo and its heights once,
-// coalesced, sweeps in LDS until nothing changes (or `reps` sweeps), and writes back only the
-// changed keys.  The first sweep visits every open voxel.  Halo keys belong to the
-// neighbouring chunks and are read-only here: their later changes reach this chunk through the
-// changed bitmaps in iteration 1, exactly as in k_frontier.  Publishes the same outputs as
-// k_frontier's iteration 0 (changed words, generation, next list), so iterations >= 1 continue
-// with k_frontier.
-template <int ND, int CW, int CY, int CZ>
-__global__ void __launch_bounds__(256) k_frontier_stage(const BlockDesc* __restrict__ D, const float* __restrict__ h,
-                                                        uint64_t* __restrict__ key, const uint64_t* __restrict__ open,
-                                                        uint64_t* __restrict__ cnext, uint32_t* __restrict__ gnext,
-                                                        const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
-                                                        uint32_t* __restrict__ list_next, uint32_t* __restrict__ cnt_next,
-                                                        uint32_t* __restrict__ qgen, uint32_t* __restrict__ nvisit, int reps) {
-    static_assert(ND == 3 || CZ == 1, "");
-    constexpr int VX = 64 * CW, VY = CY, VZ = CZ;  // chunk extent in voxels
-    constexpr int ZO = ND == 3 ? 1 : 0;
-    constexpr int HX = VX + 2, HY = VY + 2, HZ = VZ + 2 * ZO;
-    constexpr int HN = HX * HY * HZ, VN = VX * VY * VZ;
-    constexpr int NHL = (HN + 255) / 256, NVL = VN / 256;
-    static_assert(VN % 256 == 0, "");
-    __shared__ uint64_t skey[HN];  // keys with the halo (kPackInf outside the block)
-    __shared__ uint32_t sh[VN];    // ordered heights of the chunk
-    __shared__ uint64_t sfw[64], schg[64];
-    __shared__ int spre[64];
-    __shared__ int stot;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const uint32_t n_entries = *cnt;
-    const uint32_t wgid = (uint32_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
-    // the wave-0 lane's word of the chunk
-    const int lx = lane % CW, ly = (lane / CW) % CY, lz = lane / (CW * CY);
-    for (uint32_t e0 = wgid; e0 < n_entries; e0 += gridDim.x) {
-        const uint32_t ent = list[e0];
-        const int bi = (int)(ent >> kWlChunkBits);
-        const int ch0 = (int)(ent & ((1u << kWlChunkBits) - 1u));
-        const BlockDesc& B = D[bi];
-        const FChunk<CW, CY, CZ> G(B);
-        const int wpr = G.wpr;
-        const int cplane = G.ncx * G.ncy;
-        const int cx = ch0 % G.ncx, cy = (ch0 / G.ncx) % G.ncy, cz = ch0 / cplane;
-        const int X0 = cx * VX, Y0 = cy * VY, Z0 = cz * VZ;
-        const gptr_t<uint64_t> kb = gbl(key + B.base);
-        const gptr_t<float> hb = gbl(h + B.base);
-        // ---- stage: every load unconditional (clamped position), out-of-block selected away;
-        // groups of SG loads in flight per thread (registers for three workgroups per CU)
-        {
-            constexpr int SG = 6;
-#pragma unroll 1
-            for (int k0 = 0; k0 < NHL; k0 += SG) {
-                uint64_t kv[SG];
-#pragma unroll
-                for (int k = 0; k < SG; ++k) {
-                    const int c = min(t + (k0 + k) * 256, HN - 1);
-                    const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
-                    const int gx = min(max(X0 + hx - 1, 0), B.X - 1), gy = min(max(Y0 + hy - 1, 0), B.Y - 1);
-                    const int gz = min(max(Z0 + hz - ZO, 0), B.Z - 1);
-                    kv[k] = kb[((int64_t)gz * B.Y + gy) * B.X + gx];
-                }
-#pragma unroll
-                for (int k = 0; k < SG; ++k) {
-                    const int c = t + (k0 + k) * 256;
-                    if (k0 + k < NHL && c < HN) {
-                        const int hx = c % HX, hy = (c / HX) % HY, hz = c / (HX * HY);
-                        const int gx = X0 + hx - 1, gy = Y0 + hy - 1, gz = Z0 + hz - ZO;
-                        const bool in = gx >= 0 && gx < B.X && gy >= 0 && gy < B.Y && gz >= 0 && gz < B.Z;
-                        skey[c] = in ? kv[k] : kPackInf;
-                    }
-                }
-            }
-#pragma unroll 1
-            for (int k0 = 0; k0 < NVL; k0 += 8) {
-                float hv[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int c = min(t + (k0 + k) * 256, VN - 1);
-                    const int vx = c % VX, vy = (c / VX) % VY, vz = c / (VX * VY);
-                    const int gx = min(X0 + vx, B.X - 1), gy = min(Y0 + vy, B.Y - 1), gz = min(Z0 + vz, B.Z - 1);
-                    hv[k] = hb[((int64_t)gz * B.Y + gy) * B.X + gx];
-                }
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    if (k0 + k < NVL) sh[t + (k0 + k) * 256] = ordf(hv[k]);
-            }
-        }
-        // wave 0: the chunk's words (open bits, frontier)
-        const int xw = cx * CW + lx, yy = cy * CY + ly, zz = cz * CZ + lz;
-        const bool wok = xw < wpr && yy < B.Y && zz < B.Z;
-        const int wc = wok ? (zz * B.Y + yy) * wpr + xw : 0;
-        uint64_t opw = 0ull, f = 0ull, acc = 0ull;
-        if (wv == 0) {
-            opw = wok ? gbl(open + B.fbase)[wc] : 0ull;
-            f = opw;  // first sweep: every open voxel
-        }
-        bool conv = true;
-        uint32_t vis = 0;
-        __syncthreads();
-        for (int rep = 0;; ++rep) {
-            if (wv == 0) {
-                const int cnt_bits = __popcll(f);
-                int incl = cnt_bits;
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int tt = __shfl_up(incl, o);
-                    if (lane >= o) incl += tt;
-                }
-                sfw[lane] = f;
-                spre[lane] = incl - cnt_bits;
-                schg[lane] = 0ull;
-                if (lane == 63) stot = incl;
-            }
-            __syncthreads();
-            const int total = stot;
-            if (total == 0) break;
-            vis += (uint32_t)total;
-            for (int e = t; e < total; e += 256) {
-                int j = 0;
-#pragma unroll
-                for (int step = 32; step > 0; step >>= 1)
-                    if (spre[j + step] <= e) j += step;
-                const int b = kth_set_bit(sfw[j], e - spre[j]);
-                const int wx = j % CW, wy = (j / CW) % CY, wz = j / (CW * CY);
-                const int vx = wx * 64 + b;
-                const int hc = ((wz + ZO) * HY + wy + 1) * HX + vx + 1;
-                uint64_t m = min(min(skey[hc - 1], skey[hc + 1]), min(skey[hc - HX], skey[hc + HX]));
-                if (ND == 3) m = min(m, min(skey[hc - HX * HY], skey[hc + HX * HY]));
-                if (m != kPackInf) {
-                    const uint64_t k = f_packed(sh[(wz * VY + wy) * VX + vx], m);
-                    if (k != skey[hc]) {
-                        skey[hc] = k;
-                        atomicOr((unsigned long long*)&schg[j], 1ull << b);
-                    }
-                }
-            }
-            __syncthreads();
-            bool ch = false;
-            uint64_t c = 0ull;
-            if (wv == 0) {
-                c = schg[lane];
-                acc |= c;
-                ch = c != 0ull;
-            }
-            if (!__syncthreads_or(ch)) break;
-            if (rep + 1 >= reps) {
-                conv = false;
-                break;
-            }
-            if (wv == 0) {
-                // the in-chunk neighbours of this sweep's changes
-                f = (c << 1) | (c >> 1);
-                const uint64_t cxm = __shfl(c, lx > 0 ? lane - 1 : lane);
-                const uint64_t cxp = __shfl(c, lx < CW - 1 ? lane + 1 : lane);
-                if (lx > 0) f |= cxm >> 63;
-                if (lx < CW - 1 && xw + 1 < wpr) f |= cxp << 63;
-                const uint64_t cym = __shfl(c, ly > 0 ? lane - CW : lane);
-                const uint64_t cyp = __shfl(c, ly < CY - 1 ? lane + CW : lane);
-                if (ly > 0) f |= cym;
-                if (ly < CY - 1 && yy + 1 < B.Y) f |= cyp;
-                if (ND == 3 && CZ > 1) {
-                    const uint64_t czm = __shfl(c, lz > 0 ? lane - CW * CY : lane);
-                    const uint64_t czp = __shfl(c, lz < CZ - 1 ? lane + CW * CY : lane);
-                    if (lz > 0) f |= czm;
-                    if (lz < CZ - 1 && zz + 1 < B.Z) f |= czp;
-                }
-                f &= opw;
-            }
-        }
-        // ---- write back the changed keys (open voxels: inside the block)
-        if (wv == 0) sfw[lane] = acc;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < NVL; ++k) {
-            const int c = t + k * 256;
-            const int vx = c % VX, vy = (c / VX) % VY, vz = c / (VX * VY);
-            const int j = (vz * CY + vy) * CW + (vx >> 6);
-            if ((sfw[j] >> (vx & 63)) & 1ull)
-                key[B.base + ((int64_t)(Z0 + vz) * B.Y + (Y0 + vy)) * B.X + (X0 + vx)] =
-                    skey[((vz + ZO) * HY + vy + 1) * HX + vx + 1];
-        }
-        if (nvisit && t == 0 && vis) atomicAdd(&nvisit[bi], vis);
-        if (wv == 0 && __ballot(acc != 0ull) != 0ull) {
-            // publish (as k_frontier, iteration 0): changed words, generation, the next list
-            const int it = 0;
-            uint64_t* cn = cnext + B.fbase;
-            uint32_t* gn = gnext + (B.fbase >> 6);
-            uint32_t* qg = qgen + (B.fbase >> 6);
-            if (wok) cn[wc] = acc;
-            if (lane == 0) gn[ch0] = ((uint32_t)it + 1u) | (conv ? kGenConv : 0u);
-            const bool fxm = __ballot(lx == 0 && (acc & 1ull)) != 0ull;
-            const bool fxp = __ballot(lx == CW - 1 && (acc >> 63)) != 0ull;
-            const bool fym = __ballot(ly == 0 && acc != 0ull) != 0ull;
-            const bool fyp = __ballot(ly == CY - 1 && acc != 0ull) != 0ull;
-            const bool fzm = ND == 3 && __ballot(lz == 0 && acc != 0ull) != 0ull;
-            const bool fzp = ND == 3 && __ballot(lz == CZ - 1 && acc != 0ull) != 0ull;
-            int cand = -1;
-            if (lane == 0 && !conv) cand = ch0;
-            else if (lane == 1 && fxm && cx > 0) cand = ch0 - 1;
-            else if (lane == 2 && fxp && cx + 1 < G.ncx) cand = ch0 + 1;
-            else if (lane == 3 && fym && cy > 0) cand = ch0 - G.ncx;
-            else if (lane == 4 && fyp && cy + 1 < G.ncy) cand = ch0 + G.ncx;
-            else if (lane == 5 && fzm && cz > 0) cand = ch0 - cplane;
-            else if (lane == 6 && fzp && cz + 1 < G.ncz) cand = ch0 + cplane;
-            bool push = false;
-            if (cand >= 0) push = atomicMax(&qg[cand], (uint32_t)it + 1u) < (uint32_t)it + 1u;
-            const uint64_t pm = __ballot(push);
-            uint32_t base = 0;
-            if (lane == 0 && pm) base = atomicAdd(cnt_next, (uint32_t)__popcll(pm));
-            base = (uint32_t)__shfl((int)base, 0);
-            if (push)
-                list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
-        }
-        __syncthreads();  // LDS is restaged for the next chunk
-    }
-}
 // chunk bricks: 2-D ws (CZ = 1) and 3-D; CTWS_FRONTIER_CHUNK selects one (frontier_chunk_dims)
 #define CTWS_FRONTIER_INST(ND, CW, CY, CZ)                                                                           \
     template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
                                                         const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,  \
                                                         uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*,   \
                                                         uint32_t*, uint32_t*, uint32_t*, int);
-#define CTWS_STAGE_INST(ND, CW, CY, CZ)                                                                           \
-    template __global__ void k_frontier_stage<ND, CW, CY, CZ>(const BlockDesc*, const float*, uint64_t*,           \
-                                                              const uint64_t*, uint64_t*, uint32_t*, const uint32_t*, \
-                                                              const uint32_t*, uint32_t*, uint32_t*, uint32_t*,       \
-                                                              uint32_t*, int);
 #define CTWS_LIST0_INST(CW, CY, CZ)                                                                             \
     template __global__ void k_frontier_list0<CW, CY, CZ>(const BlockDesc*, const BlockStat*, const uint64_t*, \
                                                           uint32_t*, uint32_t*);
@@ -1350,16 +1129,6 @@ CTWS_FRONTIER_INST(3, 1, 16, 4)
 CTWS_FRONTIER_INST(3, 4, 4, 4)
 CTWS_FRONTIER_INST(3, 8, 8, 1)
 CTWS_FRONTIER_INST(3, 1, 32, 2)
-CTWS_STAGE_INST(2, 1, 64, 1)
-CTWS_STAGE_INST(2, 2, 32, 1)
-CTWS_STAGE_INST(2, 4, 16, 1)
-CTWS_STAGE_INST(2, 8, 8, 1)
-CTWS_STAGE_INST(3, 1, 8, 8)
-CTWS_STAGE_INST(3, 2, 8, 4)
-CTWS_STAGE_INST(3, 1, 16, 4)
-CTWS_STAGE_INST(3, 4, 4, 4)
-CTWS_STAGE_INST(3, 8, 8, 1)
-CTWS_STAGE_INST(3, 1, 32, 2)
 CTWS_LIST0_INST(1, 64, 1)
 CTWS_LIST0_INST(2, 32, 1)
 CTWS_LIST0_INST(4, 16, 1)
@@ -1371,7 +1140,6 @@ CTWS_LIST0_INST(4, 4, 4)
 CTWS_LIST0_INST(1, 32, 2)
 #undef CTWS_FRONTIER_INST
 #undef CTWS_LIST0_INST
-#undef CTWS_STAGE_INST
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,

@@ -1,8 +1,7 @@
 """The frontier relaxation's schedule knobs change the order of work, never the result.
 
 The flood's fixpoint (K = f(min of the neighbours' keys), k_flood.hip) is unique, so every
-chunk brick (CTWS_FRONTIER_CHUNK2D / _3D), the LDS-staged iteration 0 (CTWS_FRONTIER_STAGE=1)
-and a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
+chunk brick (CTWS_FRONTIER_CHUNK2D / _3D) and a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
 non-converged re-queue path runs) must reproduce the oracle's flood model bit for bit on every
 parity case, as the default schedule does (test_gpu_parity.py::test_flood_matches_model_exactly).
 The knobs are read when a handle is opened.
@@ -19,7 +18,6 @@ pytestmark = pytest.mark.gpu
 
 CASES = make_cases()
 VARIANTS = {
-    'stage_lds': {'CTWS_FRONTIER_STAGE': '1'},
     'bricks_a': {'CTWS_FRONTIER_CHUNK2D': '4x16x1', 'CTWS_FRONTIER_CHUNK3D': '2x8x4'},
     'bricks_b': {'CTWS_FRONTIER_CHUNK2D': '8x8x1', 'CTWS_FRONTIER_CHUNK3D': '4x4x4'},
     'bricks_c': {'CTWS_FRONTIER_CHUNK2D': '2x32x1', 'CTWS_FRONTIER_CHUNK3D': '1x16x4'},
