@@ -200,8 +200,24 @@ def cpu_model():
     return 'unknown'
 
 
-def cpu_baseline(cfg_id, max_cores=16):
-    """Oracle over the first n_jobs = min(n_blocks, cores) blocks, one process per block."""
+def effective_cores():
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU quota (a GPU box
+    shares a large host: nproc shows all of its CPUs, the quota is this job's share)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(cfg_id, max_cores=None):
+    """Oracle over the first n_jobs = min(n_blocks, cores) blocks, one process per block
+    (LocalTask: n_jobs = min(n_blocks, max_jobs), cluster_tasks.py:500,524-529, with max_jobs =
+    the CPUs this job may use)."""
     import multiprocessing as mp
     from concurrent.futures import ProcessPoolExecutor
     from oracle import oracle as O
@@ -211,7 +227,7 @@ def cpu_baseline(cfg_id, max_cores=16):
     blist = geo['blocks']
     if cfg.get('two_pass'):
         blist = [b for b in blist if block_colour(cfg, geo, b) == 0]   # pass-1 blocks (_ws_block)
-    cores = min(max_cores, len(os.sched_getaffinity(0)))
+    cores = effective_cores() if not max_cores else min(max_cores, effective_cores())
     n_jobs = min(len(blist), cores)
     ctx = mp.get_context('fork')
     barrier = ctx.Barrier(n_jobs)
@@ -224,9 +240,40 @@ def cpu_baseline(cfg_id, max_cores=16):
     out = {'value': inner / wall / 1e9, 'unit': 'Gvoxel/s', 'cores': n_jobs, 'kind': 'port',
            'cpu': cpu_model(),
            'sample': '%d of the config\'s %d blocks, one single-threaded oracle process per block (LocalTask '
-                     'model, n_jobs = min(n_blocks, %d cores)); %.1f s wall, %.1f s mean per block'
-                     % (n_jobs, len(blist), cores, wall, float(np.mean(per)))}
+                     'model, n_jobs = min(n_blocks, %d usable cores: affinity and cgroup quota, %d online)); '
+                     '%.1f s wall, %.1f s mean per block'
+                     % (n_jobs, len(blist), cores, os.cpu_count() or 0, wall, float(np.mean(per)))}
     return out, (blist[0]['block_id'], res[0][2])
+
+
+def pcie_rates(dev, nbytes=1 << 30, reps=4):
+    """Pinned host <-> HBM copy rates (GB/s) of this box: each direction alone, and both at once on
+    two streams (full duplex: the host path's uploads and downloads overlap)."""
+    import torch
+    hin = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    hout = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    din = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dout = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def run(h2d, d2h):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if h2d:
+                with torch.cuda.stream(s1):
+                    din.copy_(hin, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s2):
+                    hout.copy_(dout, non_blocking=True)
+        torch.cuda.synchronize()
+        return nbytes * reps / (time.perf_counter() - t0) / 1e9
+
+    run(True, True)
+    out = {'h2d_gbs': round(run(True, False), 1), 'd2h_gbs': round(run(False, True), 1),
+           'duplex_each_gbs': round(run(True, True), 1), 'bytes_per_copy': nbytes}
+    del hin, hout, din, dout
+    return out
 
 
 def progress(msg):
@@ -245,7 +292,7 @@ def main():
     ap.add_argument('--config', type=int, default=DEFAULT_CONFIG, choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe-inclusive) pass')
-    ap.add_argument('--cpu-cores', type=int, default=16)
+    ap.add_argument('--cpu-cores', type=int, default=0, help='cap on the CPU baseline jobs (0: usable cores)')
     ap.add_argument('--streams', type=int, default=3,
                     help='library handles (one HIP stream each) per GPU, driven from host threads; '
                          'the blocks are split between them so their launch-bound phases overlap')
@@ -417,15 +464,22 @@ def main():
                            mask=b['mask'].cpu().numpy() if b.get('mask') is not None else None,
                            out=np.empty(tuple(b['output'].shape), dtype=np.uint64)))
         handles[0].ws_blocks(cfg['task'], cfg['block_shape'], hb)  # warm the staging buffers
-        t0 = time.perf_counter()
-        handles[0].ws_blocks(cfg['task'], cfg['block_shape'], hb)
-        th = time.perf_counter() - t0
+        ths = []
+        for _ in range(max(1, min(3, args.steps))):
+            t0 = time.perf_counter()
+            handles[0].ws_blocks(cfg['task'], cfg['block_shape'], hb)
+            ths.append(time.perf_counter() - t0)
+        th = min(ths)
+        phases = {k: round(v, 2) for k, v in handles[0].timings().items() if k.startswith('host_')}
         same = all(np.array_equal(h_['out'], b['output'].cpu().numpy().view(np.uint64))
-                   for h_, b in zip(hb[:2], passes[0][:2]))
+                   for h_, b in zip(hb, passes[0]))
+        h2d = int(sum(x['input'].nbytes + (x['mask'].nbytes if x['mask'] is not None else 0) for x in hb))
         host = {'value': round(inner_vox / th / 1e9, 4), 'unit': 'Gvoxel/s', 'ms_per_step': round(th * 1e3, 3),
-                'path': 'ctws_ws_blocks: host numpy input -> HBM -> host numpy uint64 output, one handle',
-                'h2d_bytes': int(sum(x['input'].nbytes for x in hb)), 'd2h_bytes': int(inner_vox * 8),
-                'matches_device_path': bool(same)}
+                'runs_ms': [round(t * 1e3, 1) for t in ths],
+                'path': 'ctws_ws_blocks: host numpy input -> pinned staging -> HBM -> uint32 local labels -> '
+                        'pinned -> widened with the block id offset into the host numpy uint64 output, one handle',
+                'h2d_bytes': h2d, 'd2h_bytes': int(inner_vox * 4), 'host_output_bytes': int(inner_vox * 8),
+                'phases_ms': phases, 'pcie': pcie_rates(dev), 'matches_device_path': bool(same)}
         del hb
 
     # ---- VI of the GPU output vs the oracle on the CPU baseline's first block ---------------
@@ -476,7 +530,10 @@ def main():
                        'block_shape': list(cfg['block_shape']),
                        'halo': list(cfg['halo']), 'blocks_per_gpu': nblocks, 'passes': len(passes),
                        'inner_voxels_per_gpu': inner_vox, 'outer_voxels_per_gpu': outer_vox,
-                       'streams_per_gpu': nstreams, 'parallelism': 'blocks sharded, %d GPU(s)' % world},
+                       'streams_per_gpu': nstreams, 'parallelism': 'blocks sharded, %d GPU(s)' % world,
+                       'pass2_order': ('relaxed: every pass-2 block reads ds_out[input_bb] before any pass-2 '
+                                       'write (the reference with n_jobs >= n_blocks); the workflow serialises '
+                                       'overlapping halo corners (watershed.make_batches)') if two_pass else None},
             'roofline': {'bound': 'hbm', 'kernel': '%s (%s)' % (dom, STAGE_KERNELS[dom]),
                          'ms_per_step': round(dom_ms, 3), 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,

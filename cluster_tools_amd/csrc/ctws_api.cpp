@@ -107,6 +107,7 @@ struct ctws_handle {
     hipStream_t s_in = nullptr, s_out = nullptr;
     // relabel (k_relabel.hip)
     DevBuf rl_lab, rl_bits, rl_cnt, rl_offs, rl_out, rl_keys, rl_vals, rl_red;
+    DevBuf rl_sorted, rl_uniq, rl_counts, rl_tmp;  // sort-based unique
     int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
     // EDT: counters (64 B) + columns queued for the lower-envelope pass (k_edt_col_fh)
     DevBuf edt_fh;
@@ -143,6 +144,12 @@ struct ctws_handle {
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
+    // pass 2 (2-D): per block of the next run_batch, the slice offsets of its previous run (empty:
+    // none); a block with a wrapped-id merge runs again until its offsets are self-consistent
+    std::vector<std::vector<uint32_t>> p2_hints;
+    DevBuf p2_hint_dev;
+    int p2_depth = 0;
+    std::vector<uint8_t> last_bare;  // run_batch: per block, an in-mask voxel got the bare offset
     // RCCL
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -304,6 +311,7 @@ struct BlockIO {
     const uint8_t* mask;
     const uint64_t* init;
     uint64_t* out;
+    uint32_t* out32 = nullptr;  // host path: compact uint32 codes (widened on the host)
 };
 
 struct Plan {
@@ -781,6 +789,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         d.mask = io[i].mask;
         d.init = io[i].init;
         d.out = io[i].out;
+        d.out32 = io[i].out32;
         d.n_channels = b.n_channels;
         d.dtype = b.input_dtype;
         if (b.n_channels > 0) {
@@ -800,6 +809,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         d.id_offset = (uint64_t)b.block_id * bvol;
         d.pass2 = (uint32_t)pl.pass2;
+        d.p2hint = -1;
         if (pl.pass2 || pl.from_seeds) {
             if (!d.init) {
                 h->err = "pass 2 needs initial_seeds (ds_out[input_bb]) for every block";
@@ -848,7 +858,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             h->err = "inner block outside the outer block";
             return CTWS_EINVAL;
         }
-        if (!d.input || !d.out) {
+        if (!d.input || (!d.out && !d.out32)) {
             h->err = "null input/output";
             return CTWS_EINVAL;
         }
@@ -900,6 +910,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     set_tiles(true);
     int r;
     if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb, TH, TF)) != CTWS_OK) return r;
+    if (pl.pass2 && pl.nd_ws == 2 && (int)h->p2_hints.size() == nb) {
+        std::vector<uint32_t> flat;
+        for (int i = 0; i < nb; ++i) {
+            if ((int)h->p2_hints[i].size() != desc[i].Z) continue;
+            desc[i].p2hint = (int64_t)flat.size();
+            flat.insert(flat.end(), h->p2_hints[i].begin(), h->p2_hints[i].end());
+        }
+        if (!flat.empty()) {
+            if ((r = grow(h, h->p2_hint_dev, sizeof(uint32_t) * flat.size())) != CTWS_OK) return r;
+            HIPCHK(hipMemcpy(h->p2_hint_dev.p, flat.data(), sizeof(uint32_t) * flat.size(), hipMemcpyHostToDevice));
+        }
+    }
     HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
     h->last_desc = desc;
     std::vector<BlockStat> st(nb);
@@ -1121,7 +1143,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
         HIPCHK(hipMemsetAsync(w.hkey, 0xFF, sizeof(uint64_t) * (size_t)TH, h->stream));
         HIPCHK(hipMemsetAsync(w.hpos, 0xFF, sizeof(uint32_t) * (size_t)TH, h->stream));
-        k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.sb, w.key);
+        k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.sb, (const uint32_t*)h->p2_hint_dev.p, w.key);
         k_p2_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.hkey, w.hpos);
         HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
         const dim3 hg((unsigned)std::min<int64_t>((maxH + 255) / 256, 4096), nb);
@@ -1439,12 +1461,16 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     }
 
     HIPCHK(hipMemcpyAsync(st.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
-    std::vector<uint32_t> sbh, inmask;
+    std::vector<uint32_t> sbh, inmask, soffh;
     if (pl.pass2) {
         sbh.resize(TS);
         inmask.resize(TS);
         HIPCHK(hipMemcpyAsync(sbh.data(), w.sb, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipMemcpyAsync(inmask.data(), w.smin, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+        if (pl.nd_ws == 2) {
+            soffh.resize(TS);
+            HIPCHK(hipMemcpyAsync(soffh.data(), w.soff, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+        }
     }
     HIPCHK(hipStreamSynchronize(h->stream));
     for (size_t i = 1; i < ev; ++i) {
@@ -1464,6 +1490,21 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     add_timing(h, "flood_local_iters", (float)h->flood_iters);
     add_timing(h, "flood_lines_swept", (float)h->flood_lines);
     add_timing(h, "size_filter_kernel_ms", fk2);
+    // pass 2 (2-D): blocks whose relabel needs the wrapped-id merge (k_p2_check) or whose offsets
+    // differ from the hint they ran with run again with their offsets as the hint
+    std::vector<int> redo;
+    std::vector<std::vector<uint32_t>> redo_hint;
+    if (pl.pass2 && pl.nd_ws == 2) {
+        for (int i = 0; i < nb; ++i) {
+            if (!st[i].active) continue;
+            std::vector<uint32_t> so(soffh.begin() + desc[i].sbase, soffh.begin() + desc[i].sbase + desc[i].Z);
+            const bool again = desc[i].p2hint < 0 ? (st[i].err & kErrCollision) != 0 : so != h->p2_hints[i];
+            if (!again || (st[i].err & ~kErrCollision)) continue;  // (other failures stay failures)
+            if (h->p2_depth > desc[i].Z + 1) continue;  // not converging: reported as a collision
+            redo.push_back(i);
+            redo_hint.push_back(std::move(so));
+        }
+    }
     for (int i = 0; i < nb; ++i) {
         blocks[i].status = st[i].active ? CTWS_BLOCK_WRITTEN : (pl.pass2 ? CTWS_BLOCK_EMPTY_PASS2 : CTWS_BLOCK_EMPTY);
         blocks[i].max_label = st[i].active ? st[i].max_label : 0;
@@ -1477,7 +1518,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const uint32_t bare = (st[i].active ? st[i]._p[0] : 1u) && desc[i].id_offset != 0;
         blocks[i].n_ids = (pl.pass2 || pl.from_seeds) ? -1 : (int32_t)((st[i].active ? st[i].n_cc : 0u) + bare);
         if (!st[i].active) continue;
+        if (std::find(redo.begin(), redo.end(), i) != redo.end()) continue;  // filled by the re-run below
         uint32_t err = st[i].err | (regrow_bad ? kErrVerify : 0u);
+        if (desc[i].p2hint >= 0 && !soffh.empty() &&
+            !std::equal(h->p2_hints[i].begin(), h->p2_hints[i].end(), soffh.begin() + desc[i].sbase))
+            err |= kErrCollision;  // the re-runs did not converge
         const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
         if (pl.pass2) {
             // a slice/block without any seed: watershedsNew seeds from the hmap minima and the
@@ -1497,7 +1542,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             char msg[256];
             std::snprintf(msg, sizeof msg, "block %lld failed (%s%s%s%s%s%s%s); ", (long long)blocks[i].block_id,
                           (err & kErrHashFull) ? "pass-2 relabel hash table full " : "",
-                          (err & kErrCollision) ? "pass-2 2-D wrapped id collision not resolved " : "",
+                          (err & kErrCollision) ? "pass-2 2-D wrapped-id merge did not converge " : "",
                           (err & kErrLabelBits) ? "auto-seed labels beyond 2^20 " : "",
                           (err & kErrTakeDict) ? "takeDict: no new_to_old entry, as in the reference " : "",
                           (err & kErrUnsupported) ? "auto-seeded regrow with >= 2^20 seeds " : "",
@@ -1506,6 +1551,32 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             h->err += msg;
         }
     }
+    // per block: an in-mask voxel without a label (its output is the bare id offset), for the
+    // host path's widening of the uint32 codes (empty blocks: every in-mask voxel)
+    std::vector<uint8_t> bare(nb);
+    for (int i = 0; i < nb; ++i) bare[i] = st[i].active ? (st[i]._p[0] != 0) : 1;
+    if (!redo.empty()) {
+        std::vector<ctws_block> rb;
+        std::vector<BlockIO> rio;
+        for (int i : redo) {
+            rb.push_back(blocks[i]);
+            rio.push_back(io[i]);
+        }
+        auto saved = std::move(h->p2_hints);
+        h->p2_hints = std::move(redo_hint);
+        ++h->p2_depth;
+        const int rr = run_batch(h, cfg, pl, rb.data(), rio.data(), (int)rb.size());
+        --h->p2_depth;
+        h->p2_hints = std::move(saved);
+        if (rr != CTWS_OK) return rr;
+        for (size_t k = 0; k < redo.size(); ++k) {
+            blocks[redo[k]].status = rb[k].status;
+            blocks[redo[k]].max_label = rb[k].max_label;
+            blocks[redo[k]].n_ids = rb[k].n_ids;
+        }
+        add_timing(h, "p2_merge_reruns", (float)redo.size());
+    }
+    h->last_bare = std::move(bare);
     return CTWS_OK;
 }
 
@@ -1574,6 +1645,45 @@ int grow_pinned(ctws_handle* h, void*& p, size_t& have, size_t bytes) {
     return CTWS_OK;
 }
 
+// uint32 codes of a block's inner region (k_output: the local label) -> the caller's uint64
+// output: code + off, except for masked voxels (0).  A zero code is a masked voxel, or -- when
+// the block has `bare` voxels (in-mask without a label) or off == 0 -- looked up in the caller's
+// mask.  Rows are split over the threads.
+void widen_codes(const ctws_block& b, const uint32_t* codes, uint64_t off, bool bare, unsigned max_threads) {
+    const int64_t IZ = b.inner_shape[0], IY = b.inner_shape[1], IX = b.inner_shape[2];
+    const int64_t rows = IZ * IY;
+    const uint8_t* mask = (b.mask && off != 0 && bare) ? b.mask : nullptr;
+    const bool masked = b.mask != nullptr;
+    auto work = [&](int64_t r0, int64_t r1) {
+        for (int64_t r = r0; r < r1; ++r) {
+            const uint32_t* c = codes + r * IX;
+            uint64_t* o = b.output + r * IX;
+            if (!masked || off == 0) {
+                for (int64_t x = 0; x < IX; ++x) o[x] = (uint64_t)c[x] + off;
+            } else if (!mask) {
+                for (int64_t x = 0; x < IX; ++x) o[x] = c[x] ? (uint64_t)c[x] + off : 0ull;
+            } else {
+                const int64_t z = r / IY, y = r - z * IY;
+                const uint8_t* m = mask + ((z + b.inner_begin[0]) * b.outer_shape[1] + (y + b.inner_begin[1])) *
+                                              b.outer_shape[2] + b.inner_begin[2];
+                for (int64_t x = 0; x < IX; ++x) o[x] = (c[x] || m[x]) ? (uint64_t)c[x] + off : 0ull;
+            }
+        }
+    };
+    const int64_t bytes = rows * IX * 12;
+    const unsigned nt = std::max(1u, std::min(max_threads, std::thread::hardware_concurrency()));
+    if (nt == 1 || bytes < (16ll << 20)) {
+        work(0, rows);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) {
+        const int64_t r0 = rows * t / nt, r1 = rows * (t + 1) / nt;
+        if (r0 < r1) th.emplace_back(work, r0, r1);
+    }
+    for (auto& t : th) t.join();
+}
+
 struct HostBatch {
     int k, nb;  // blocks todo[k .. k + nb)
     std::vector<size_t> in_off, in_sz, m_off, i_off, o_off, o_sz;
@@ -1615,7 +1725,7 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             if (b.mask) B.in_bytes += al((size_t)nv);
             B.i_off.push_back(b.initial_seeds ? B.in_bytes : 0);
             if (b.initial_seeds) B.in_bytes += al((size_t)nv * 8);
-            B.o_sz.push_back((size_t)(b.inner_shape[0] * b.inner_shape[1] * b.inner_shape[2]) * 8);
+            B.o_sz.push_back((size_t)(b.inner_shape[0] * b.inner_shape[1] * b.inner_shape[2]) * 4);  // uint32 codes
             B.o_off.push_back(B.out_bytes);
             B.out_bytes += al(B.o_sz.back());
         }
@@ -1645,6 +1755,9 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
         HIPCHK(hipEventRecord(sl.ev_d2h, h->s_out));
         HIPCHK(hipEventRecord(sl.ev_comp, h->stream));
     }
+    // wall times (summed over batches) of the packing, widening and compute phases; the first
+    // two run on worker threads, so they are only added to the timings at the end
+    double pack_ms = 0.0, unpack_ms = 0.0, compute_ms = 0.0;
     // pack batch j's inputs into its slot and start the upload (worker thread)
     // pack batch j's inputs block by block into its slot, each block's upload starting as soon
     // as it is packed (worker thread)
@@ -1674,25 +1787,34 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
                             hipMemcpyHostToDevice, h->s_in) != hipSuccess)
                 return CTWS_EHIP;
         }
-        if (h->trace)
-            std::fprintf(stderr, "[ctws] host batch %d: pack %.1f ms (%zu B)\n", j,
-                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3, B.in_bytes);
+        const double ms = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3;
+        pack_ms += ms;
+        if (h->trace) std::fprintf(stderr, "[ctws] host batch %d: pack %.1f ms (%zu B)\n", j, ms, B.in_bytes);
         return hipEventRecord(sl.ev_h2d, h->s_in) == hipSuccess ? CTWS_OK : CTWS_EHIP;
     };
-    // unpack batch j's outputs block by block as their downloads complete (worker thread)
+    // widen batch j's uint32 codes into the callers' uint64 outputs block by block as their
+    // downloads complete (worker thread)
+    const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
+    std::vector<std::vector<uint8_t>> bare_of(hb.size());
     auto drain_out = [&](int j, std::vector<ctws_block>* bbp) -> int {
         const HostBatch& B = hb[j];
         auto& sl = h->hslot[j % nslots];
         const auto t0 = std::chrono::steady_clock::now();
         for (int i = 0; i < B.nb; ++i) {
-            if ((*bbp)[i].status == CTWS_BLOCK_EMPTY_PASS2) continue;  // nothing written (:240-242)
+            const int st = (*bbp)[i].status;
+            // nothing written: pass-2 empty (:240-242) or a failed block
+            if (st == CTWS_BLOCK_EMPTY_PASS2 || st == CTWS_BLOCK_FAILED) continue;
             if (hipEventSynchronize(sl.ev_blk[i]) != hipSuccess) return CTWS_EHIP;
-            par_memcpy({{blocks[todo[B.k + i]].output, (char*)sl.pin_out + B.o_off[i]}}, {B.o_sz[i]},
-                       (unsigned)h->host_threads);
+            const ctws_block& b = blocks[todo[B.k + i]];
+            // pass 1: in-mask voxels get + block_id * prod(block_shape); pass 2 / from-seeds
+            // outputs are the uint32 values themselves
+            const uint64_t off = (pl.pass2 || pl.from_seeds) ? 0ull : (uint64_t)b.block_id * bvol;
+            widen_codes(b, (const uint32_t*)((char*)sl.pin_out + B.o_off[i]), off, bare_of[j][i] != 0,
+                        (unsigned)h->host_threads);
         }
-        if (h->trace)
-            std::fprintf(stderr, "[ctws] host batch %d: unpack %.1f ms (%zu B)\n", j,
-                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3, B.out_bytes);
+        const double ms = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3;
+        unpack_ms += ms;
+        if (h->trace) std::fprintf(stderr, "[ctws] host batch %d: unpack %.1f ms (%zu B)\n", j, ms, B.out_bytes);
         return CTWS_OK;
     };
     for (auto& sl : h->hslot) HIPCHK(hipEventRecord(sl.ev_h2d, h->s_in));
@@ -1718,7 +1840,8 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             io[i].in = (char*)sl.d_in.p + B.in_off[i];
             io[i].mask = b.mask ? (const uint8_t*)((char*)sl.d_in.p + B.m_off[i]) : nullptr;
             io[i].init = b.initial_seeds ? (const uint64_t*)((char*)sl.d_in.p + B.i_off[i]) : nullptr;
-            io[i].out = (uint64_t*)((char*)sl.d_out.p + B.o_off[i]);
+            io[i].out = nullptr;
+            io[i].out32 = (uint32_t*)((char*)sl.d_out.p + B.o_off[i]);
         }
         // inputs uploaded; the slot's previous outputs downloaded
         if (hipEventSynchronize(sl.ev_h2d) != hipSuccess || hipEventSynchronize(sl.ev_d2h) != hipSuccess) {
@@ -1730,10 +1853,13 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             join_all();
             return r;
         }
-        if (h->trace)
-            std::fprintf(stderr, "[ctws] host batch %zu: compute %.1f ms\n", j,
-                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count() * 1e3);
+        {
+            const double ms = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count() * 1e3;
+            compute_ms += ms;
+            if (h->trace) std::fprintf(stderr, "[ctws] host batch %zu: compute %.1f ms\n", j, ms);
+        }
         HIPCHK(hipEventRecord(sl.ev_comp, h->stream));
+        bare_of[j] = h->last_bare;
         // the slot's pinned outputs are free once the drain of batch j - 2 finished
         if (t_out.joinable()) t_out.join();
         if (r_out != CTWS_OK) {
@@ -1779,6 +1905,10 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
         }
     }
     join_all();
+    add_timing(h, "host_pack_ms", (float)pack_ms);
+    add_timing(h, "host_unpack_ms", (float)unpack_ms);
+    add_timing(h, "host_compute_ms", (float)compute_ms);
+    add_timing(h, "host_batches", (float)hb.size());
     return r_out;
 }
 
@@ -1950,7 +2080,7 @@ void ctws_close(ctws_handle* h) {
                     w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
                     w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
                     h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p,
-                    h->edt_fh.p,
+                    h->edt_fh.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
                     h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p};
     for (void* p : ptrs)
@@ -1999,23 +2129,23 @@ int ctws_eval_begin(ctws_handle* h, int64_t cap_labels, int64_t cap_pairs) {
     HIPCHK(hipSetDevice(h->device));
     const int64_t ca = pow2_at_least(2 * std::max<int64_t>(cap_labels, 1));
     const int64_t cp = pow2_at_least(2 * std::max<int64_t>(cap_pairs, 1));
-    if (ca > (1ll << 32) || cp > (1ll << 33)) {
+    if (ca > (1ll << 31) || cp > (1ll << 33)) {  // slots + the 2^64 - 1 slot fit the pair key's 32-bit halves
         h->err = "ctws_eval_begin: capacity too large";
         return CTWS_EINVAL;
     }
     int r;
-    if ((r = grow(h, h->ev_ka, 8 * (size_t)ca)) != CTWS_OK || (r = grow(h, h->ev_ca, 8 * (size_t)ca)) != CTWS_OK ||
-        (r = grow(h, h->ev_kb, 8 * (size_t)ca)) != CTWS_OK || (r = grow(h, h->ev_cb, 8 * (size_t)ca)) != CTWS_OK ||
+    if ((r = grow(h, h->ev_ka, 8 * (size_t)(ca + 1))) != CTWS_OK || (r = grow(h, h->ev_ca, 8 * (size_t)(ca + 1))) != CTWS_OK ||
+        (r = grow(h, h->ev_kb, 8 * (size_t)(ca + 1))) != CTWS_OK || (r = grow(h, h->ev_cb, 8 * (size_t)(ca + 1))) != CTWS_OK ||
         (r = grow(h, h->ev_kp, 8 * (size_t)cp)) != CTWS_OK || (r = grow(h, h->ev_cp, 8 * (size_t)cp)) != CTWS_OK ||
         (r = grow(h, h->ev_state, 16)) != CTWS_OK || (r = grow(h, h->ev_out, 6 * sizeof(double))) != CTWS_OK)
         return r;
     h->ev_cap_a = h->ev_cap_b = ca;
     h->ev_cap_p = cp;
-    HIPCHK(hipMemsetAsync(h->ev_ka.p, 0xFF, 8 * (size_t)ca, h->stream));
-    HIPCHK(hipMemsetAsync(h->ev_kb.p, 0xFF, 8 * (size_t)ca, h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_ka.p, 0xFF, 8 * (size_t)(ca + 1), h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_kb.p, 0xFF, 8 * (size_t)(ca + 1), h->stream));
     HIPCHK(hipMemsetAsync(h->ev_kp.p, 0xFF, 8 * (size_t)cp, h->stream));
-    HIPCHK(hipMemsetAsync(h->ev_ca.p, 0, 8 * (size_t)ca, h->stream));
-    HIPCHK(hipMemsetAsync(h->ev_cb.p, 0, 8 * (size_t)ca, h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_ca.p, 0, 8 * (size_t)(ca + 1), h->stream));
+    HIPCHK(hipMemsetAsync(h->ev_cb.p, 0, 8 * (size_t)(ca + 1), h->stream));
     HIPCHK(hipMemsetAsync(h->ev_cp.p, 0, 8 * (size_t)cp, h->stream));
     HIPCHK(hipMemsetAsync(h->ev_state.p, 0, 16, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -2142,7 +2272,79 @@ int ctws_debug_read(ctws_handle* h, const char* array, int block, void* dst, int
     return CTWS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// np.unique(labels[, return_counts]) by radix sort + run-length encoding (k_relabel.hip): any
+// value range.  dl: device labels; out / counts: caller buffers (device or host), cap entries.
+int unique_sorted(ctws_handle* h, const uint64_t* dl, int64_t n, int on_device, uint64_t* out, uint64_t* counts,
+                  int64_t cap, int64_t* n_unique) {
+    if (n >= (1ll << 31)) {
+        h->err = "unique: more than 2^31 - 1 labels in one call";
+        return CTWS_EUNSUPPORTED;
+    }
+    int r;
+    size_t tb_sort = 0, tb_rle = 0;
+    HIPCHK(u64_sort(nullptr, tb_sort, dl, nullptr, n, h->stream));
+    HIPCHK(u64_runs(nullptr, tb_rle, nullptr, nullptr, nullptr, nullptr, n, h->stream));
+    if ((r = grow(h, h->rl_sorted, sizeof(uint64_t) * (size_t)n)) != CTWS_OK) return r;
+    if ((r = grow(h, h->rl_uniq, sizeof(uint64_t) * (size_t)n)) != CTWS_OK) return r;
+    if ((r = grow(h, h->rl_counts, sizeof(uint64_t) * (size_t)n + 64)) != CTWS_OK) return r;
+    if ((r = grow(h, h->rl_tmp, std::max(tb_sort, tb_rle))) != CTWS_OK) return r;
+    uint64_t* sorted = (uint64_t*)h->rl_sorted.p;
+    uint64_t* uniq = (uint64_t*)h->rl_uniq.p;
+    uint64_t* cnt = (uint64_t*)h->rl_counts.p;
+    uint64_t* nruns = cnt + n;  // (the counts buffer has 64 spare bytes)
+    HIPCHK(u64_sort(h->rl_tmp.p, tb_sort, dl, sorted, n, h->stream));
+    HIPCHK(u64_runs(h->rl_tmp.p, tb_rle, sorted, uniq, cnt, nruns, n, h->stream));
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, nruns, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    *n_unique = (int64_t)total;
+    if ((int64_t)total > cap) {
+        h->err = "unique: output capacity too small";
+        return CTWS_EINVAL;
+    }
+    const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (total) {
+        HIPCHK(hipMemcpyAsync(out, uniq, sizeof(uint64_t) * total, k, h->stream));
+        if (counts) HIPCHK(hipMemcpyAsync(counts, cnt, sizeof(uint64_t) * total, k, h->stream));
+    }
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return CTWS_OK;
+}
+
+const uint64_t* stage_labels(ctws_handle* h, const uint64_t* labels, int64_t n, int on_device, int* r) {
+    *r = CTWS_OK;
+    if (on_device) return labels;
+    if ((*r = grow(h, h->rl_lab, sizeof(uint64_t) * (size_t)n)) != CTWS_OK) return nullptr;
+    if (hipMemcpyAsync(h->rl_lab.p, labels, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice, h->stream) !=
+        hipSuccess) {
+        h->err = "unique: label upload failed";
+        *r = CTWS_EHIP;
+        return nullptr;
+    }
+    return (const uint64_t*)h->rl_lab.p;
+}
+}  // namespace
+
+extern "C" {
+
 // ---- RelabelWorkflow kernels (k_relabel.hip) ----------------------------------------------
+int ctws_unique_counts_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_device, uint64_t* out,
+                           uint64_t* counts, int64_t cap, int64_t* n_unique) {
+    if (!h || (!labels && n > 0) || n < 0 || !n_unique || cap < 0 || ((!out || !counts) && cap > 0))
+        return CTWS_EINVAL;
+    h->err.clear();
+    HIPCHK(hipSetDevice(h->device));
+    *n_unique = 0;
+    if (n == 0) return CTWS_OK;
+    int r;
+    const uint64_t* dl = stage_labels(h, labels, n, on_device, &r);
+    if (r != CTWS_OK) return r;
+    return unique_sorted(h, dl, n, on_device, out, counts, cap, n_unique);
+}
+
 int ctws_unique_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_device, uint64_t* out, int64_t cap,
                     int64_t* n_unique) {
     if (!h || (!labels && n > 0) || n < 0 || !n_unique || cap < 0 || (!out && cap > 0)) return CTWS_EINVAL;
@@ -2151,12 +2353,8 @@ int ctws_unique_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_de
     *n_unique = 0;
     if (n == 0) return CTWS_OK;
     int r;
-    const uint64_t* dl = labels;
-    if (!on_device) {
-        if ((r = grow(h, h->rl_lab, sizeof(uint64_t) * (size_t)n)) != CTWS_OK) return r;
-        HIPCHK(hipMemcpyAsync(h->rl_lab.p, labels, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice, h->stream));
-        dl = (const uint64_t*)h->rl_lab.p;
-    }
+    const uint64_t* dl = stage_labels(h, labels, n, on_device, &r);
+    if (r != CTWS_OK) return r;
     if ((r = grow(h, h->rl_red, 4 * sizeof(uint64_t))) != CTWS_OK) return r;
     unsigned long long* red = (unsigned long long*)h->rl_red.p;
     const unsigned long long init[3] = {~0ull, 0ull, 0ull};
@@ -2171,12 +2369,12 @@ int ctws_unique_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_de
     const int64_t first = hr[2] ? 1 : 0;
     int64_t total = first;
     if (has_nz) {
-        const uint64_t lo = hr[0], span = hr[1] - hr[0] + 1;
-        if (span > (1ull << 35)) {
-            h->err = "ctws_unique_u64: nonzero labels span more than 2^35 values";
-            return CTWS_EUNSUPPORTED;
-        }
-        const int64_t nw = (int64_t)((span + 63) / 64), nc = (nw + 255) / 256;
+        const uint64_t lo = hr[0], span = hr[1] - hr[0];  // (+ 1 below; 0 .. 2^64 - 1 would wrap)
+        // the bitmap (span / 8 bytes) only while it is no larger than sorting the labels would
+        // need (~16 bytes each) or small anyway; otherwise sort (any value range)
+        if (span >= (1ull << 35) || span / 64 + 1 > (uint64_t)std::max<int64_t>(2 * n, 1 << 20))
+            return unique_sorted(h, dl, n, on_device, out, nullptr, cap, n_unique);
+        const int64_t nw = (int64_t)(span / 64 + 1), nc = (nw + 255) / 256;
         if ((r = grow(h, h->rl_bits, sizeof(uint64_t) * (size_t)nw)) != CTWS_OK) return r;
         if ((r = grow(h, h->rl_cnt, sizeof(uint32_t) * (size_t)nc)) != CTWS_OK) return r;
         if ((r = grow(h, h->rl_offs, sizeof(uint64_t) * (size_t)(nc + 1))) != CTWS_OK) return r;

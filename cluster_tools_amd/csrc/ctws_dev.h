@@ -34,6 +34,7 @@ struct BlockDesc {
     const uint8_t* mask;    // outer mask or nullptr
     const uint64_t* init;   // pass-2 initial seeds or nullptr
     uint64_t* out;          // inner uint64 output
+    uint32_t* out32;        // host path: inner uint32 codes instead (the host widens them, see k_output)
     int n_channels, c0, C, dtype;
     uint64_t id_offset;     // block_id * prod(block_shape)
     int tz, ty, tx, tbase;  // flood tile grid, offset into per-tile arrays
@@ -42,7 +43,7 @@ struct BlockDesc {
     int64_t hbase;          // pass 2: offset into the relabel hash arrays
     int64_t hcap;           // pass 2: hash capacity of this block (power of two)
     int64_t fbase;          // offset into the frontier bitmaps (Z*Y rows of ceil(X/64) words)
-    int64_t _r0;
+    int64_t p2hint;         // pass 2 (2-D): offset of the block's per-slice offset hint (-1: none)
 };
 
 struct BlockStat {

@@ -187,7 +187,8 @@ __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t
 
 // k_pass2.hip (two-pass watershed, pass 2)
 __global__ void k_p2_zero_dt(const BlockDesc*, const BlockStat*, float*);
-__global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint64_t*);
+__global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, const uint32_t*,
+                            uint64_t*);
 __global__ void k_p2_insert(const BlockDesc*, BlockStat*, const uint64_t*, uint64_t*, uint32_t*);
 __global__ void k_p2_roots(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint64_t*);
 __global__ void k_p2_label(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, const uint64_t*,
@@ -207,5 +208,8 @@ __global__ void k_bits_chunk_count(const uint64_t*, int64_t, uint32_t*);
 __global__ void k_scan_chunks(const uint32_t*, int64_t, uint64_t*);
 __global__ void k_bits_compact(const uint64_t*, int64_t, const uint64_t*, uint64_t, uint64_t, uint64_t*);
 __global__ void k_u64_lookup(uint64_t*, int64_t, const uint64_t*, const uint64_t*, int64_t, unsigned long long*);
+hipError_t u64_sort(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out, int64_t n, hipStream_t stream);
+hipError_t u64_runs(void* tmp, size_t& bytes, const uint64_t* sorted, uint64_t* uniq, uint64_t* counts,
+                    uint64_t* n_runs, int64_t n, hipStream_t stream);
 
 }  // namespace ctws

@@ -388,7 +388,12 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
             if (valid) mx = max(mx, l);
             v = l;
         }
-        if (valid) out[i] = inm ? v + B.id_offset : v;
+        // out32 (host path): the uint32 local label; the host adds the block's id offset to every
+        // in-mask voxel, so half the bytes cross PCIe (the offset is a per-block constant)
+        if (valid) {
+            if (B.out32) gblw(B.out32)[i] = (uint32_t)v;
+            else out[i] = inm ? v + B.id_offset : v;
+        }
         zero_in |= valid && active && inm && v == 0;
         if (active && !B.crop) {
             const uint32_t l = valid ? (uint32_t)v : 0u;

@@ -29,8 +29,10 @@ __device__ __forceinline__ uint64_t ev_mix(uint64_t x) {
     return x;
 }
 
-// slot of k (inserted if absent); -1 when the table is full
+// slot of k (inserted if absent); -1 when the table is full.  The label 2^64 - 1 (= the empty
+// marker) has the extra slot `cap` of its own (arrays hold cap + 1 entries): present iff counted.
 __device__ __forceinline__ int64_t ev_insert(uint64_t* keys, int64_t cap, uint64_t k) {
+    if (k == kEvEmpty) return cap;
     int64_t s = (int64_t)(ev_mix(k) & (uint64_t)(cap - 1));
     for (int64_t p = 0; p < cap; ++p) {
         uint64_t v = keys[s];
@@ -102,14 +104,14 @@ __global__ void __launch_bounds__(256) k_eval_reduce(const uint64_t* __restrict_
     const double n = (double)state[0];
     double v[6] = {0, 0, 0, 0, 0, 0};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap_a; s += stride)
-        if (ka[s] != kEvEmpty) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= cap_a; s += stride)
+        if (s < cap_a ? ka[s] != kEvEmpty : ca[s] != 0ull) {
             const double c = (double)ca[s];
             v[0] += -c / n * log2(c / n);
             v[3] += c * c;
         }
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap_b; s += stride)
-        if (kb[s] != kEvEmpty) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= cap_b; s += stride)
+        if (s < cap_b ? kb[s] != kEvEmpty : cb[s] != 0ull) {
             const double c = (double)cb[s];
             v[1] += -c / n * log2(c / n);
             v[4] += c * c;

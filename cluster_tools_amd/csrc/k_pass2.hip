@@ -15,9 +15,13 @@
 // In 2-D mode `offset` grows slice by slice by the max_id of the previous slices (:166-168),
 // which is only known after their floods.  relabelConsecutive numbers by first appearance,
 // so the offset changes the numbering only where a shifted new seed value equals an initial
-// value of the same slice.  The relabel therefore keys new seeds by (slice, tag 0, local
-// seed id) and initial seeds by (slice, tag 1, value); once the slice offsets are known,
-// k_p2_check verifies that no such equality exists (it raises CTWS_EUNSUPPORTED if one does).
+// value of the same slice (then both are one id: the new seed merges into the initial seed's
+// segment).  The first run keys new seeds by (slice, tag 0, local seed id) and initial seeds
+// by (slice, tag 1, value); once the slice offsets are known, k_p2_check flags a block where
+// such an equality exists.  The host then runs the block again with the offsets as a hint:
+// every seed is keyed by (slice, tag 1, its uint32 value), so equal values merge exactly as in
+// relabelConsecutive, and it repeats until the offsets the run produces equal its hint (slice
+// z's offset depends only on slices < z, so each run fixes at least one more slice).
 // In 3-D mode the offset is the constant block_id * prod(block_shape), so keys are the exact
 // uint32 values, as in the reference.
 //
@@ -79,10 +83,11 @@ __global__ void __launch_bounds__(256) k_p2_zero_dt(const BlockDesc* __restrict_
     }
 }
 
-// per-voxel relabel key (kEmptyKey: unlabelled); written into `vkey`
+// per-voxel relabel key (kEmptyKey: unlabelled); written into `vkey`.  `hint` (2-D, blocks with
+// B.p2hint >= 0): the slice offsets of the previous run, new seeds keyed by their uint32 value
 __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                    const uint32_t* __restrict__ PFg, const uint32_t* __restrict__ sb,
-                                                   uint64_t* __restrict__ vkey) {
+                                                   const uint32_t* __restrict__ hint, uint64_t* __restrict__ vkey) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -102,6 +107,10 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
                 if (B.nd_ws == 3) {
                     const uint32_t v = gl + (uint32_t)B.id_offset;  // wraps to 0: background
                     if (v) k = v;
+                } else if (B.p2hint >= 0) {
+                    // seeds[seeds != 0] += offset in uint32: a value that wraps to 0 is background
+                    const uint32_t v = (gl - sb[B.sbase + z]) + (uint32_t)B.id_offset + hint[B.p2hint + z];
+                    if (v) k = ((uint64_t)z << 33) | kInitTag | v;
                 } else k = ((uint64_t)z << 33) | (uint64_t)(gl - sb[B.sbase + z]);
             }
         }
@@ -227,13 +236,13 @@ __global__ void __launch_bounds__(256) k_p2_excl_zero(const BlockDesc* __restric
         excl[B.base + i] = 0;
 }
 
-// 2-D: with the slice offsets known, no shifted new seed may equal an initial value of its
-// slice (else relabelConsecutive would have merged them: unsupported, err bit 1)
+// 2-D: with the slice offsets known, flag a shifted new seed equal to an initial value of its
+// slice (relabelConsecutive merges them: the host re-runs the block with value keys)
 __global__ void __launch_bounds__(256) k_p2_check(const BlockDesc* __restrict__ D, BlockStat* S,
                                                   const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ soff) {
     uint32_t* err = &S[blockIdx.y].err;
     const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || B.nd_ws != 2) return;
+    if (!S[blockIdx.y].active || B.nd_ws != 2 || B.p2hint >= 0) return;  // hint runs merge equal values
     const int64_t YX = (int64_t)B.Y * B.X;
     BLOCK_LOOP(i, B) {
         const uint64_t u = gbl(B.init)[i];
@@ -271,7 +280,8 @@ __global__ void __launch_bounds__(256) k_p2_output(const BlockDesc* __restrict__
             if (B.nd_ws == 2 && !oldt[B.base + l]) v = v + (uint32_t)B.id_offset + soff[B.sbase + z + B.iz0];
         }
         mx = max(mx, v);
-        gblw(B.out)[i] = v;
+        if (B.out32) gblw(B.out32)[i] = v;  // pass-2 values are uint32 (Appendix B.2)
+        else gblw(B.out)[i] = v;
     }
     mx = wg_reduce_u32(mx, OpMax());
     if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);

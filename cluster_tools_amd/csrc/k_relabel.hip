@@ -12,9 +12,16 @@
 // a compaction pass writes the set bits in ascending order: the uniques come out sorted with
 // no sort at all.  0 is tracked with a flag and emitted first.
 //
+// When the values span too wide a range for a bitmap (sparse or arbitrary ids: more than 2^35
+// values, or a bitmap larger than the labels themselves), or when the counts are wanted
+// (np.unique(return_counts=True), find_uniques.py:104-106), the uniques come from a radix sort
+// of the labels and a run-length encoding of the sorted run (hipcub, both device-wide).
+//
 // Lookup: every label is replaced by values[j] for keys[j] == label (keys ascending) by a
 // binary search in the table; labels absent from the table are counted and left unchanged
 // (takeDict would raise; the caller decides).
+#include <hipcub/hipcub.hpp>
+
 #include "ctws_kernels.h"
 
 namespace ctws {
@@ -150,6 +157,16 @@ __global__ void __launch_bounds__(256) k_copy_to_host(const uint4* __restrict__ 
                                                       size_t n16) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
         dst[i] = src[i];
+}
+
+// sort-based unique: radix sort of the uint64 keys, then (value, count) runs.  With tmp ==
+// nullptr the temporary storage is only sized.
+hipError_t u64_sort(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out, int64_t n, hipStream_t stream) {
+    return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, in, out, n, 0, 64, stream);
+}
+hipError_t u64_runs(void* tmp, size_t& bytes, const uint64_t* sorted, uint64_t* uniq, uint64_t* counts,
+                    uint64_t* n_runs, int64_t n, hipStream_t stream) {
+    return hipcub::DeviceRunLengthEncode::Encode(tmp, bytes, sorted, uniq, counts, n_runs, n, stream);
 }
 
 }  // namespace ctws

@@ -200,7 +200,8 @@ __global__ void __launch_bounds__(256) k_fs_output(const BlockDesc* __restrict__
         const uint32_t l = flood_label(lab, key, keys_final, B.base + i);
         uint64_t v = l == 0u ? 0ull : (raw ? (uint64_t)l : (uint64_t)sv[l - 1]);
         if (B.mask && !gbl(B.mask)[i]) v = 0ull;
-        B.out[i] = v;
+        if (B.out32) B.out32[i] = (uint32_t)v;  // seed ids < 2^32 - 1 (the overflow assert)
+        else B.out[i] = v;
         mx = v > mx ? v : mx;
     }
     for (int s = 32; s > 0; s >>= 1) {

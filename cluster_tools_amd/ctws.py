@@ -52,6 +52,8 @@ def lib():
             L.ctws_allgather_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
             L.ctws_unique_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
                                           C.POINTER(C.c_int64)]
+            L.ctws_unique_counts_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p,
+                                                 C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
             L.ctws_lookup_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
                                           C.c_int64, C.POINTER(C.c_int64)]
             L.ctws_set_table_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
@@ -66,7 +68,7 @@ def lib():
 
 EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
                     'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_comm_unique_id', 'ctws_comm_init',
-                    'ctws_allgather_counts', 'ctws_unique_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
+                    'ctws_allgather_counts', 'ctws_unique_u64', 'ctws_unique_counts_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
                     'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
                     'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end')
 
@@ -318,6 +320,23 @@ class Handle:
                 continue
             self._check(ret, 'ctws_unique_u64')
             return out[:n.value]
+
+    def unique_counts_u64(self, labels):
+        """np.unique(labels, return_counts=True) on the GPU (radix sort + run-length encoding):
+        (sorted uniques uint64, counts uint64)."""
+        lab = np.ascontiguousarray(labels, dtype=np.uint64).ravel()
+        n = C.c_int64(0)
+        cap = 1024
+        while True:
+            out = np.empty(cap, dtype=np.uint64)
+            cnt = np.empty(cap, dtype=np.uint64)
+            ret = lib().ctws_unique_counts_u64(self._h, lab.ctypes.data, lab.size, 0, out.ctypes.data,
+                                               cnt.ctypes.data, cap, C.byref(n))
+            if ret == -1 and n.value > cap:
+                cap = n.value
+                continue
+            self._check(ret, 'ctws_unique_counts_u64')
+            return out[:n.value], cnt[:n.value]
 
     def set_table_u64(self, keys, values):
         """Upload an assignment table (keys ascending) and keep it resident on the GPU."""

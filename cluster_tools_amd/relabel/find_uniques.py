@@ -66,9 +66,7 @@ def find_uniques(job_id, config_path):
     fu.log("reading config from %s" % config_path)
     with open(config_path) as f:
         config = json.load(f)
-    if config['return_counts']:
-        raise NotImplementedError("find_uniques with return_counts (post-processing workflows) is outside "
-                                  "the watershed path; only the relabel mode is implemented")
+    return_counts = config['return_counts']
     block_list = config['block_list']
     with vu.file_reader(config['input_path'], 'r') as f, ctws.Handle(_device()) as h, \
             futures.ThreadPoolExecutor(1) as io:
@@ -78,17 +76,33 @@ def find_uniques(job_id, config_path):
         def read(block_id):
             return ds[vu.block_to_bb(blocking.getBlock(block_id))]
 
-        per_block = []
+        per_block, per_counts = [], []
         nxt = io.submit(read, block_list[0]) if block_list else None
         for k, block_id in enumerate(block_list):
             fu.log("start processing block %i" % block_id)
             labels = nxt.result()
             nxt = io.submit(read, block_list[k + 1]) if k + 1 < len(block_list) else None
-            u = h.unique_u64(labels)
+            if return_counts:
+                u, c = h.unique_counts_u64(labels)
+                per_counts.append(c)
+            else:
+                u = h.unique_u64(labels)
             per_block.append(u)
             if not (len(u) == 1 and u[0] == 0):
                 fu.log_block_success(block_id)
-        unique_values = h.unique_u64(np.concatenate(per_block)) if per_block else np.zeros(0, 'uint64')
+        if return_counts and per_block:
+            # counts of equal values summed over the blocks (find_uniques.py:143-151): a merge of
+            # the per-block (value, count) tables -- uniques, not voxels -- on the host
+            allv = np.concatenate(per_block)
+            allc = np.concatenate(per_counts)
+            order = np.argsort(allv, kind='stable')
+            allv, allc = allv[order], allc[order]
+            unique_values, starts = np.unique(allv, return_index=True)
+            counts = np.add.reduceat(allc, starts).astype('uint64')
+            count_path = os.path.join(config['tmp_folder'], 'counts_job_%i.npy' % job_id)
+            np.save(count_path, counts)
+        else:
+            unique_values = h.unique_u64(np.concatenate(per_block)) if per_block else np.zeros(0, 'uint64')
     save_path = os.path.join(config['tmp_folder'], 'find_uniques_job_%i.npy' % job_id)
     fu.log("saving results to %s" % save_path)
     np.save(save_path, unique_values)

@@ -209,8 +209,10 @@ int ctws_allgather_counts(ctws_handle* h, const int64_t* local_counts, int64_t n
  *
  * ctws_unique_u64: the sorted unique values of labels[0..n) (np.unique) into out[0..cap);
  *   *n_unique = their number (also when cap is too small: then CTWS_EINVAL, retry with a
- *   larger buffer).  The nonzero values must span < 2^35 (always true for watershed ids of
- *   volumes below 2^35 voxels), else CTWS_EUNSUPPORTED.
+ *   larger buffer).  Any value range: a bitmap over the range when it is dense enough
+ *   (watershed ids), else a radix sort.  Fewer than 2^31 labels per call.
+ * ctws_unique_counts_u64: np.unique(labels, return_counts=True) (find_uniques.py:104-106):
+ *   sorted uniques into out, their voxel counts into counts (both cap entries).
  * ctws_set_table_u64: upload an assignment table (host keys ascending, values) and keep it
  *   resident on the handle (one upload per Write job instead of one per block).
  * ctws_lookup_u64: labels[i] <- values[j] where keys[j] == labels[i] (keys ascending;
@@ -221,6 +223,8 @@ int ctws_allgather_counts(ctws_handle* h, const int64_t* local_counts, int64_t n
 int ctws_set_table_u64(ctws_handle* h, const uint64_t* keys, const uint64_t* values, int64_t n_table);
 int ctws_unique_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_device, uint64_t* out, int64_t cap,
                     int64_t* n_unique);
+int ctws_unique_counts_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_device, uint64_t* out,
+                           uint64_t* counts, int64_t cap, int64_t* n_unique);
 int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, const uint64_t* keys,
                     const uint64_t* values, int64_t n_table, int64_t* n_missing);
 

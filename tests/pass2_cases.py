@@ -16,7 +16,12 @@ GRID_BLOCK = (24, 64, 64)
 
 D3 = dict(apply_dt_2d=False, apply_ws_2d=False)
 
-# name -> (task config, halo, block-id base, masked)
+# name -> (task config, halo, block-id base, masked[, block-id stride])
+# '2d_collide': block ids 2^17 apart, so every block_id * prod(block_shape) (V = 3 * 2^15) is
+# 0 mod 2^32 -- the modular coincidence of a z-halo grid with V = 2^22 and gy * gx = 1024: the
+# pass-2 block's new seeds (uint32 offset + local id) take the same uint32 values as the
+# neighbours' pass-1 ids in its halo, and relabelConsecutive merges them
+# (two_pass_watershed.py:147-155)
 SCENARIOS = {
     '3d': (dict(D3), (0, 16, 16), 0, False),
     '2d': ({}, (0, 16, 16), 0, False),
@@ -27,6 +32,8 @@ SCENARIOS = {
     '3d_nofilter': (dict(D3, size_filter=0), (0, 16, 16), 0, False),
     '3d_bigfilter': (dict(D3, size_filter=400), (0, 16, 16), 0, False),
     '2d_dt3d': (dict(apply_dt_2d=False), (0, 16, 16), 0, False),
+    '2d_collide': ({}, (0, 16, 16), 0, False, 1 << 17),
+    '2d_collide_mask': ({}, (0, 16, 16), 0, True, 1 << 17),
 }
 
 
@@ -48,7 +55,8 @@ def _blocks(block_shape, halo):
 
 def scenario(name, seed=3):
     """-> (config, block_shape, list of pass-2 block dicts with initial_seeds)."""
-    config, halo, id_base, masked = SCENARIOS[name]
+    config, halo, id_base, masked = SCENARIOS[name][:4]
+    stride = SCENARIOS[name][4] if len(SCENARIOS[name]) > 4 else 1
     config = dict(config, halo=list(halo))
     x = boundary_map(VOL, seed=seed)
     mask = ellipsoid_mask(VOL) if masked else None
@@ -58,7 +66,7 @@ def scenario(name, seed=3):
     blocks = _blocks(block_shape, halo)
 
     def as_block(b):
-        d = dict(input=x[b['outer']], block_id=id_base + b['local_id'], inner_begin=b['inner_begin'],
+        d = dict(input=x[b['outer']], block_id=id_base + b['local_id'] * stride, inner_begin=b['inner_begin'],
                  inner_shape=GRID_BLOCK, crop_relabel=sum(halo) > 0)
         if mask is not None:
             d['mask'] = mask[b['outer']]

@@ -47,7 +47,14 @@ def _cases():
     noisy[flip] = rng.integers(1, 50, size=int(flip.sum())).astype(np.uint64)
     gt0 = gt.copy()
     gt0[:, :10] = 0
-    return {'identical': (gt.copy(), gt, False), 'split': (split, gt, False), 'merge': (merge, gt, False),
+    # -1 in an int64 volume cast to uint64: the hash tables' empty marker as a real label
+    maxlab = noisy.copy()
+    maxlab[:, 30:40] = np.uint64(2 ** 64 - 1)
+    gtmax = gt.copy()
+    gtmax[5:8] = np.uint64(2 ** 64 - 1)
+    return {'max_uint64_seg': (maxlab, gt, False), 'max_uint64_gt': (noisy, gtmax, False),
+            'max_uint64_both': (maxlab, gtmax, False),
+            'identical': (gt.copy(), gt, False), 'split': (split, gt, False), 'merge': (merge, gt, False),
             'noisy': (noisy, gt, False), 'ignore_gt0': (noisy, gt0, True), 'no_ignore_gt0': (noisy, gt0, False)}
 
 

@@ -119,6 +119,21 @@ def test_watershed_workflow(tmp_path, name, with_mask):
         table = f['relabel_watershed'][:]
     _check_result(res.astype('uint64'), with_mask)
     assert len(np.unique(res)) == len(table)
+    # RelabelWorkflow parity: find_labeling.py:104-116 (sorted uniques -> consecutive ids from
+    # 0 if 0 occurs, else 1) + write.py (takeDict) applied to the raw watershed output
+    np.testing.assert_array_equal(res.astype('uint64'), _reference_relabel(raw))
+    uniq = np.unique(raw)
+    start = 0 if uniq[0] == 0 else 1
+    np.testing.assert_array_equal(table[:, 0], uniq)
+    np.testing.assert_array_equal(table[:, 1], np.arange(start, start + len(uniq), dtype='uint64'))
+
+
+def _reference_relabel(raw):
+    """RelabelWorkflow restated with numpy: FindUniques/FindLabeling (np.unique, arange from 0
+    or 1, find_labeling.py:104-116) then Write (takeDict, write.py:153-175)."""
+    uniq, inv = np.unique(raw, return_inverse=True)
+    start = 0 if uniq[0] == 0 else 1
+    return (inv.reshape(raw.shape) + start).astype('uint64')
 
 
 def _oracle_two_pass(x, c, mask):
