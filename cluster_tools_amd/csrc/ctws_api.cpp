@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <utility>
@@ -33,6 +34,7 @@
 
 #include "../../include/ctws.h"
 #include "ctws_kernels.h"
+#include "host_pool.h"
 
 using namespace ctws;
 
@@ -102,6 +104,7 @@ struct ctws_handle {
         size_t pin_out_bytes = 0;
         DevBuf d_in, d_out;
         hipEvent_t ev_h2d = nullptr, ev_comp = nullptr, ev_d2h = nullptr;
+        hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // CTWS_TRACE: the batch's upload, timed
         std::vector<hipEvent_t> ev_blk;  // per block of the batch: its output downloaded
     } hslot[2];
     hipStream_t s_in = nullptr, s_out = nullptr;
@@ -126,8 +129,16 @@ struct ctws_handle {
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int words_per_wave = 32;    // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels
-    int d2h_wgs = 32;           // CTWS_D2H_WGS: workgroups of the device-to-host copy kernel (0: hipMemcpyAsync)
-    int host_threads = 8;       // CTWS_HOST_THREADS: memcpy threads per direction of the host path
+    // CTWS_D2H_WGS: workgroups of a device-to-host copy kernel; 0 (default): hipMemcpyAsync on the
+    // SDMA engines.  r03 (uint32 downloads, config 3): the copy kernel's workgroups slowed the
+    // concurrent compute from 94 to 140 ms per step (host-resident 7.69 vs 6.08 Gvoxel/s)
+    int d2h_wgs = 0;
+    int pack_threads = 6;       // CTWS_PACK_THREADS: threads packing inputs into pinned staging
+    int unpack_threads = 9;     // CTWS_UNPACK_THREADS: threads widening downloads into the outputs
+    std::unique_ptr<ctws_host::WorkerPool> pack_pool, unpack_pool;
+    int h2d_mode = 0;           // CTWS_H2D_MODE: 0 a copy per block as packed, 1 one copy per batch, 2 pull kernel
+    int h2d_wgs = 64;           // CTWS_H2D_WGS: workgroups of the pull kernel (mode 2)
+    int host_ramp = 1;          // CTWS_HOST_RAMP=0: equal batches (no smaller first / last batches)
     int host_batch_blocks = 0;  // CTWS_HOST_BATCH_BLOCKS: cap on blocks per host-path batch (0: voxel cap)
     int64_t host_batch_voxels = (int64_t)256 << 20;  // CTWS_HOST_BATCH_VOXELS: smaller batches pipeline better
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
@@ -1591,34 +1602,22 @@ int64_t batch_voxels_budget() {
 // buffer and starts its host-to-device copy on s_in while the calling thread runs batch j on
 // the library stream; batch j's outputs go device-to-host on s_out and another worker unpacks
 // them into the callers' arrays while batch j + 1 computes.  Events order every reuse of a slot.
-// (few threads: the calling thread's host round trips inside run_batch must not wait for a core)
-void par_memcpy(const std::vector<std::pair<void*, const void*>>& dst_src, const std::vector<size_t>& sizes,
-                unsigned max_threads) {
-    size_t total = 0;
-    for (size_t v : sizes) total += v;
-    const unsigned nt = std::max(1u, std::min(max_threads, std::thread::hardware_concurrency()));
-    if (total < (64u << 20) || nt == 1) {
-        for (size_t i = 0; i < sizes.size(); ++i) std::memcpy(dst_src[i].first, dst_src[i].second, sizes[i]);
-        return;
-    }
-    // split the byte range of the concatenated copies evenly over the threads
-    std::vector<std::thread> th;
-    const size_t per = (total + nt - 1) / nt;
-    for (unsigned t = 0; t < nt; ++t) {
-        const size_t b0 = t * per, b1 = std::min(total, b0 + per);
-        if (b0 >= b1) break;
-        th.emplace_back([&, b0, b1]() {
-            size_t off = 0;
-            for (size_t i = 0; i < sizes.size(); ++i) {
-                const size_t s0 = std::max(off, b0), s1 = std::min(off + sizes[i], b1);
-                if (s0 < s1)
-                    std::memcpy((char*)dst_src[i].first + (s0 - off), (const char*)dst_src[i].second + (s0 - off), s1 - s0);
-                off += sizes[i];
-                if (off >= b1) break;
-            }
-        });
-    }
-    for (auto& t : th) t.join();
+// Host copies run on two persistent worker pools of the handle (ctws_host::WorkerPool): one for
+// packing, one for widening.  Their sizes (CTWS_PACK_THREADS, CTWS_UNPACK_THREADS) leave a core
+// to the calling thread, whose host round trips inside run_batch must not wait for one.
+constexpr size_t kCopyChunk = (size_t)4 << 20;  // bytes per pool task
+
+// the copies (dst, src, bytes) in 4 MiB tasks over the pool, streaming stores
+void pool_copy(ctws_host::WorkerPool& pool, const std::vector<std::pair<void*, const void*>>& dst_src,
+               const std::vector<size_t>& sizes) {
+    std::vector<std::pair<size_t, size_t>> tasks;  // (copy index, byte offset)
+    for (size_t i = 0; i < sizes.size(); ++i)
+        for (size_t o = 0; o < sizes[i]; o += kCopyChunk) tasks.push_back({i, o});
+    pool.parallel_for((int64_t)tasks.size(), [&](int64_t t) {
+        const size_t i = tasks[t].first, o = tasks[t].second;
+        ctws_host::stream_copy((char*)dst_src[i].first + o, (const char*)dst_src[i].second + o,
+                               std::min(kCopyChunk, sizes[i] - o));
+    });
 }
 
 // host <-> device copy in pieces of at most 1 GiB: larger copies are not given to the SDMA
@@ -1647,41 +1646,32 @@ int grow_pinned(ctws_handle* h, void*& p, size_t& have, size_t bytes) {
 
 // uint32 codes of a block's inner region (k_output: the local label) -> the caller's uint64
 // output: code + off, except for masked voxels (0).  A zero code is a masked voxel, or -- when
-// the block has `bare` voxels (in-mask without a label) or off == 0 -- looked up in the caller's
-// mask.  Rows are split over the threads.
-void widen_codes(const ctws_block& b, const uint32_t* codes, uint64_t off, bool bare, unsigned max_threads) {
-    const int64_t IZ = b.inner_shape[0], IY = b.inner_shape[1], IX = b.inner_shape[2];
-    const int64_t rows = IZ * IY;
+// the block has `bare` voxels (in-mask without a label) -- looked up in the caller's mask.
+// Row ranges are the pool's tasks; stores stream past the caches.
+void widen_codes(ctws_host::WorkerPool& pool, const ctws_block& b, const uint32_t* codes, uint64_t off, bool bare) {
+    const int64_t IY = b.inner_shape[1], IX = b.inner_shape[2];
+    const int64_t rows = b.inner_shape[0] * IY;
     const uint8_t* mask = (b.mask && off != 0 && bare) ? b.mask : nullptr;
-    const bool masked = b.mask != nullptr;
-    auto work = [&](int64_t r0, int64_t r1) {
-        for (int64_t r = r0; r < r1; ++r) {
-            const uint32_t* c = codes + r * IX;
-            uint64_t* o = b.output + r * IX;
-            if (!masked || off == 0) {
-                for (int64_t x = 0; x < IX; ++x) o[x] = (uint64_t)c[x] + off;
-            } else if (!mask) {
-                for (int64_t x = 0; x < IX; ++x) o[x] = c[x] ? (uint64_t)c[x] + off : 0ull;
-            } else {
+    const bool masked = b.mask != nullptr && off != 0;
+    const int64_t per = std::max<int64_t>(1, (int64_t)(kCopyChunk / 12) / std::max<int64_t>(IX, 1));  // rows per task
+    pool.parallel_for((rows + per - 1) / per, [&](int64_t t) {
+        const int64_t r0 = t * per, r1 = std::min(rows, r0 + per);
+        if (!masked) {
+            ctws_host::widen_add(b.output + r0 * IX, codes + r0 * IX, (r1 - r0) * IX, off);
+        } else if (!mask) {
+            ctws_host::widen_add_nz(b.output + r0 * IX, codes + r0 * IX, (r1 - r0) * IX, off);
+        } else {
+            for (int64_t r = r0; r < r1; ++r) {
+                const uint32_t* c = codes + r * IX;
+                uint64_t* o = b.output + r * IX;
                 const int64_t z = r / IY, y = r - z * IY;
                 const uint8_t* m = mask + ((z + b.inner_begin[0]) * b.outer_shape[1] + (y + b.inner_begin[1])) *
                                               b.outer_shape[2] + b.inner_begin[2];
                 for (int64_t x = 0; x < IX; ++x) o[x] = (c[x] || m[x]) ? (uint64_t)c[x] + off : 0ull;
             }
         }
-    };
-    const int64_t bytes = rows * IX * 12;
-    const unsigned nt = std::max(1u, std::min(max_threads, std::thread::hardware_concurrency()));
-    if (nt == 1 || bytes < (16ll << 20)) {
-        work(0, rows);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t) {
-        const int64_t r0 = rows * t / nt, r1 = rows * (t + 1) / nt;
-        if (r0 < r1) th.emplace_back(work, r0, r1);
-    }
-    for (auto& t : th) t.join();
+        _mm_sfence();
+    });
 }
 
 struct HostBatch {
@@ -1698,18 +1688,29 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
     // batches and their packed layouts (inputs, masks and initial seeds in one buffer)
     std::vector<HostBatch> hb;
     size_t max_in = 0, max_out = 0;
+    int64_t rem_vox = 0;
+    for (int i : todo) rem_vox += blocks[i].outer_shape[0] * blocks[i].outer_shape[1] * blocks[i].outer_shape[2];
     for (size_t k = 0; k < todo.size();) {
         size_t e = k;
         int64_t vox = 0;
+        // ramped batches: the first upload and the last download + widening are not overlapped
+        // with compute, so the first two and the last batches are smaller (1/4, 1/2 of the budget)
+        int64_t bud = budget;
+        if (h->host_ramp) {
+            if (hb.size() == 0) bud = budget / 4;
+            else if (hb.size() == 1) bud = budget / 2;
+            if (rem_vox < 2 * budget) bud = std::min(bud, std::max(budget / 4, rem_vox / 2));
+        }
         while (e < todo.size()) {
             const ctws_block& b = blocks[todo[e]];
             const int64_t nv = b.outer_shape[0] * b.outer_shape[1] * b.outer_shape[2];
-            if (e > k && (vox + nv > budget || e - k >= 4096 || (h->host_batch_blocks > 0 &&
-                                                                  (int)(e - k) >= h->host_batch_blocks)))
+            if (e > k && (vox + nv > bud || e - k >= 4096 || (h->host_batch_blocks > 0 &&
+                                                               (int)(e - k) >= h->host_batch_blocks)))
                 break;
             vox += nv;
             ++e;
         }
+        rem_vox -= vox;
         HostBatch B;
         B.k = (int)k;
         B.nb = (int)(e - k);
@@ -1735,6 +1736,8 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
         k = e;
     }
     if (hb.empty()) return CTWS_OK;
+    if (!h->pack_pool) h->pack_pool.reset(new ctws_host::WorkerPool(h->pack_threads));
+    if (!h->unpack_pool) h->unpack_pool.reset(new ctws_host::WorkerPool(h->unpack_threads));
     if (!h->s_in) {
         HIPCHK(hipStreamCreateWithFlags(&h->s_in, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&h->s_out, hipStreamNonBlocking));
@@ -1742,6 +1745,8 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             HIPCHK(hipEventCreateWithFlags(&sl.ev_h2d, hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&sl.ev_comp, hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&sl.ev_d2h, hipEventDisableTiming));
+            HIPCHK(hipEventCreate(&sl.ev_t0));
+            HIPCHK(hipEventCreate(&sl.ev_t1));
         }
     }
     const int nslots = hb.size() > 1 ? 2 : 1;
@@ -1758,6 +1763,8 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
     // wall times (summed over batches) of the packing, widening and compute phases; the first
     // two run on worker threads, so they are only added to the timings at the end
     double pack_ms = 0.0, unpack_ms = 0.0, compute_ms = 0.0;
+    const auto tcall = std::chrono::steady_clock::now();
+    auto since = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - tcall).count() * 1e3; };
     // pack batch j's inputs into its slot and start the upload (worker thread)
     // pack batch j's inputs block by block into its slot, each block's upload starting as soon
     // as it is packed (worker thread)
@@ -1781,15 +1788,29 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
                 ds.push_back({(char*)sl.pin_in + B.i_off[i], b.initial_seeds});
                 sz.push_back((size_t)nv * 8);
             }
-            par_memcpy(ds, sz, (unsigned)h->host_threads);
+            pool_copy(*h->pack_pool, ds, sz);
+            if (h->h2d_mode == 1 && i + 1 < B.nb) continue;  // one copy for the whole batch
+            const size_t beg = h->h2d_mode == 1 ? 0 : B.in_off[i];
             const size_t end = i + 1 < B.nb ? B.in_off[i + 1] : B.in_bytes;
-            if (copy_pieces((char*)sl.d_in.p + B.in_off[i], (char*)sl.pin_in + B.in_off[i], end - B.in_off[i],
-                            hipMemcpyHostToDevice, h->s_in) != hipSuccess)
+            if (i == 0 || h->h2d_mode == 1) {
+                if (h->trace) hipEventRecord(sl.ev_t0, h->s_in);
+            }
+            if (h->h2d_mode == 2) {
+                // pull kernel: a few workgroups read the pinned buffer over PCIe
+                void* hsrc = nullptr;
+                if (hipHostGetDevicePointer(&hsrc, sl.pin_in, 0) != hipSuccess) return CTWS_EHIP;
+                k_copy_to_host<<<h->h2d_wgs, 256, 0, h->s_in>>>((const uint4*)((char*)hsrc + beg),
+                                                                 (uint4*)((char*)sl.d_in.p + beg), (end - beg + 15) / 16);
+                if (hipGetLastError() != hipSuccess) return CTWS_EHIP;
+            } else if (copy_pieces((char*)sl.d_in.p + beg, (char*)sl.pin_in + beg, end - beg, hipMemcpyHostToDevice,
+                                   h->s_in) != hipSuccess) {
                 return CTWS_EHIP;
+            }
         }
+        if (h->trace) hipEventRecord(sl.ev_t1, h->s_in);
         const double ms = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3;
         pack_ms += ms;
-        if (h->trace) std::fprintf(stderr, "[ctws] host batch %d: pack %.1f ms (%zu B)\n", j, ms, B.in_bytes);
+        if (h->trace) std::fprintf(stderr, "[ctws] t=%.1f host batch %d: packed+queued in %.1f ms (%zu B)\n", since(), j, ms, B.in_bytes);
         return hipEventRecord(sl.ev_h2d, h->s_in) == hipSuccess ? CTWS_OK : CTWS_EHIP;
     };
     // widen batch j's uint32 codes into the callers' uint64 outputs block by block as their
@@ -1809,12 +1830,11 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             // pass 1: in-mask voxels get + block_id * prod(block_shape); pass 2 / from-seeds
             // outputs are the uint32 values themselves
             const uint64_t off = (pl.pass2 || pl.from_seeds) ? 0ull : (uint64_t)b.block_id * bvol;
-            widen_codes(b, (const uint32_t*)((char*)sl.pin_out + B.o_off[i]), off, bare_of[j][i] != 0,
-                        (unsigned)h->host_threads);
+            widen_codes(*h->unpack_pool, b, (const uint32_t*)((char*)sl.pin_out + B.o_off[i]), off, bare_of[j][i] != 0);
         }
         const double ms = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3;
         unpack_ms += ms;
-        if (h->trace) std::fprintf(stderr, "[ctws] host batch %d: unpack %.1f ms (%zu B)\n", j, ms, B.out_bytes);
+        if (h->trace) std::fprintf(stderr, "[ctws] t=%.1f host batch %d: widened in %.1f ms (%zu B)\n", since(), j, ms, B.out_bytes);
         return CTWS_OK;
     };
     for (auto& sl : h->hslot) HIPCHK(hipEventRecord(sl.ev_h2d, h->s_in));
@@ -1848,6 +1868,12 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             join_all();
             return CTWS_EHIP;
         }
+        if (h->trace) {
+            float up = 0.f;
+            hipEventElapsedTime(&up, sl.ev_t0, sl.ev_t1);
+            std::fprintf(stderr, "[ctws] t=%.1f host batch %zu: inputs on the device (first copy -> last: %.1f ms)\n",
+                         since(), j, up);
+        }
         const auto tb = std::chrono::steady_clock::now();
         if ((r = run_batch(h, cfg, pl, bb.data(), io.data(), B.nb)) != CTWS_OK) {
             join_all();
@@ -1856,7 +1882,7 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
         {
             const double ms = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count() * 1e3;
             compute_ms += ms;
-            if (h->trace) std::fprintf(stderr, "[ctws] host batch %zu: compute %.1f ms\n", j, ms);
+            if (h->trace) std::fprintf(stderr, "[ctws] t=%.1f host batch %zu (%d blocks): computed in %.1f ms\n", since(), j, B.nb, ms);
         }
         HIPCHK(hipEventRecord(sl.ev_comp, h->stream));
         bare_of[j] = h->last_bare;
@@ -2033,8 +2059,12 @@ int ctws_open(int device, ctws_handle** out) {
         h->frontier_max_iters = std::max(0, std::min(kFrontierMaxItersCap, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_GAUSS_YX")) h->gauss_yx = std::atoi(t);
     if (const char* t = std::getenv("CTWS_HOST_BATCH_VOXELS")) h->host_batch_voxels = std::max<int64_t>(1, std::atoll(t));
+    if (const char* t = std::getenv("CTWS_HOST_RAMP")) h->host_ramp = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_H2D_MODE")) h->h2d_mode = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_H2D_WGS")) h->h2d_wgs = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_HOST_BATCH_BLOCKS")) h->host_batch_blocks = std::max(0, std::atoi(t));
-    if (const char* t = std::getenv("CTWS_HOST_THREADS")) h->host_threads = std::max(1, std::atoi(t));
+    if (const char* t = std::getenv("CTWS_PACK_THREADS")) h->pack_threads = std::max(1, std::atoi(t));
+    if (const char* t = std::getenv("CTWS_UNPACK_THREADS")) h->unpack_threads = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_D2H_WGS")) h->d2h_wgs = std::max(0, std::atoi(t));
     if (const char* t = std::getenv("CTWS_WORDS_PER_WAVE")) h->words_per_wave = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_GAUSS_W")) {
@@ -2095,7 +2125,7 @@ void ctws_close(ctws_handle* h) {
         if (sl.pin_out) hipHostFree(sl.pin_out);
         if (sl.d_in.p) hipFree(sl.d_in.p);
         if (sl.d_out.p) hipFree(sl.d_out.p);
-        for (hipEvent_t e : {sl.ev_h2d, sl.ev_comp, sl.ev_d2h})
+        for (hipEvent_t e : {sl.ev_h2d, sl.ev_comp, sl.ev_d2h, sl.ev_t0, sl.ev_t1})
             if (e) hipEventDestroy(e);
         for (hipEvent_t e : sl.ev_blk) hipEventDestroy(e);
     }
@@ -2365,7 +2395,7 @@ int ctws_unique_u64(ctws_handle* h, const uint64_t* labels, int64_t n, int on_de
     unsigned long long hr[3];
     HIPCHK(hipMemcpyAsync(hr, red, sizeof(hr), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
-    const bool has_nz = hr[0] != ~0ull;
+    const bool has_nz = hr[1] != 0ull;  // (the min stays ~0 when every nonzero label is 2^64 - 1)
     const int64_t first = hr[2] ? 1 : 0;
     int64_t total = first;
     if (has_nz) {
