@@ -67,6 +67,7 @@ struct Workspace {
     // frontier bitmaps of the descent flood
     int64_t cap_front = 0;
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
+    uint64_t* fopen2 = nullptr;  // open voxels left to the frontier (k_open_tile clears the solved ones)
     uint32_t* fflags = nullptr;
     uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: generation of its last change
     uint32_t *wl0 = nullptr, *wl1 = nullptr, *qgen = nullptr;  // chunk worklists, queued generation
@@ -114,6 +115,8 @@ struct ctws_handle {
     int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
     // EDT: counters (64 B) + columns queued for the lower-envelope pass (k_edt_col_fh)
     DevBuf edt_fh;
+    DevBuf ot_stats;  // CTWS_TRACE: k_open_tile statistics
+    DevBuf edt_scratch;  // k_edt_real_line: per-thread parabola stacks
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
     // evaluation (k_eval.hip): gt / seg / pair hash tables with counts, state, sums, staging
@@ -151,6 +154,8 @@ struct ctws_handle {
     int fchunk3_masked[3] = {1, 32, 2};
     int fchunk3_env = 0;  // CTWS_FRONTIER_CHUNK3D given: used for every 3-D batch
     int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
+    int open_tile_passes = 2;  // CTWS_OPEN_TILE: k_open_tile passes before the frontier (0: none)
+    int cur_max[3] = {0, 0, 0};  // largest outer block extents (Z, Y, X) of the current batch
     int frontier_grid = 2048;  // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4)
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
@@ -276,6 +281,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(front0, front);
         ALLOC(front1, front);
         ALLOC(fopen, front);
+        ALLOC(fopen2, front);
         ALLOC(fchunk0, front / 64 + 1);
         ALLOC(fchunk1, front / 64 + 1);
         ALLOC(wl0, front / 64 + 1);
@@ -290,7 +296,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         w.cap_fstat = blocks;
     }
     if (!w.counter) ALLOC(counter, kCounterBytes / 4);
-    if (!w.taps) ALLOC(taps, 6 * 128);
+    if (!w.taps) ALLOC(taps, 6 * kTapSlot);
 #undef ALLOC
     return CTWS_OK;
 }
@@ -330,6 +336,8 @@ struct Plan {
     int nd_ws, dt_2d, pass2;
     int from_seeds;  // WatershedFromSeeds (watershed_from_seeds.py): given seeds, hmap = input
     int pitch[3];
+    double pitchd[3];  // pixel_pitch as given
+    bool real_pitch;   // a non-integer pitch: vigra's double-temporary distance path
     bool seeds_smooth, weights_smooth;
     double sig_seeds[3], sig_weights[3];
 };
@@ -343,7 +351,11 @@ int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
         return CTWS_EINVAL;
     }
     p.pass2 = cfg->pass_id == 1 ? 1 : 0;
-    for (int k = 0; k < 3; ++k) p.pitch[k] = 1;
+    for (int k = 0; k < 3; ++k) {
+        p.pitch[k] = 1;
+        p.pitchd[k] = 1.0;
+    }
+    p.real_pitch = false;
     if (cfg->has_pixel_pitch) {
         if (p.dt_2d) {
             h->err = "apply_dt_2d requires pixel_pitch None (watershed.py:151)";
@@ -351,11 +363,14 @@ int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
         }
         for (int k = 0; k < 3; ++k) {
             const double v = cfg->pixel_pitch[k];
-            if (v != std::floor(v) || v < 1.0 || v > 1000.0) {
-                h->err = "non-integer pixel_pitch is not supported by the exact integer EDT";
-                return CTWS_EUNSUPPORTED;
+            if (!(v > 0.0) || !std::isfinite(v)) {
+                h->err = "pixel_pitch must be positive";
+                return CTWS_EINVAL;
             }
-            p.pitch[k] = (int)v;
+            p.pitchd[k] = v;
+            // vigra: int(pitch) != pitch selects the real-valued path (multi_distance.hxx)
+            if (v != std::floor(v) || v > 4096.0) p.real_pitch = true;
+            else p.pitch[k] = (int)v;
         }
     }
     auto sig = [&](const double* s, int is_list, double* out, bool& en) -> int {
@@ -370,8 +385,8 @@ int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
                 h->err = "negative sigma";
                 return CTWS_EINVAL;
             }
-            if ((int)(3.0 * out[k] + 0.5) > 63) {
-                h->err = "sigma too large (radius > 63)";
+            if ((int)(3.0 * out[k] + 0.5) >= kTapSlot / 2) {
+                h->err = "sigma too large (radius >= 2048)";
                 return CTWS_EUNSUPPORTED;
             }
         }
@@ -441,8 +456,8 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
         const int a = axes[i];
         auto taps = gaussian_taps(sig[a]);
         const int r = (int)taps.size() / 2;
-        double* dtaps = w.taps + (taps_slot * 3 + a) * 128;
-        double* htaps = h->h_taps + (taps_slot * 3 + a) * 128;
+        double* dtaps = w.taps + (taps_slot * 3 + a) * kTapSlot;
+        double* htaps = h->h_taps + (taps_slot * 3 + a) * kTapSlot;
         std::memcpy(htaps, taps.data(), sizeof(double) * taps.size());
         HIPCHK(hipMemcpyAsync(dtaps, htaps, sizeof(double) * taps.size(), hipMemcpyHostToDevice, h->stream));
         float* out = (i == na - 1) ? dst : ((i % 2 == 0) ? w.A : w.Bf);
@@ -452,8 +467,8 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
         if (h->gauss_yx && a == 1 && i + 1 == na - 1 && axes[i + 1] == 2 && r >= 1 && r <= kGaussMaxR) {
             auto tx = gaussian_taps(sig[2]);
             if ((int)tx.size() / 2 == r) {
-                double* dtx = w.taps + (taps_slot * 3 + 2) * 128;
-                double* htx = h->h_taps + (taps_slot * 3 + 2) * 128;
+                double* dtx = w.taps + (taps_slot * 3 + 2) * kTapSlot;
+                double* htx = h->h_taps + (taps_slot * 3 + 2) * kTapSlot;
                 std::memcpy(htx, tx.data(), sizeof(double) * tx.size());
                 HIPCHK(hipMemcpyAsync(dtx, htx, sizeof(double) * tx.size(), hipMemcpyHostToDevice, h->stream));
                 const int TX = 128 - 2 * r;
@@ -468,7 +483,12 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
         }
         if (r >= 1 && r <= kGaussMaxR) {
             // sliding-window kernels (k_gauss.hip)
-            if (a == 2) {
+            if (a == 2 && maxX > 1024) {
+                // rows longer than a wave's registers hold: the generic row kernel
+                dim3 g((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
+                const size_t lds = 2 * 128 * 4 + 4 * (size_t)maxX * 4;
+                k_gauss_row<<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax, out);
+            } else if (a == 2) {
                 // rows per wave shrink with X: size the grid for the widest block
                 const int rpw = 64 / ((maxX + 15) / 16);
                 dim3 g((unsigned)(((int64_t)maxZ * maxY + 4 * rpw - 1) / (4 * rpw)), nb);
@@ -511,6 +531,8 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
     }
     return CTWS_OK;
 }
+
+int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // ---- flood rounds until no tile is active -----------------------------------------------
 // tile extents of k_flood_packed (PTile) and k_flood (FloodTile)
@@ -610,6 +632,41 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     HIPCHK(hipMemsetAsync(w.fchunk1, 0, sizeof(uint32_t) * (size_t)nch, h->stream));
     HIPCHK(hipMemsetAsync(w.qgen, 0, sizeof(uint32_t) * (size_t)nch, h->stream));
     HIPCHK(hipMemsetAsync(w.wlcnt, 0, sizeof(uint32_t) * (size_t)(h->frontier_max_iters + 2), h->stream));
+    // open components closed inside a tile: solved in LDS (k_open_tile), on the plain and the
+    // half-shifted tile grid; the frontier relaxes what is left (w.fopen2).  w.fopen keeps every
+    // relaxed voxel for the fixpoint check.
+    HIPCHK(hipMemcpyAsync(w.fopen2, w.fopen, sizeof(uint64_t) * (size_t)TF, hipMemcpyDeviceToDevice, h->stream));
+    {
+        uint32_t* ost = nullptr;
+        if (h->trace) {
+            int r0;
+            if ((r0 = grow(h, h->ot_stats, 16)) != CTWS_OK) return r0;
+            ost = (uint32_t*)h->ot_stats.p;
+            HIPCHK(hipMemsetAsync(ost, 0, 16, h->stream));
+        }
+        for (int pass = 0; pass < h->open_tile_passes; ++pass) {
+            if (pl.nd_ws == 3) {
+                using T = OTileDims<3>;
+                const int sz = pass ? T::TZ / 2 : 0, sy = pass ? T::TY / 2 : 0, sx = pass ? T::TX / 2 : 0;
+                const unsigned nt = (unsigned)(cdiv(h->cur_max[0] + sz, T::TZ) * cdiv(h->cur_max[1] + sy, T::TY) *
+                                               cdiv(h->cur_max[2] + sx, T::TX));
+                k_open_tile<3><<<dim3(nt, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen2, sz, sy, sx, ost);
+            } else {
+                using T = OTileDims<2>;
+                const int sy = pass ? T::TY / 2 : 0, sx = pass ? T::TX / 2 : 0;
+                const unsigned nt = (unsigned)(h->cur_max[0] * cdiv(h->cur_max[1] + sy, T::TY) *
+                                               cdiv(h->cur_max[2] + sx, T::TX));
+                k_open_tile<2><<<dim3(nt, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen2, 0, sy, sx, ost);
+            }
+            LAUNCHCHK();
+        }
+        if (ost) {
+            uint32_t c[3];
+            HIPCHK(hipMemcpy(c, ost, sizeof(c), hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "[ctws] open tiles: %u of %u open voxels solved in LDS, %u in over-full tiles\n", c[0],
+                         c[1], c[2]);
+        }
+    }
     // iteration 0: every chunk with an open voxel
     const dim3 lg((unsigned)std::min<int64_t>((TF / nb + 64 * 64 * kFrontierWavesHost - 1) / (64 * 64 * kFrontierWavesHost) + 1,
                                               1024), nb);
@@ -619,7 +676,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     X(0, 2, 1, 64, 1) X(1, 2, 2, 32, 1) X(2, 2, 4, 16, 1) X(3, 2, 8, 8, 1) X(4, 3, 1, 8, 8) X(5, 3, 2, 8, 4) \
     X(6, 3, 1, 16, 4) X(7, 3, 4, 4, 4) X(8, 3, 8, 8, 1) X(9, 3, 1, 32, 2)
 #define CTWS_LIST0(K, ND, CW, CY, CZ) \
-    case K: k_frontier_list0<CW, CY, CZ><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt); break;
+    case K: k_frontier_list0<CW, CY, CZ><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen2, wl[0], w.wlcnt); break;
     switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_LIST0) default: h->err = "bad frontier chunk"; return CTWS_EINVAL; }
 #undef CTWS_LIST0
     LAUNCHCHK();
@@ -641,7 +698,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
 #define CTWS_FRONTIER(K, ND, CW, CY, CZ)                                                                            \
     case K:                                                                                                         \
         k_frontier<ND, CW, CY, CZ><<<fg, 256, 0, h->stream>>>(                                                      \
-            w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
+            w.desc, w.stat, w.hm, w.key, w.fopen2, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             h->frontier_reps);                                                                                      \
         break;
@@ -690,7 +747,6 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     return CTWS_OK;
 }
 
-int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 
 int64_t words_of(int64_t n) { return n / 64 + 1; }
@@ -767,6 +823,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int maxZ = 0, maxY = 0, maxX = 0, max_tiles = 0;
     int64_t maxN = 0, maxNI = 0;
     int maxIZ = 0, maxIY = 0, maxIX = 0;
+    bool real_edt = pl.real_pitch;  // the batch's distances take vigra's real-valued path
     const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
     {
         bool any_mask = false;
@@ -832,8 +889,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             d.hcap = cap;
             TH += cap;
         }
-        d.maxd = (uint32_t)((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z + (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
-                            (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X);
+        d.maxd = (uint32_t)std::min<int64_t>((int64_t)pl.pitch[0] * pl.pitch[0] * d.Z * d.Z +
+                                                 (int64_t)pl.pitch[1] * pl.pitch[1] * d.Y * d.Y +
+                                                 (int64_t)pl.pitch[2] * pl.pitch[2] * d.X * d.X, 0xFFFFFFFFll);
         d.fbase = TF;
         // frontier bitmaps: rows padded to a multiple of 64, and at least 64 words per frontier
         // chunk brick (k_frontier), so that the per-chunk arrays can be indexed at fbase / 64
@@ -859,9 +917,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         maxH = std::max(maxH, d.hcap);
         maxRows = std::max(maxRows, (int64_t)d.Z * d.Y);
         maxIRows = std::max(maxIRows, (int64_t)d.IZ * d.IY);
-        // validation against what the kernels assume
-        if (d.X > 1024 || d.Y > 2048 || d.Z > 2048 || d.N >= (1ll << 31)) {
-            h->err = "outer block too large for the kernels (X <= 1024, Y, Z <= 2048, N < 2^31)";
+        // validation against what the kernels assume (run_blocks already failed such blocks
+        // individually, block_refusal)
+        if (d.X > 4096 || d.Y > 2048 || d.Z > 2048 || d.N >= (1ll << 31)) {
+            h->err = "outer block too large for the kernels (X <= 4096, Y, Z <= 2048, N < 2^31)";
             return CTWS_EUNSUPPORTED;
         }
         if (d.iz0 < 0 || d.iy0 < 0 || d.ix0 < 0 || d.iz0 + d.IZ > d.Z || d.iy0 + d.IY > d.Y || d.ix0 + d.IX > d.X ||
@@ -892,12 +951,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         double dmax;
         if (pl.dt_2d) dmax = (double)d.Y * d.Y + (double)d.X * d.X;
         else
-            dmax = std::pow((double)pl.pitch[0] * d.Z, 2) + std::pow((double)pl.pitch[1] * d.Y, 2) +
-                   std::pow((double)pl.pitch[2] * d.X, 2);
-        if (dmax >= 16777216.0 && !pl.from_seeds) {
-            h->err = "dmax >= 2^24: float32 squared distances are no longer exact";
-            return CTWS_EUNSUPPORTED;
-        }
+            dmax = std::pow(pl.pitchd[0] * d.Z, 2) + std::pow(pl.pitchd[1] * d.Y, 2) + std::pow(pl.pitchd[2] * d.X, 2);
+        // dmax >= 2^24: float32 squared distances are no longer exact integers; vigra's float
+        // arithmetic is then reproduced by the real-valued path (k_edt_real_*)
+        if (dmax >= 16777216.0 && !pl.from_seeds) real_edt = true;
     }
     // flood tile grids: the largest (wide kernel) bounds the per-tile arrays
     auto set_tiles = [&](bool packed) {
@@ -914,6 +971,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             max_tiles = std::max(max_tiles, d.tz * d.ty * d.tx);
         }
     };
+    h->last_bare.assign(nb, 1);  // (a run stopped early by a test hook writes no labels)
+    h->cur_max[0] = maxZ;
+    h->cur_max[1] = maxY;
+    h->cur_max[2] = maxX;
     set_tiles(true);
     const int64_t TT_packed = TT;
     set_tiles(false);
@@ -1034,7 +1095,31 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     if (pl.from_seeds) {
         if ((r = fs_seeds(h, desc, nb, TH, TW, TS, maxH, maxRows, vg, wg)) != CTWS_OK) return r;
     } else {
-    {
+    if (real_edt) {
+        // vigra's real-valued path: double temporary (non-integer pitch) or float (dmax >= 2^24)
+        EdtRealParams er{{pl.pitchd[0], pl.pitchd[1], pl.pitchd[2]}, pl.dt_2d, pl.real_pitch ? 1 : 0};
+        const int nthr = 64 * 256;
+        const int maxL = std::max(maxZ, std::max(maxY, maxX));
+        const size_t esz = pl.real_pitch ? 8 : 4;
+        if ((r = grow(h, h->edt_scratch, (size_t)nthr * maxL * (2 * esz + 20))) != CTWS_OK) return r;
+        char* scr = (char*)h->edt_scratch.p;
+        auto run_real = [&](auto tag) {
+            using T = decltype(tag);
+            T* tmp = (T*)w.key;  // free until the flood
+            k_edt_real_init<T><<<vg, 256, 0, h->stream>>>(w.desc, w.stat, er, (const uint32_t*)w.A, tmp);
+            for (int a = pl.dt_2d ? 1 : 0; a < 3; ++a)
+                k_edt_real_line<T><<<nthr / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb, er, a, tmp, scr, maxL);
+            k_edt_real_final<T><<<vg, 256, 0, h->stream>>>(w.desc, w.stat, er, tmp, w.dt, w.smin, w.smax);
+        };
+        if (pl.real_pitch) run_real(double());
+        else run_real(float());
+        LAUNCHCHK();
+        if (!pl.dt_2d && pl.nd_ws == 2) {
+            dim3 gs((unsigned)maxZ, nb);
+            k_dt_slice_stats<<<gs, 256, 0, h->stream>>>(w.desc, w.stat, w.dt, w.smin, w.smax);
+            LAUNCHCHK();
+        }
+    } else {
         // y pass (final for a 2-D dt), then z pass (3-D dt)
         const int Wy = h->edt_w ? h->edt_w : edt_col_width(maxY);
         EdtColParams ep{1, pl.pitch[1] * pl.pitch[1], pl.dt_2d, pl.dt_2d, 0u};
@@ -1081,7 +1166,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             }
         }
     }
-    if (h->trace) {
+    if (h->trace && !real_edt) {
         uint32_t c[2];
         HIPCHK(hipMemcpy(c, h->edt_fh.p, sizeof(c), hipMemcpyDeviceToHost));
         std::fprintf(stderr, "[ctws] edt lower-envelope columns: y %u z %u\n", c[0], c[1]);
@@ -1591,6 +1676,30 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     return CTWS_OK;
 }
 
+// Why a block cannot run, or nullptr.  These blocks get CTWS_BLOCK_FAILED with the reason (the
+// reference job would raise at that block, or the block is outside what the kernels support)
+// while the other blocks of the call run.
+const char* block_refusal(const Plan& pl, const ctws_block& b) {
+    const int64_t Z = b.outer_shape[0], Y = b.outer_shape[1], X = b.outer_shape[2];
+    if (X > 4096 || Y > 2048 || Z > 2048 || Z * Y * X >= (1ll << 31))
+        return "outer block too large for the kernels (X <= 4096, Y, Z <= 2048, fewer than 2^31 voxels)";
+    // vigra's convolveLine: "kernel longer than line" (the reference raises at this block)
+    auto too_short = [&](const double* sg, bool en) -> bool {
+        if (!en) return false;
+        const int64_t lens[3] = {Z, Y, X};
+        for (int a = (pl.nd_ws == 3 ? 0 : 1); a < 3; ++a) {
+            if (sg[a] <= 0) continue;
+            int r = (int)(3.0 * sg[a] + 0.5);
+            if (r == 0) r = 1;
+            if (lens[a] < r + 1) return true;
+        }
+        return false;
+    };
+    if (!pl.from_seeds && (too_short(pl.sig_seeds, pl.seeds_smooth) || too_short(pl.sig_weights, pl.weights_smooth)))
+        return "convolveLine(): kernel longer than line (vigra raises, as the reference job would)";
+    return nullptr;
+}
+
 int64_t batch_voxels_budget() {
     const char* e = std::getenv("CTWS_BATCH_VOXELS");
     if (e) return std::max<int64_t>(1, std::atoll(e));
@@ -1830,7 +1939,8 @@ int run_blocks_host(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_bl
             // pass 1: in-mask voxels get + block_id * prod(block_shape); pass 2 / from-seeds
             // outputs are the uint32 values themselves
             const uint64_t off = (pl.pass2 || pl.from_seeds) ? 0ull : (uint64_t)b.block_id * bvol;
-            widen_codes(*h->unpack_pool, b, (const uint32_t*)((char*)sl.pin_out + B.o_off[i]), off, bare_of[j][i] != 0);
+            const bool bare = i < (int)bare_of[j].size() ? bare_of[j][i] != 0 : true;
+            widen_codes(*h->unpack_pool, b, (const uint32_t*)((char*)sl.pin_out + B.o_off[i]), off, bare);
         }
         const double ms = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3;
         unpack_ms += ms;
@@ -1980,6 +2090,11 @@ int run_blocks(ctws_handle* h, const ctws_cfg* cfg_in, ctws_block* blocks, int n
         b.status = CTWS_BLOCK_WRITTEN;
         b.n_ids = 0;
         b.max_label = 0;
+        if (const char* why = block_refusal(pl, b)) {
+            b.status = CTWS_BLOCK_FAILED;
+            h->err += "block " + std::to_string((long long)b.block_id) + " failed (" + why + "); ";
+            continue;
+        }
         if (!device_ptrs && b.mask) {
             const int64_t* sh = b.outer_shape;
             bool any = false;
@@ -2088,11 +2203,12 @@ int ctws_open(int device, ctws_handle** out) {
         parse_chunk(t, h->fchunk3, true);
         h->fchunk3_env = 1;
     }
+    if (const char* t = std::getenv("CTWS_OPEN_TILE")) h->open_tile_passes = std::max(0, std::min(2, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_taps, 6 * 128 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void**)&h->h_taps, 6 * kTapSlot * sizeof(double), hipHostMallocDefault) != hipSuccess) {
         delete h;
         return CTWS_EHIP;
     }
@@ -2107,10 +2223,10 @@ void ctws_close(ctws_handle* h) {
     Workspace& w = h->ws;
     void* ptrs[] = {w.fin, w.dt, w.A, w.Bf, w.sm, w.hm, w.cls, w.P, w.PF, w.lab, w.key, w.W, w.Wp, w.csum,
                     w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.lines0, w.lines1, w.desc, w.stat, w.counter,
-                    w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
+                    w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fopen2, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
                     w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
                     h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p,
-                    h->edt_fh.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
+                    h->edt_fh.p, h->ot_stats.p, h->edt_scratch.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
                     h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p};
     for (void* p : ptrs)

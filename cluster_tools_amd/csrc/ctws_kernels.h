@@ -18,6 +18,11 @@ struct EdtColParams {
     int per_slice;
     uint32_t max_dist;
 };
+struct EdtRealParams {
+    double pitch[3];
+    int per_slice;  // 2-D dt: per-slice lines (y, x), dmax = Y^2 + X^2
+    int real;       // 1: non-integer pitch (double temporary, maxDist = dmax); 0: float, ceil(dmax)
+};
 struct HmapParams {
     float a, b;
     int per_slice;
@@ -48,6 +53,12 @@ __global__ void k_edt_col(const BlockDesc*, BlockStat*, EdtColParams, const uint
                           uint32_t*, unsigned long long*, uint32_t*);
 __global__ void k_edt_col_fh(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*, uint32_t*,
                              uint32_t*, const unsigned long long*, const uint32_t*);
+template <class T>
+__global__ void k_edt_real_init(const BlockDesc*, const BlockStat*, EdtRealParams, const uint32_t*, T*);
+template <class T>
+__global__ void k_edt_real_line(const BlockDesc*, const BlockStat*, int, EdtRealParams, int, T*, char*, int);
+template <class T>
+__global__ void k_edt_real_final(const BlockDesc*, BlockStat*, EdtRealParams, const T*, float*, uint32_t*, uint32_t*);
 __global__ void k_dt_slice_stats(const BlockDesc*, const BlockStat*, const float*, uint32_t*, uint32_t*);
 __global__ void k_set_active(const BlockDesc*, BlockStat*, int);
 
@@ -59,6 +70,7 @@ __global__ void k_gauss_col(const BlockDesc*, const BlockStat*, GaussParams, Hma
                             const float*, const uint32_t*, const uint32_t*, float*);
 __global__ void k_gauss_row(const BlockDesc*, const BlockStat*, GaussParams, HmapParams, const double*, const float*,
                             const float*, const uint32_t*, const uint32_t*, float*);
+constexpr int kTapSlot = 4096;  // doubles per taps slot: radius <= 2047
 constexpr int kGaussMaxR = 12;  // sliding-window kernels for radius <= 12 (sigma < 4)
 template <int W, int R>
 __global__ void k_gauss_col_r(const BlockDesc*, const BlockStat*, GaussParams, HmapParams, const double*, const float*,
@@ -155,6 +167,19 @@ hipError_t fs_segmented_sort(void* tmp, size_t& bytes, const uint32_t* in, uint3
                              const int* beg, const int* end, hipStream_t stream);
 template <int CW, int CY, int CZ>
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
+template <int ND>
+__global__ void k_open_tile(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint64_t*, int, int, int,
+                            uint32_t*);
+template <int ND>
+struct OTileDims;
+template <>
+struct OTileDims<2> {
+    static constexpr int TZ = 1, TY = 64, TX = 64;
+};
+template <>
+struct OTileDims<3> {
+    static constexpr int TZ = 8, TY = 8, TX = 64;
+};
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>
 __global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint64_t*,

@@ -677,6 +677,148 @@ __global__ void __launch_bounds__(256) k_dt_slice_stats(const BlockDesc* __restr
 }  // namespace ctws
 
 namespace ctws {
+// =========================================================================================
+// vigra's real-valued distance path, for the configurations the exact integer kernels above do
+// not cover: a non-integer pixel_pitch (watershed.py:157-158; vigra then works on a temporary
+// array, T = double) and dmax >= 2^24 (squared distances are no longer exact integers in the
+// float32 destination vigra works on directly, T = float).  separableMultiDistSquared: init
+// f = (fg ? 0 : maxDist), then per axis 0, 1, 2 (2-D dt: y, x) detail::distParabola on every
+// line with sigma = pitch[axis] -- the same double expressions in the same order as the
+// restatement in oracle/ctws_oracle.cpp (dist_parabola), so the result is bit-identical -- then
+// sqrt in float.  One thread per line, its parabola stack in a global scratch (element k of
+// thread t at k * nthr + t); the few blocks that need this are not a throughput path.
+// =========================================================================================
+template <class T>
+__global__ void __launch_bounds__(256) k_edt_real_init(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                       EdtRealParams ep, const uint32_t* __restrict__ xd2,
+                                                       T* __restrict__ tmp) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    double dmax;
+    if (ep.per_slice) dmax = (double)B.Y * B.Y + (double)B.X * B.X;
+    else {
+        const double a = ep.pitch[0] * B.Z, b = ep.pitch[1] * B.Y, c = ep.pitch[2] * B.X;
+        dmax = a * a + b * b + c * c;
+    }
+    // real pitch: (Real)dmax; integer pitch (float destination): DestType(ceil(dmax))
+    const T maxd = ep.real ? (T)dmax : (T)ceil(dmax);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x)
+        tmp[B.base + i] = xd2[B.base + i] == 0u ? (T)0 : maxd;  // x pass: 0 exactly at the foreground
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_edt_real_line(const BlockDesc* __restrict__ D, const BlockStat* S, int nb,
+                                                       EdtRealParams ep, int axis, T* __restrict__ arr,
+                                                       char* __restrict__ scratch, int max_len) {
+    const int nthr = gridDim.x * blockDim.x;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    // scratch: line (T), left (double), right (double), apex values (T), centers (int)
+    T* sline = (T*)scratch;
+    double* sleft = (double*)(scratch + (size_t)nthr * max_len * sizeof(T));
+    double* sright = sleft + (size_t)nthr * max_len;
+    T* sval = (T*)(sright + (size_t)nthr * max_len);
+    int* scen = (int*)(sval + (size_t)nthr * max_len);
+    const double sigma = ep.per_slice ? 1.0 : ep.pitch[axis];
+    const double sigma2 = sigma * sigma, sigma22 = 2.0 * sigma2;
+    for (int bi = 0; bi < nb; ++bi) {
+        const BlockDesc& B = D[bi];
+        if (!S[bi].active) continue;
+        const int L = axis == 0 ? B.Z : (axis == 1 ? B.Y : B.X);
+        const int64_t lstride = axis == 0 ? (int64_t)B.Y * B.X : (axis == 1 ? B.X : 1);
+        const int64_t nlines = B.N / L;
+        for (int64_t ln = t; ln < nlines; ln += nthr) {
+            int64_t base;
+            if (axis == 0) base = ln;  // (y, x)
+            else if (axis == 1) base = (ln / B.X) * (int64_t)B.Y * B.X + ln % B.X;  // (z, x)
+            else base = ln * B.X;  // (z, y)
+            T* a = arr + B.base + base;
+            auto LN = [&](int i) -> T& { return sline[(size_t)i * nthr + t]; };
+            auto LF = [&](int k) -> double& { return sleft[(size_t)k * nthr + t]; };
+            auto RT = [&](int k) -> double& { return sright[(size_t)k * nthr + t]; };
+            auto PV = [&](int k) -> T& { return sval[(size_t)k * nthr + t]; };
+            auto CN = [&](int k) -> int& { return scen[(size_t)k * nthr + t]; };
+            for (int i = 0; i < L; ++i) LN(i) = a[i * lstride];
+            const double w = (double)L;
+            int top = 0;
+            LF(0) = 0.0;
+            CN(0) = 0;
+            RT(0) = w;
+            PV(0) = LN(0);
+            double current = 1.0;
+            for (int is = 1; is < L; ++is, current += 1.0) {
+                double intersection;
+                while (true) {
+                    const double diff = current - (double)CN(top);
+                    intersection = current + ((double)(LN(is) - PV(top)) - sigma2 * (diff * diff)) / (sigma22 * diff);
+                    if (intersection < LF(top)) {
+                        if (--top < 0) {  // the stack ran empty
+                            intersection = 0.0;
+                            break;
+                        }
+                        continue;
+                    } else if (intersection < RT(top)) {
+                        RT(top) = intersection;
+                    }
+                    break;
+                }
+                ++top;
+                LF(top) = intersection;
+                CN(top) = is;
+                RT(top) = w;
+                PV(top) = LN(is);
+            }
+            int it = 0;
+            double cur = 0.0;
+            for (int o = 0; o < L; ++o, cur += 1.0) {
+                while (cur >= RT(it)) ++it;
+                const double diff = cur - (double)CN(it);
+                a[o * lstride] = (T)(sigma2 * (diff * diff) + (double)PV(it));
+            }
+        }
+    }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) k_edt_real_final(const BlockDesc* __restrict__ D, BlockStat* S, EdtRealParams ep,
+                                                        const T* __restrict__ tmp, float* __restrict__ dt,
+                                                        uint32_t* __restrict__ slice_min, uint32_t* __restrict__ slice_max) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = __fsqrt_rn((float)tmp[B.base + i]);
+        dt[B.base + i] = v;
+        const uint32_t o = ordf(v);
+        mn = min(mn, o);
+        mx = max(mx, o);
+        if (ep.per_slice) {
+            const int z = (int)(i / YX);
+            atomic_min_if(&slice_min[B.sbase + z], o);
+            atomic_max_if(&slice_max[B.sbase + z], o);
+        }
+    }
+    mn = wg_reduce_u32(mn, OpMin());
+    mx = wg_reduce_u32(mx, OpMax());
+    if (threadIdx.x == 0) {
+        atomic_min_if(&S[blockIdx.y].dt_min, mn);
+        atomic_max_if(&S[blockIdx.y].dt_max, mx);
+    }
+}
+
+#define CTWS_EDT_REAL(T)                                                                                          \
+    template __global__ void k_edt_real_init<T>(const BlockDesc*, const BlockStat*, EdtRealParams, const uint32_t*, \
+                                                T*);                                                               \
+    template __global__ void k_edt_real_line<T>(const BlockDesc*, const BlockStat*, int, EdtRealParams, int, T*, char*, \
+                                                int);                                                              \
+    template __global__ void k_edt_real_final<T>(const BlockDesc*, BlockStat*, EdtRealParams, const T*, float*,      \
+                                                 uint32_t*, uint32_t*);
+CTWS_EDT_REAL(float)
+CTWS_EDT_REAL(double)
+#undef CTWS_EDT_REAL
+}  // namespace ctws
+
+namespace ctws {
 // a block takes part in the pipeline iff something is above the threshold (_apply_dt)
 __global__ void k_set_active(const BlockDesc* __restrict__ D, BlockStat* S, int n) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;

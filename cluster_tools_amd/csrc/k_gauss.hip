@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256) k_gauss_col(const BlockDesc* __restrict__
                                                    const uint32_t* smin, const uint32_t* smax,
                                                    float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) int smem_i[];
-    double* k = (double*)smem_i;                        // 2r+1 taps (<= 128)
+    const double* k = taps;                             // 2r+1 taps (any radius: read through the cache)
     float* col = (float*)(smem_i + 2 * 128);
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
@@ -75,8 +75,6 @@ __global__ void __launch_bounds__(256) k_gauss_col(const BlockDesc* __restrict__
     const int c = threadIdx.x % W;
     const int r0 = threadIdx.x / W;
     constexpr int RS = 256 / W;
-    const int ntap = 2 * gp.r + 1;
-    for (int j = threadIdx.x; j < ntap; j += 256) k[j] = taps[j];
     const bool colok = xb + c < B.X;
     if (gp.hmap_src) {
         const BlockStat& st = S[blockIdx.y];
@@ -121,14 +119,12 @@ __global__ void __launch_bounds__(256) k_gauss_row(const BlockDesc* __restrict__
                                                    const uint32_t* smin, const uint32_t* smax,
                                                    float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) int smem_i[];
-    double* k = (double*)smem_i;
+    const double* k = taps;  // 2r+1 taps (any radius: read through the cache)
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int X = B.X;
     float* rowb = (float*)(smem_i + 2 * 128) + wave * X;
-    const int ntap = 2 * gp.r + 1;
-    for (int j = threadIdx.x; j < ntap; j += 256) k[j] = taps[j];
     const int64_t row = (int64_t)blockIdx.x * 4 + wave;
     const bool rowok = row < (int64_t)B.Z * B.Y;
     const int64_t rbase = row * X;

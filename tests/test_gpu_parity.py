@@ -187,3 +187,16 @@ def test_config2_block_full_size(gpu_handle):
     vis, vim = vi_scores(res['output'], ref['output'])
     assert vis + vim <= VI_TOL
     assert rand_scores(res['output'], ref['output'])[0] <= ARE_TOL
+
+
+def test_refusals_are_per_block(gpu_handle):
+    """A block the reference would fail on (vigra: kernel longer than line) fails alone: the
+    other blocks of the call are written, as the reference job writes the blocks before the one
+    that raises."""
+    config, block = CASES['3d_default']
+    short = dict(input=np.ascontiguousarray(block['input'][:4]), block_id=5)   # Z = 4 < radius 6 + 1
+    res = gpu_handle.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=3), short, dict(block, block_id=4)])
+    assert [r['status'] for r in res] == [0, 4, 0]
+    ref = O.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=4)])[0]
+    vis, vim = vi_scores(res[2]['output'], ref['output'])
+    assert vis + vim <= VI_TOL
