@@ -67,7 +67,6 @@ struct Workspace {
     // frontier bitmaps of the descent flood
     int64_t cap_front = 0;
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
-    uint64_t* fopen2 = nullptr;  // open voxels left to the frontier (k_open_tile clears the solved ones)
     uint32_t* fflags = nullptr;
     uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: generation of its last change
     uint32_t *wl0 = nullptr, *wl1 = nullptr, *qgen = nullptr;  // chunk worklists, queued generation
@@ -115,7 +114,6 @@ struct ctws_handle {
     int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
     // EDT: counters (64 B) + columns queued for the lower-envelope pass (k_edt_col_fh)
     DevBuf edt_fh;
-    DevBuf ot_stats;  // CTWS_TRACE: k_open_tile statistics
     DevBuf edt_scratch;  // k_edt_real_line: per-thread parabola stacks
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
@@ -154,7 +152,6 @@ struct ctws_handle {
     int fchunk3_masked[3] = {1, 32, 2};
     int fchunk3_env = 0;  // CTWS_FRONTIER_CHUNK3D given: used for every 3-D batch
     int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
-    int open_tile_passes = 2;  // CTWS_OPEN_TILE: k_open_tile passes before the frontier (0: none)
     int cur_max[3] = {0, 0, 0};  // largest outer block extents (Z, Y, X) of the current batch
     int frontier_grid = 2048;  // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4)
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
@@ -281,7 +278,6 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(front0, front);
         ALLOC(front1, front);
         ALLOC(fopen, front);
-        ALLOC(fopen2, front);
         ALLOC(fchunk0, front / 64 + 1);
         ALLOC(fchunk1, front / 64 + 1);
         ALLOC(wl0, front / 64 + 1);
@@ -632,41 +628,6 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     HIPCHK(hipMemsetAsync(w.fchunk1, 0, sizeof(uint32_t) * (size_t)nch, h->stream));
     HIPCHK(hipMemsetAsync(w.qgen, 0, sizeof(uint32_t) * (size_t)nch, h->stream));
     HIPCHK(hipMemsetAsync(w.wlcnt, 0, sizeof(uint32_t) * (size_t)(h->frontier_max_iters + 2), h->stream));
-    // open components closed inside a tile: solved in LDS (k_open_tile), on the plain and the
-    // half-shifted tile grid; the frontier relaxes what is left (w.fopen2).  w.fopen keeps every
-    // relaxed voxel for the fixpoint check.
-    HIPCHK(hipMemcpyAsync(w.fopen2, w.fopen, sizeof(uint64_t) * (size_t)TF, hipMemcpyDeviceToDevice, h->stream));
-    {
-        uint32_t* ost = nullptr;
-        if (h->trace) {
-            int r0;
-            if ((r0 = grow(h, h->ot_stats, 16)) != CTWS_OK) return r0;
-            ost = (uint32_t*)h->ot_stats.p;
-            HIPCHK(hipMemsetAsync(ost, 0, 16, h->stream));
-        }
-        for (int pass = 0; pass < h->open_tile_passes; ++pass) {
-            if (pl.nd_ws == 3) {
-                using T = OTileDims<3>;
-                const int sz = pass ? T::TZ / 2 : 0, sy = pass ? T::TY / 2 : 0, sx = pass ? T::TX / 2 : 0;
-                const unsigned nt = (unsigned)(cdiv(h->cur_max[0] + sz, T::TZ) * cdiv(h->cur_max[1] + sy, T::TY) *
-                                               cdiv(h->cur_max[2] + sx, T::TX));
-                k_open_tile<3><<<dim3(nt, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen2, sz, sy, sx, ost);
-            } else {
-                using T = OTileDims<2>;
-                const int sy = pass ? T::TY / 2 : 0, sx = pass ? T::TX / 2 : 0;
-                const unsigned nt = (unsigned)(h->cur_max[0] * cdiv(h->cur_max[1] + sy, T::TY) *
-                                               cdiv(h->cur_max[2] + sx, T::TX));
-                k_open_tile<2><<<dim3(nt, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen2, 0, sy, sx, ost);
-            }
-            LAUNCHCHK();
-        }
-        if (ost) {
-            uint32_t c[3];
-            HIPCHK(hipMemcpy(c, ost, sizeof(c), hipMemcpyDeviceToHost));
-            std::fprintf(stderr, "[ctws] open tiles: %u of %u open voxels solved in LDS, %u in over-full tiles\n", c[0],
-                         c[1], c[2]);
-        }
-    }
     // iteration 0: every chunk with an open voxel
     const dim3 lg((unsigned)std::min<int64_t>((TF / nb + 64 * 64 * kFrontierWavesHost - 1) / (64 * 64 * kFrontierWavesHost) + 1,
                                               1024), nb);
@@ -676,7 +637,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
     X(0, 2, 1, 64, 1) X(1, 2, 2, 32, 1) X(2, 2, 4, 16, 1) X(3, 2, 8, 8, 1) X(4, 3, 1, 8, 8) X(5, 3, 2, 8, 4) \
     X(6, 3, 1, 16, 4) X(7, 3, 4, 4, 4) X(8, 3, 8, 8, 1) X(9, 3, 1, 32, 2)
 #define CTWS_LIST0(K, ND, CW, CY, CZ) \
-    case K: k_frontier_list0<CW, CY, CZ><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen2, wl[0], w.wlcnt); break;
+    case K: k_frontier_list0<CW, CY, CZ><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt); break;
     switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_LIST0) default: h->err = "bad frontier chunk"; return CTWS_EINVAL; }
 #undef CTWS_LIST0
     LAUNCHCHK();
@@ -698,7 +659,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
 #define CTWS_FRONTIER(K, ND, CW, CY, CZ)                                                                            \
     case K:                                                                                                         \
         k_frontier<ND, CW, CY, CZ><<<fg, 256, 0, h->stream>>>(                                                      \
-            w.desc, w.stat, w.hm, w.key, w.fopen2, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
+            w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             h->frontier_reps);                                                                                      \
         break;
@@ -2203,7 +2164,6 @@ int ctws_open(int device, ctws_handle** out) {
         parse_chunk(t, h->fchunk3, true);
         h->fchunk3_env = 1;
     }
-    if (const char* t = std::getenv("CTWS_OPEN_TILE")) h->open_tile_passes = std::max(0, std::min(2, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -2223,10 +2183,10 @@ void ctws_close(ctws_handle* h) {
     Workspace& w = h->ws;
     void* ptrs[] = {w.fin, w.dt, w.A, w.Bf, w.sm, w.hm, w.cls, w.P, w.PF, w.lab, w.key, w.W, w.Wp, w.csum,
                     w.smin, w.smax, w.sb, w.slmax, w.soff, w.surv, w.act0, w.act1, w.lines0, w.lines1, w.desc, w.stat, w.counter,
-                    w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fopen2, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
+                    w.taps, w.hkey, w.hpos, w.p2err, w.front0, w.front1, w.fopen, w.fflags, w.fchunk0, w.fchunk1, w.wl0, w.wl1, w.qgen, w.wlcnt,
                     w.fstat, h->st_in.p, h->st_mask.p, h->st_init.p, h->st_out.p, h->rl_lab.p, h->rl_bits.p,
                     h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p,
-                    h->edt_fh.p, h->ot_stats.p, h->edt_scratch.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
+                    h->edt_fh.p, h->edt_scratch.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
                     h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p};
     for (void* p : ptrs)

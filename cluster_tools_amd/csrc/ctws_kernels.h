@@ -167,19 +167,6 @@ hipError_t fs_segmented_sort(void* tmp, size_t& bytes, const uint32_t* in, uint3
                              const int* beg, const int* end, hipStream_t stream);
 template <int CW, int CY, int CZ>
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
-template <int ND>
-__global__ void k_open_tile(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint64_t*, int, int, int,
-                            uint32_t*);
-template <int ND>
-struct OTileDims;
-template <>
-struct OTileDims<2> {
-    static constexpr int TZ = 1, TY = 64, TX = 64;
-};
-template <>
-struct OTileDims<3> {
-    static constexpr int TZ = 8, TY = 8, TX = 64;
-};
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>
 __global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint64_t*,

@@ -121,37 +121,19 @@ __global__ void __launch_bounds__(256) k_prep_edt_x(const BlockDesc* __restrict_
     if (lane == 0) left = -1;
     int right = __shfl_down(rn, 1);
     if (lane == 63) right = 0x3FFFFFFF;
-    // backward: distance to the nearest fg at or after x
-    int dist[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dist[k] = 0;
+    // backward over the lane's chunk: the distance to the nearest fg at or after x (0 exactly at
+    // the fg voxels), in place; then forward: the nearer of that and the last fg before x
     {
         int r = right;
-#pragma unroll
-        for (int k = 15; k >= 0; --k) {
-            const int x = x0 + k;
-            if (x < x1) {
-                if (sdist[x]) r = x;
-                dist[k] = (r >= 0x3FFFFFFF) ? 0x3FFFFFFF : r - x;
-            }
+        for (int x = x1 - 1; x >= x0; --x) {
+            if (sdist[x]) r = x;
+            sdist[x] = (r >= 0x3FFFFFFF) ? 0x3FFFFFFF : r - x;
         }
         int l = left;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int x = x0 + k;
-            if (x < x1) {
-                if (sdist[x]) l = x;
-                const int dl = (l < 0) ? 0x3FFFFFFF : x - l;
-                dist[k] = min(dist[k], dl);
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int x = x0 + k;
-        if (x < x1) {
-            const int d = dist[k];
+        for (int x = x0; x < x1; ++x) {
+            int d = sdist[x];
+            if (d == 0) l = x;
+            d = min(d, (l < 0) ? 0x3FFFFFFF : x - l);
             sdist[x] = (d >= 0x3FFFFFFF) ? (int)kInfD2 : pp.px2 * d * d;
         }
     }
@@ -415,6 +397,23 @@ template __global__ void k_input_minmax_t<double>(const BlockDesc*, BlockStat*);
 // hardware v_sqrt_f32 is not correctly rounded, so round a double sqrt to float and fix it
 // with exact arithmetic: the float r is correct iff mid(r-,r)^2 < n < mid(r,r+)^2 (midpoints
 // have <= 25 significant bits, so their squares are exact in double; no ties for n < 2^24).
+// correctly rounded sqrt of a float >= 0 (v_sqrt_f32, what __fsqrt_rn lowers to, is not):
+// the double sqrt rounded to float, corrected by the exact midpoint tests (the midpoint of two
+// floats has 25 significant bits, its square 50: exact in double)
+__device__ __forceinline__ float sqrt_rn_f(float x) {
+    float r = (float)__dsqrt_rn((double)x);
+    const double dx = (double)x;
+    const float up = __uint_as_float(__float_as_uint(r) + 1u);
+    const double mhi = 0.5 * ((double)r + (double)up);
+    if (mhi * mhi < dx) return up;
+    if (r > 0.0f) {
+        const float lo = __uint_as_float(__float_as_uint(r) - 1u);
+        const double mlo = 0.5 * ((double)r + (double)lo);
+        if (mlo * mlo > dx) return lo;
+    }
+    return r;
+}
+
 __device__ __forceinline__ float sqrt_rn_int(uint32_t n) {
     float r = (float)__dsqrt_rn((double)n);
     const double dn = (double)n;
@@ -787,7 +786,7 @@ __global__ void __launch_bounds__(256) k_edt_real_final(const BlockDesc* __restr
     const int64_t YX = (int64_t)B.Y * B.X;
     uint32_t mn = 0xFFFFFFFFu, mx = 0u;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
-        const float v = __fsqrt_rn((float)tmp[B.base + i]);
+        const float v = sqrt_rn_f((float)tmp[B.base + i]);
         dt[B.base + i] = v;
         const uint32_t o = ordf(v);
         mn = min(mn, o);

@@ -1141,194 +1141,6 @@ CTWS_LIST0_INST(1, 32, 2)
 #undef CTWS_FRONTIER_INST
 #undef CTWS_LIST0_INST
 
-// Closed open components, solved per tile in LDS (before the frontier relaxation).
-//
-// After the descent (or the regrow's initialisation) every voxel is either final or open, and
-// the open voxels of one connected component (flood neighbourhood) depend only on each other
-// and on the final keys around them: two different open components are never adjacent.  So a
-// component that lies inside a tile -- none of its voxels has an open neighbour outside the
-// tile -- is solved completely by relaxing it in LDS against its fixed boundary keys; no other
-// voxel can change its fixpoint.  One workgroup per tile: the open voxels get LDS slots, each
-// slot the minimum of its final neighbours' keys, then sweeps K = f(min(boundary, open
-// neighbours)) run to the (unique) fixpoint while a "crossing" taint spreads from the slots next
-// to an open voxel outside the tile through open-open adjacency.  Untainted slots are final:
-// their keys are stored and their bits leave `ofr`, the open bitmap the frontier relaxation
-// uses next (the verification keeps the full open bitmap).  Tainted components (crossing the
-// tile border), tiles with more than kOtCap open voxels and sweeps beyond kOtSweeps are left
-// to the frontier.  A second pass on a grid shifted by half a tile closes most components that
-// crossed a border of the first.  On config 3 the open voxels are mostly small basins of
-// seedless noise minima and the regrow's open voxels are the removed small segments.
-constexpr int kOtCap = 1024;     // LDS slots per tile
-constexpr int kOtSweeps = 2048;  // sweeps before the tile gives up (left to the frontier)
-
-template <int ND>
-struct OTile;
-template <>
-struct OTile<2> {
-    static constexpr int TZ = 1, TY = 64, TX = 64;
-};
-template <>
-struct OTile<3> {
-    static constexpr int TZ = 8, TY = 8, TX = 64;
-};
-
-template <int ND>
-__global__ void __launch_bounds__(256) k_open_tile(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                   const float* __restrict__ h, uint64_t* __restrict__ key,
-                                                   uint64_t* __restrict__ ofr, int sz, int sy, int sx,
-                                                   uint32_t* __restrict__ stats) {
-    using T = OTile<ND>;
-    constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, TN = TZ * TY * TX, NT = 256;
-    constexpr uint16_t kNone = 0xFFFF;
-    __shared__ uint16_t slot[TN];
-    __shared__ uint16_t pos[kOtCap];
-    __shared__ uint64_t K[kOtCap], Bm[kOtCap];
-    __shared__ uint32_t H[kOtCap];
-    __shared__ uint8_t taint[kOtCap];
-    __shared__ uint64_t rowdone[TZ * TY][2];  // solved bits of each tile row, per bitmap word touched
-    __shared__ int cnt;
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
-    // tile grid shifted by (sz, sy, sx): tile t covers [t * T - shift, (t + 1) * T - shift)
-    const int ntx = (B.X + sx + TX - 1) / TX, nty = (B.Y + sy + TY - 1) / TY, ntz = (B.Z + sz + TZ - 1) / TZ;
-    const int t = blockIdx.x;
-    if (t >= ntx * nty * ntz) return;
-    const int z0 = (t / (ntx * nty)) * TZ - sz, y0 = ((t / ntx) % nty) * TY - sy, x0 = (t % ntx) * TX - sx;
-    const int wpr = (B.X + 63) >> 6;
-    const gptr_t<uint64_t> ob = gbl(ofr + B.fbase);
-    const int64_t YX = (int64_t)B.Y * B.X;
-    auto open_at = [&](int z, int y, int x) -> bool {
-        return (ob[((int64_t)z * B.Y + y) * wpr + (x >> 6)] >> (x & 63)) & 1ull;
-    };
-    if (threadIdx.x == 0) cnt = 0;
-    for (int r = threadIdx.x; r < TZ * TY * 2; r += NT) rowdone[r >> 1][r & 1] = 0ull;
-    __syncthreads();
-    // ---- slots: the tile's open voxels (one row word load per lane group; x0 may be mid-word)
-    for (int c = threadIdx.x; c < TN; c += NT) {
-        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-        const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
-        bool op = false;
-        if (z >= 0 && z < B.Z && y >= 0 && y < B.Y && x >= 0 && x < B.X) op = open_at(z, y, x);
-        uint16_t s = kNone;
-        if (op) {
-            const int k = atomicAdd(&cnt, 1);
-            if (k < kOtCap) {
-                s = (uint16_t)k;
-                pos[k] = (uint16_t)c;
-            }
-        }
-        slot[c] = s;
-    }
-    __syncthreads();
-    const int n = cnt;
-    if (n == 0 || n > kOtCap) {
-        if (stats && threadIdx.x == 0 && n > kOtCap) atomicAdd(&stats[2], (uint32_t)n);
-        return;  // nothing open, or too many: the frontier relaxes this tile
-    }
-    // ---- per slot: height, minimum of the final neighbours' keys, crossing flag
-    for (int k = threadIdx.x; k < n; k += NT) {
-        const int c = pos[k];
-        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-        const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
-        const int64_t gi = (int64_t)z * YX + (int64_t)y * B.X + x;
-        uint64_t bm = kPackInf;
-        bool cross = false;
-        auto nb = [&](int dz, int dy, int dx, int ilz, int ily, int ilx) {
-            const int zz = z + dz, yy = y + dy, xx = x + dx;
-            if (zz < 0 || zz >= B.Z || yy < 0 || yy >= B.Y || xx < 0 || xx >= B.X) return;
-            const bool in_tile = ilz >= 0 && ilz < TZ && ily >= 0 && ily < TY && ilx >= 0 && ilx < TX;
-            if (in_tile && slot[(ilz * TY + ily) * TX + ilx] != kNone) return;  // open, in LDS
-            if (!in_tile && open_at(zz, yy, xx)) {
-                cross = true;  // an open neighbour outside the tile: the component crosses
-                return;
-            }
-            bm = min(bm, gbl(key)[B.base + gi + (int64_t)dz * YX + (int64_t)dy * B.X + dx]);
-        };
-        if (ND == 3) {
-            nb(-1, 0, 0, lz - 1, ly, lx);
-            nb(1, 0, 0, lz + 1, ly, lx);
-        }
-        nb(0, -1, 0, lz, ly - 1, lx);
-        nb(0, 1, 0, lz, ly + 1, lx);
-        nb(0, 0, -1, lz, ly, lx - 1);
-        nb(0, 0, 1, lz, ly, lx + 1);
-        Bm[k] = bm;
-        K[k] = kPackInf;
-        H[k] = ordf(gbl(h)[B.base + gi]);
-        taint[k] = cross ? 1 : 0;
-    }
-    __syncthreads();
-    // ---- sweeps to the fixpoint (in place; the fixpoint is unique, so the order is free)
-    int sweeps = 0;
-    for (; sweeps < kOtSweeps; ++sweeps) {
-        bool ch = false;
-        for (int k = threadIdx.x; k < n; k += NT) {
-            const int c = pos[k];
-            const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-            uint64_t m = Bm[k];
-            uint8_t tn = taint[k];
-            auto in = [&](int ilz, int ily, int ilx) {
-                if (ilz < 0 || ilz >= TZ || ily < 0 || ily >= TY || ilx < 0 || ilx >= TX) return;
-                const uint16_t s2 = slot[(ilz * TY + ily) * TX + ilx];
-                if (s2 == kNone) return;
-                m = min(m, K[s2]);
-                tn |= taint[s2];
-            };
-            if (ND == 3) {
-                in(lz - 1, ly, lx);
-                in(lz + 1, ly, lx);
-            }
-            in(lz, ly - 1, lx);
-            in(lz, ly + 1, lx);
-            in(lz, ly, lx - 1);
-            in(lz, ly, lx + 1);
-            const uint64_t nk = m == kPackInf ? kPackInf : f_packed(H[k], m);
-            if (nk != K[k]) {
-                K[k] = nk;
-                ch = true;
-            }
-            if (tn != taint[k]) {
-                taint[k] = tn;
-                ch = true;
-            }
-        }
-        if (!__syncthreads_or(ch)) break;
-    }
-    if (sweeps >= kOtSweeps) return;  // not converged: the frontier relaxes the tile
-    // ---- untainted slots are final
-    uint32_t solved = 0;
-    for (int k = threadIdx.x; k < n; k += NT) {
-        if (taint[k]) continue;
-        const int c = pos[k];
-        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-        const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
-        if (K[k] != kPackInf) key[B.base + (int64_t)z * YX + (int64_t)y * B.X + x] = K[k];
-        const int wsel = ((x >> 6) != ((x0 < 0 ? 0 : x0) >> 6)) ? 1 : 0;
-        atomicOr((unsigned long long*)&rowdone[lz * TY + ly][wsel], 1ull << (x & 63));
-        ++solved;
-    }
-    __syncthreads();
-    for (int r = threadIdx.x; r < TZ * TY * 2; r += NT) {
-        const uint64_t bits = rowdone[r >> 1][r & 1];
-        if (!bits) continue;
-        const int lz = (r >> 1) / TY, ly = (r >> 1) % TY;
-        const int xa = x0 < 0 ? 0 : x0;
-        const int xw = (xa >> 6) + (r & 1);
-        atomicAnd((unsigned long long*)&ofr[B.fbase + ((int64_t)(z0 + lz) * B.Y + (y0 + ly)) * wpr + xw], ~bits);
-    }
-    if (stats) {
-        solved = wg_reduce_u32(solved, OpAdd());
-        if (threadIdx.x == 0) {
-            atomicAdd(&stats[0], solved);
-            atomicAdd(&stats[1], (uint32_t)n);
-        }
-    }
-}
-template __global__ void k_open_tile<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint64_t*, int,
-                                        int, int, uint32_t*);
-template __global__ void k_open_tile<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, uint64_t*, int,
-                                        int, int, uint32_t*);
-
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                         const uint64_t* __restrict__ open, uint32_t* __restrict__ act,

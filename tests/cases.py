@@ -43,12 +43,12 @@ def make_cases():
     # rows wider than a wave's registers (X > 1024: generic x-pass and row kernels), and a 2-D
     # dt with Y^2 + X^2 >= 2^24 (vigra's float arithmetic: k_edt_real_* with T = float)
     xw1100 = _x(seed=15, shape=(8, 10, 1100))
-    xw4100 = _x(seed=16, shape=(2, 24, 4100))
+    xw4096 = _x(seed=16, shape=(2, 24, 4096))
     return {
         '3d_pitch_real': (dict(D3, pixel_pitch=(10.5, 1, 1)), dict(input=x)),
         '3d_pitch_frac': (dict(D3, pixel_pitch=(2.25, 0.75, 1.5)), dict(input=x)),
         '3d_pitch_bigdmax': (dict(D3, pixel_pitch=(600, 1, 1)), dict(input=x)),
-        '2d_wide4100_bigdmax': ({}, dict(input=xw4100)),
+        '2d_wide4096_bigdmax': ({}, dict(input=xw4096)),
         '3d_wide1100': (dict(D3), dict(input=xw1100)),
         '2d_sigma22': (dict(sigma_seeds=22.0), dict(input=x)),
         '3d_sparse_fg': (dict(D3), dict(input=xs)),
