@@ -147,9 +147,11 @@ struct ctws_handle {
     // 3-D batches with a mask default to 1x32x2 instead of 1x8x8: a masked region is one flat
     // plateau (fin = 1) that the flood crosses hop by hop, and wider bricks in y cut the launches
     // (config 5: 104 -> 72 ms of relaxation, 156 -> 82 launches; unmasked config 4: 33 vs 41 ms)
-    int fchunk2[3] = {1, 64, 1};
-    int fchunk3[3] = {1, 8, 8};
-    int fchunk3_masked[3] = {1, 32, 2};
+    // (r03) bricks of k_frontier_lds (keys staged in LDS) by default; CTWS_FRONTIER_CHUNK2D/3D
+    // select any brick of frontier_chunk_kind, the 64-word ones run k_frontier
+    int fchunk2[3] = {1, 32, 1};
+    int fchunk3[3] = {1, 4, 4};
+    int fchunk3_masked[3] = {1, 4, 4};
     int fchunk3_env = 0;  // CTWS_FRONTIER_CHUNK3D given: used for every 3-D batch
     int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
     int cur_max[3] = {0, 0, 0};  // largest outer block extents (Z, Y, X) of the current batch
@@ -278,11 +280,11 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(front0, front);
         ALLOC(front1, front);
         ALLOC(fopen, front);
-        ALLOC(fchunk0, front / 64 + 1);
-        ALLOC(fchunk1, front / 64 + 1);
-        ALLOC(wl0, front / 64 + 1);
-        ALLOC(wl1, front / 64 + 1);
-        ALLOC(qgen, front / 64 + 1);
+        ALLOC(fchunk0, (front >> kChunkShift) + 1);
+        ALLOC(fchunk1, (front >> kChunkShift) + 1);
+        ALLOC(wl0, (front >> kChunkShift) + 1);
+        ALLOC(wl1, (front >> kChunkShift) + 1);
+        ALLOC(qgen, (front >> kChunkShift) + 1);
         w.cap_front = front;
     }
     if (!w.fflags) ALLOC(fflags, kFrontierBatch);
@@ -534,9 +536,11 @@ int cdiv(int a, int b) { return (a + b - 1) / b; }
 // tile extents of k_flood_packed (PTile) and k_flood (FloodTile)
 // frontier chunk bricks instantiated in k_flood.hip (CTWS_FRONTIER_SHAPES below): index or -1
 int frontier_chunk_kind(int nd, int cw, int cy, int cz) {
-    static const int shapes[10][4] = {{2, 1, 64, 1}, {2, 2, 32, 1}, {2, 4, 16, 1}, {2, 8, 8, 1}, {3, 1, 8, 8},
-                                      {3, 2, 8, 4},  {3, 1, 16, 4}, {3, 4, 4, 4},  {3, 8, 8, 1}, {3, 1, 32, 2}};
-    for (int k = 0; k < 10; ++k)
+    // kinds 0-9: k_frontier (64-word bricks); 10-13: k_frontier_lds (one-word-wide bricks staged in LDS)
+    static const int shapes[14][4] = {{2, 1, 64, 1}, {2, 2, 32, 1}, {2, 4, 16, 1}, {2, 8, 8, 1}, {3, 1, 8, 8},
+                                      {3, 2, 8, 4},  {3, 1, 16, 4}, {3, 4, 4, 4},  {3, 8, 8, 1}, {3, 1, 32, 2},
+                                      {2, 1, 32, 1}, {2, 1, 16, 1}, {3, 1, 8, 4},  {3, 1, 4, 4}};
+    for (int k = 0; k < 14; ++k)
         if (shapes[k][0] == nd && shapes[k][1] == cw && shapes[k][2] == cy && shapes[k][3] == cz) return k;
     return -1;
 }
@@ -620,7 +624,7 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
                  uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
     Workspace& w = h->ws;
-    const int64_t nch = TF / 64 + 1;
+    const int64_t nch = (TF >> kChunkShift) + 1;
     uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
     uint32_t* gen[2] = {w.fchunk0, w.fchunk1};  // iteration it writes gen[it & 1], reads gen[(it + 1) & 1]
     uint32_t* wl[2] = {w.wl0, w.wl1};
@@ -636,9 +640,14 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
 #define CTWS_FRONTIER_SHAPES(X) \
     X(0, 2, 1, 64, 1) X(1, 2, 2, 32, 1) X(2, 2, 4, 16, 1) X(3, 2, 8, 8, 1) X(4, 3, 1, 8, 8) X(5, 3, 2, 8, 4) \
     X(6, 3, 1, 16, 4) X(7, 3, 4, 4, 4) X(8, 3, 8, 8, 1) X(9, 3, 1, 32, 2)
+#define CTWS_LDS_SHAPES(X) X(10, 2, 1, 32, 1) X(11, 2, 1, 16, 1) X(12, 3, 1, 8, 4) X(13, 3, 1, 4, 4)
 #define CTWS_LIST0(K, ND, CW, CY, CZ) \
     case K: k_frontier_list0<CW, CY, CZ><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt); break;
-    switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_LIST0) default: h->err = "bad frontier chunk"; return CTWS_EINVAL; }
+    switch (fkind) {
+        CTWS_FRONTIER_SHAPES(CTWS_LIST0)
+        CTWS_LDS_SHAPES(CTWS_LIST0)
+        default: h->err = "bad frontier chunk"; return CTWS_EINVAL;
+    }
 #undef CTWS_LIST0
     LAUNCHCHK();
     // one wave per list entry; the largest list is every chunk of the batch
@@ -663,8 +672,19 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             h->frontier_reps);                                                                                      \
         break;
-            switch (fkind) { CTWS_FRONTIER_SHAPES(CTWS_FRONTIER) }
+#define CTWS_FRONTIER_LDS(K, ND, CW, CY, CZ)                                                                        \
+    case K:                                                                                                         \
+        k_frontier_lds<ND, CY, CZ><<<fg, 256, 0, h->stream>>>(                                                      \
+            w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
+            wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
+            h->frontier_reps);                                                                                      \
+        break;
+            switch (fkind) {
+                CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
+                CTWS_LDS_SHAPES(CTWS_FRONTIER_LDS)
+            }
 #undef CTWS_FRONTIER
+#undef CTWS_FRONTIER_LDS
             if (h->trace) hipEventRecord(tev[k + 1], h->stream);
         }
         LAUNCHCHK();
@@ -690,6 +710,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
         }
     }
 #undef CTWS_FRONTIER_SHAPES
+#undef CTWS_LDS_SHAPES
     *iters_out += fiters;
     if (!converged) {
         int TZ, TY, TX;
@@ -860,7 +881,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             const int* fc = h->fc_cur;
             const int64_t wpr = (d.X + 63) / 64;
             const int64_t nch = ((wpr + fc[0] - 1) / fc[0]) * ((d.Y + fc[1] - 1) / fc[1]) * ((d.Z + fc[2] - 1) / fc[2]);
-            TF += std::max((((int64_t)d.Z * d.Y + 63) / 64) * 64 * wpr, nch * 64);
+            TF += std::max((((int64_t)d.Z * d.Y + 63) / 64) * 64 * wpr, nch << kChunkShift);
         }
         T += d.N;
         TI += d.NI;
