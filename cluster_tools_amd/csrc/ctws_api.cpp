@@ -147,11 +147,9 @@ struct ctws_handle {
     // 3-D batches with a mask default to 1x32x2 instead of 1x8x8: a masked region is one flat
     // plateau (fin = 1) that the flood crosses hop by hop, and wider bricks in y cut the launches
     // (config 5: 104 -> 72 ms of relaxation, 156 -> 82 launches; unmasked config 4: 33 vs 41 ms)
-    // (r03) bricks of k_frontier_lds (keys staged in LDS) by default; CTWS_FRONTIER_CHUNK2D/3D
-    // select any brick of frontier_chunk_kind, the 64-word ones run k_frontier
-    int fchunk2[3] = {1, 32, 1};
-    int fchunk3[3] = {1, 4, 4};
-    int fchunk3_masked[3] = {1, 4, 4};
+    int fchunk2[3] = {1, 64, 1};
+    int fchunk3[3] = {1, 8, 8};
+    int fchunk3_masked[3] = {1, 32, 2};
     int fchunk3_env = 0;  // CTWS_FRONTIER_CHUNK3D given: used for every 3-D batch
     int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
     int cur_max[3] = {0, 0, 0};  // largest outer block extents (Z, Y, X) of the current batch
@@ -536,11 +534,9 @@ int cdiv(int a, int b) { return (a + b - 1) / b; }
 // tile extents of k_flood_packed (PTile) and k_flood (FloodTile)
 // frontier chunk bricks instantiated in k_flood.hip (CTWS_FRONTIER_SHAPES below): index or -1
 int frontier_chunk_kind(int nd, int cw, int cy, int cz) {
-    // kinds 0-9: k_frontier (64-word bricks); 10-13: k_frontier_lds (one-word-wide bricks staged in LDS)
-    static const int shapes[14][4] = {{2, 1, 64, 1}, {2, 2, 32, 1}, {2, 4, 16, 1}, {2, 8, 8, 1}, {3, 1, 8, 8},
-                                      {3, 2, 8, 4},  {3, 1, 16, 4}, {3, 4, 4, 4},  {3, 8, 8, 1}, {3, 1, 32, 2},
-                                      {2, 1, 32, 1}, {2, 1, 16, 1}, {3, 1, 8, 4},  {3, 1, 4, 4}};
-    for (int k = 0; k < 14; ++k)
+    static const int shapes[10][4] = {{2, 1, 64, 1}, {2, 2, 32, 1}, {2, 4, 16, 1}, {2, 8, 8, 1}, {3, 1, 8, 8},
+                                      {3, 2, 8, 4},  {3, 1, 16, 4}, {3, 4, 4, 4},  {3, 8, 8, 1}, {3, 1, 32, 2}};
+    for (int k = 0; k < 10; ++k)
         if (shapes[k][0] == nd && shapes[k][1] == cw && shapes[k][2] == cy && shapes[k][3] == cz) return k;
     return -1;
 }
@@ -640,12 +636,10 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
 #define CTWS_FRONTIER_SHAPES(X) \
     X(0, 2, 1, 64, 1) X(1, 2, 2, 32, 1) X(2, 2, 4, 16, 1) X(3, 2, 8, 8, 1) X(4, 3, 1, 8, 8) X(5, 3, 2, 8, 4) \
     X(6, 3, 1, 16, 4) X(7, 3, 4, 4, 4) X(8, 3, 8, 8, 1) X(9, 3, 1, 32, 2)
-#define CTWS_LDS_SHAPES(X) X(10, 2, 1, 32, 1) X(11, 2, 1, 16, 1) X(12, 3, 1, 8, 4) X(13, 3, 1, 4, 4)
 #define CTWS_LIST0(K, ND, CW, CY, CZ) \
     case K: k_frontier_list0<CW, CY, CZ><<<lg, 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, wl[0], w.wlcnt); break;
     switch (fkind) {
         CTWS_FRONTIER_SHAPES(CTWS_LIST0)
-        CTWS_LDS_SHAPES(CTWS_LIST0)
         default: h->err = "bad frontier chunk"; return CTWS_EINVAL;
     }
 #undef CTWS_LIST0
@@ -672,19 +666,10 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             h->frontier_reps);                                                                                      \
         break;
-#define CTWS_FRONTIER_LDS(K, ND, CW, CY, CZ)                                                                        \
-    case K:                                                                                                         \
-        k_frontier_lds<ND, CY, CZ><<<fg, 256, 0, h->stream>>>(                                                      \
-            w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
-            wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
-            h->frontier_reps);                                                                                      \
-        break;
             switch (fkind) {
                 CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
-                CTWS_LDS_SHAPES(CTWS_FRONTIER_LDS)
             }
 #undef CTWS_FRONTIER
-#undef CTWS_FRONTIER_LDS
             if (h->trace) hipEventRecord(tev[k + 1], h->stream);
         }
         LAUNCHCHK();
@@ -710,7 +695,6 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
         }
     }
 #undef CTWS_FRONTIER_SHAPES
-#undef CTWS_LDS_SHAPES
     *iters_out += fiters;
     if (!converged) {
         int TZ, TY, TX;

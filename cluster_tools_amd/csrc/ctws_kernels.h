@@ -165,13 +165,9 @@ __global__ void k_fs_output(const BlockDesc*, BlockStat*, const uint32_t*, const
                             const uint32_t*, int);
 hipError_t fs_segmented_sort(void* tmp, size_t& bytes, const uint32_t* in, uint32_t* out, int n, int nseg,
                              const int* beg, const int* end, hipStream_t stream);
-template <int ND, int CY, int CZ>
-__global__ void k_frontier_lds(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                               const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
-                               const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 // per-chunk arrays (generations, queued marks) are indexed at fbase >> kChunkShift: a block's
-// frontier words hold at least 2^kChunkShift words per chunk of any brick (32 or 64 words)
-constexpr int kChunkShift = 5;
+// frontier words hold at least 2^kChunkShift words per chunk (every brick is 64 words)
+constexpr int kChunkShift = 6;
 template <int CW, int CY, int CZ>
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);

@@ -1110,267 +1110,6 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
     }
 }
-// The frontier iteration with the chunk's keys staged in the wave's LDS (k_frontier_lds).
-//
-// k_frontier gathers every neighbour key from global memory on every local sweep; with
-// thousands of chunks in flight their keys do not stay in L2, so each sweep re-reads them from
-// HBM (r02 counters: 86 GB read per step on config 3 against 15 GB of algorithmic flood bytes).
-// Here a wave loads its chunk's keys with a one-voxel halo into LDS once (one coalesced 512-byte
-// row per load), runs the local sweeps on LDS, and writes back only the keys that changed.  A
-// chunk is one x word wide (64 voxels) and CY x CZ rows (WPC = CY * CZ <= 64 words, one per
-// lane), so a wave's LDS stays small enough for 8 waves per CU.  The halo keys are a snapshot:
-// a neighbour's later change on the shared face queues this chunk again through the changed
-// bitmaps and generations, exactly as in k_frontier (whose bookkeeping this kernel shares).
-// Heights are read from global memory (read-only, one 4-byte load per visit).
-template <int ND, int CY, int CZ>
-struct LdsChunk {
-    static constexpr int WPC = CY * CZ;  // words (rows) per chunk
-    static constexpr int ZH = ND == 3 ? 1 : 0;
-    static constexpr int HX = 66, HY = CY + 2, HZ = CZ + 2 * ZH;
-    static constexpr int HN = HX * HY * HZ;
-};
-
-template <int ND, int CY, int CZ>
-__global__ void __launch_bounds__(256) k_frontier_lds(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                      const float* __restrict__ h, uint64_t* __restrict__ key,
-                                                      const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
-                                                      uint64_t* __restrict__ cnext, const uint32_t* __restrict__ gprev,
-                                                      uint32_t* __restrict__ gnext, int it, const uint32_t* __restrict__ list,
-                                                      const uint32_t* __restrict__ cnt, uint32_t* __restrict__ list_next,
-                                                      uint32_t* __restrict__ cnt_next, uint32_t* __restrict__ qgen,
-                                                      uint32_t* __restrict__ nvisit, int reps) {
-    static_assert(ND == 3 || CZ == 1, "2-D ws: slices are independent, chunks are one slice deep");
-    using LC = LdsChunk<ND, CY, CZ>;
-    constexpr int WPC = LC::WPC, HX = LC::HX, HY = LC::HY, ZH = LC::ZH, HN = LC::HN;
-    static_assert(WPC <= 64 && (64 % WPC) == 0, "one word per lane");
-    __shared__ uint64_t skey[kFrontierWaves][HN];
-    __shared__ uint64_t schg[kFrontierWaves][64];
-    __shared__ uint64_t sfw[kFrontierWaves][64];
-    __shared__ int spre[kFrontierWaves][64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int ly = lane % CY, lz = lane / CY;  // the lane's word (row) in the chunk; lane < WPC
-    const bool lok = lane < WPC;
-    const uint32_t n_entries = *cnt;
-    const uint32_t prev_gen = (uint32_t)it;
-    const uint32_t wg = (uint32_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
-    uint64_t* K = skey[wv];
-    for (uint32_t e0 = wg * kFrontierWaves + wv; e0 < n_entries; e0 += gridDim.x * kFrontierWaves) {
-        const uint32_t ent = list[e0];
-        const int bi = (int)(ent >> kWlChunkBits);
-        const int ch0 = (int)(ent & ((1u << kWlChunkBits) - 1u));
-        const BlockDesc& B = D[bi];
-        const int wpr = (B.X + 63) >> 6;
-        const int ncx = wpr, ncy = (B.Y + CY - 1) / CY, ncz = (B.Z + CZ - 1) / CZ;
-        const int cplane = ncx * ncy;
-        const int ws = B.Y * wpr;
-        const uint64_t* cp = cprev + B.fbase;
-        const uint64_t* op = open + B.fbase;
-        uint64_t* cn = cnext + B.fbase;
-        const gptr_t<uint64_t> kb = gbl(key + B.base);
-        const gptr_t<float> hb = gbl(h + B.base);
-        const uint32_t* gp = gprev + (B.fbase >> kChunkShift);
-        uint32_t* gn = gnext + (B.fbase >> kChunkShift);
-        uint32_t* qg = qgen + (B.fbase >> kChunkShift);
-        const int cx = ch0 % ncx, cy = (ch0 / ncx) % ncy, cz = ch0 / cplane;
-        const int xw = cx, yy = cy * CY + ly, zz = cz * CZ + lz;
-        const bool wok = lok && yy < B.Y && zz < B.Z;
-        const int wc = wok ? (zz * B.Y + yy) * wpr + xw : 0;
-        // ---- the frontier words (as k_frontier)
-        constexpr int NW = ND == 3 ? 7 : 5;
-        int wi[NW], ci[NW];
-        bool ok[NW];
-        wi[0] = wc;
-        ci[0] = ch0;
-        ok[0] = wok;
-        wi[1] = wc - 1;
-        ci[1] = ch0 - 1;
-        ok[1] = wok && xw > 0;
-        wi[2] = wc + 1;
-        ci[2] = ch0 + 1;
-        ok[2] = wok && xw + 1 < wpr;
-        wi[3] = wc - wpr;
-        ci[3] = ly == 0 ? ch0 - ncx : ch0;
-        ok[3] = wok && yy > 0;
-        wi[4] = wc + wpr;
-        ci[4] = ly == CY - 1 ? ch0 + ncx : ch0;
-        ok[4] = wok && yy + 1 < B.Y;
-        if (ND == 3) {
-            wi[5] = wc - ws;
-            ci[5] = lz == 0 ? ch0 - cplane : ch0;
-            ok[5] = wok && zz > 0;
-            wi[6] = wc + ws;
-            ci[6] = lz == CZ - 1 ? ch0 + cplane : ch0;
-            ok[6] = wok && zz + 1 < B.Z;
-        }
-        uint32_t gv[NW];
-        uint64_t cv[NW];
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            gv[k] = gbl(gp)[ok[k] ? ci[k] : ch0];
-            cv[k] = gbl(cp)[ok[k] ? wi[k] : wc];
-        }
-        const uint64_t opw = wok ? gbl(op)[wc] : 0ull;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            const bool own = ci[k] == ch0;
-            const bool valid = own ? gv[k] == prev_gen : (gv[k] & ~kGenConv) == prev_gen;
-            cv[k] = (ok[k] && valid) ? cv[k] : 0ull;
-        }
-        uint64_t f = (cv[0] << 1) | (cv[0] >> 1) | (cv[1] >> 63) | (cv[2] << 63) | cv[3] | cv[4];
-        if (ND == 3) f |= cv[5] | cv[6];
-        f &= opw;
-        if (__ballot(f != 0ull) == 0ull) continue;  // nothing to relax in this chunk
-        // ---- stage the chunk's keys and their one-voxel halo: row r = (hz, hy), lane = x + 1;
-        // lanes 0 / 1 also fetch the x - 1 / x + 64 halo ends
-        const int x0 = xw * 64;
-        const int zb = cz * CZ - ZH, yb = cy * CY - 1;
-        {
-            constexpr int NR = HY * LC::HZ;
-            constexpr int BATCH = 8;
-#pragma unroll 1
-            for (int r0 = 0; r0 < NR; r0 += BATCH) {
-                uint64_t v[BATCH], e[BATCH];
-#pragma unroll
-                for (int q = 0; q < BATCH; ++q) {
-                    const int r = r0 + q;
-                    const int z = zb + r / HY, y = yb + r % HY;
-                    const bool rok = r < NR && z >= 0 && z < B.Z && y >= 0 && y < B.Y;
-                    const int x = x0 + lane;
-                    const int xe = lane == 0 ? x0 - 1 : x0 + 64;
-                    const int64_t rowb = ((int64_t)(rok ? z : 0) * B.Y + (rok ? y : 0)) * B.X;
-                    v[q] = (rok && x < B.X) ? kb[rowb + x] : kPackInf;
-                    e[q] = (rok && lane < 2 && xe >= 0 && xe < B.X) ? kb[rowb + xe] : kPackInf;
-                }
-#pragma unroll
-                for (int q = 0; q < BATCH; ++q) {
-                    const int r = r0 + q;
-                    if (r < NR) {
-                        K[r * HX + lane + 1] = v[q];
-                        if (lane == 0) K[r * HX] = e[q];
-                        if (lane == 1) K[r * HX + 65] = e[q];
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint64_t acc = 0ull;
-        bool conv = true;
-        uint32_t vis = 0;
-        for (int rep = 0;; ++rep) {
-            const int cnt_bits = __popcll(f);
-            int incl = cnt_bits;
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t = __shfl_up(incl, o);
-                if (lane >= o) incl += t;
-            }
-            const int total = __shfl(incl, 63);
-            if (total == 0) break;
-            vis += (uint32_t)total;
-            schg[wv][lane] = 0ull;
-            sfw[wv][lane] = f;
-            spre[wv][lane] = incl - cnt_bits;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int t0 = 0; t0 < total; t0 += 64) {
-                const int e = t0 + lane;
-                if (e < total) {
-                    int j = 0;
-#pragma unroll
-                    for (int step = 32; step > 0; step >>= 1)
-                        if (spre[wv][j + step] <= e) j += step;
-                    const int b = kth_set_bit(sfw[wv][j], e - spre[wv][j]);
-                    const int jy = j % CY, jz = j / CY;
-                    const int c = ((jz + ZH) * HY + (jy + 1)) * HX + b + 1;
-                    uint64_t m = min(min(K[c - 1], K[c + 1]), min(K[c - HX], K[c + HX]));
-                    if (ND == 3) m = min(m, min(K[c - HX * HY], K[c + HX * HY]));
-                    if (m != kPackInf) {
-                        const int z = cz * CZ + jz, y = cy * CY + jy;
-                        const float hv = hb[((int64_t)z * B.Y + y) * B.X + x0 + b];
-                        const uint64_t k = f_packed(ordf(hv), m);
-                        if (k != K[c]) {
-                            K[c] = k;
-                            atomicOr((unsigned long long*)&schg[wv][j], 1ull << b);
-                        }
-                    }
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint64_t c = schg[wv][lane];
-            acc |= c;
-            if (__ballot(c != 0ull) == 0ull) break;
-            if (rep + 1 >= reps) {
-                conv = false;
-                break;
-            }
-            // the in-chunk neighbours of this sweep's changes (rows: lanes; x: bit shifts)
-            f = (c << 1) | (c >> 1);
-            const uint64_t cym = __shfl(c, ly > 0 ? lane - 1 : lane);
-            const uint64_t cyp = __shfl(c, ly < CY - 1 ? lane + 1 : lane);
-            if (ly > 0) f |= cym;
-            if (ly < CY - 1 && yy + 1 < B.Y) f |= cyp;
-            if (ND == 3 && CZ > 1) {
-                const uint64_t czm = __shfl(c, lz > 0 ? lane - CY : lane);
-                const uint64_t czp = __shfl(c, lz < CZ - 1 ? lane + CY : lane);
-                if (lz > 0) f |= czm;
-                if (lz < CZ - 1 && zz + 1 < B.Z) f |= czp;
-            }
-            f &= opw;
-        }
-        if (nvisit && lane == 0 && vis) atomicAdd(&nvisit[bi], vis);
-        if (__ballot(acc != 0ull) == 0ull) continue;
-        // ---- write back the changed keys, one coalesced row per word
-#pragma unroll 1
-        for (int j = 0; j < WPC; ++j) {
-            const uint64_t a = __shfl(acc, j);
-            if (!a) continue;
-            const int jy = j % CY, jz = j / CY;
-            if ((a >> lane) & 1ull)
-                key[B.base + ((int64_t)(cz * CZ + jz) * B.Y + (cy * CY + jy)) * B.X + x0 + lane] =
-                    K[((jz + ZH) * HY + (jy + 1)) * HX + lane + 1];
-        }
-        // ---- publish (as k_frontier): changed words, generation, the chunks to queue
-        if (wok) cn[wc] = acc;
-        if (lane == 0) gn[ch0] = ((uint32_t)it + 1u) | (conv ? kGenConv : 0u);
-        const bool fxm = __ballot(lok && (acc & 1ull)) != 0ull;
-        const bool fxp = __ballot(lok && (acc >> 63)) != 0ull;
-        const bool fym = __ballot(lok && ly == 0 && acc != 0ull) != 0ull;
-        const bool fyp = __ballot(lok && ly == CY - 1 && acc != 0ull) != 0ull;
-        const bool fzm = ND == 3 && __ballot(lok && lz == 0 && acc != 0ull) != 0ull;
-        const bool fzp = ND == 3 && __ballot(lok && lz == CZ - 1 && acc != 0ull) != 0ull;
-        int cand = -1;
-        if (lane == 0 && !conv) cand = ch0;
-        else if (lane == 1 && fxm && cx > 0) cand = ch0 - 1;
-        else if (lane == 2 && fxp && cx + 1 < ncx) cand = ch0 + 1;
-        else if (lane == 3 && fym && cy > 0) cand = ch0 - ncx;
-        else if (lane == 4 && fyp && cy + 1 < ncy) cand = ch0 + ncx;
-        else if (lane == 5 && fzm && cz > 0) cand = ch0 - cplane;
-        else if (lane == 6 && fzp && cz + 1 < ncz) cand = ch0 + cplane;
-        bool push = false;
-        if (cand >= 0) push = atomicMax(&qg[cand], (uint32_t)it + 1u) < (uint32_t)it + 1u;
-        const uint64_t pm = __ballot(push);
-        uint32_t base = 0;
-        if (lane == 0 && pm) base = atomicAdd(cnt_next, (uint32_t)__popcll(pm));
-        base = (uint32_t)__shfl((int)base, 0);
-        if (push)
-            list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
-    }
-}
-#define CTWS_FRONTIER_LDS_INST(ND, CY, CZ)                                                                           \
-    template __global__ void k_frontier_lds<ND, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
-                                                        const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,  \
-                                                        uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*,   \
-                                                        uint32_t*, uint32_t*, uint32_t*, int);
-CTWS_FRONTIER_LDS_INST(2, 32, 1)
-CTWS_FRONTIER_LDS_INST(2, 16, 1)
-CTWS_FRONTIER_LDS_INST(3, 8, 4)
-CTWS_FRONTIER_LDS_INST(3, 4, 4)
-#undef CTWS_FRONTIER_LDS_INST
-
 // chunk bricks: 2-D ws (CZ = 1) and 3-D; CTWS_FRONTIER_CHUNK selects one (frontier_chunk_dims)
 #define CTWS_FRONTIER_INST(ND, CW, CY, CZ)                                                                           \
     template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
@@ -1399,11 +1138,6 @@ CTWS_LIST0_INST(2, 8, 4)
 CTWS_LIST0_INST(1, 16, 4)
 CTWS_LIST0_INST(4, 4, 4)
 CTWS_LIST0_INST(1, 32, 2)
-CTWS_LIST0_INST(1, 32, 1)
-CTWS_LIST0_INST(1, 16, 1)
-CTWS_LIST0_INST(1, 8, 4)
-CTWS_LIST0_INST(1, 4, 4)
-CTWS_LIST0_INST(1, 16, 2)
 #undef CTWS_FRONTIER_INST
 #undef CTWS_LIST0_INST
 

@@ -1,8 +1,7 @@
 """The frontier relaxation's schedule knobs change the order of work, never the result.
 
 The flood's fixpoint (K = f(min of the neighbours' keys), k_flood.hip) is unique, so every
-chunk brick (CTWS_FRONTIER_CHUNK2D / _3D; 64-word bricks run k_frontier, one-word-wide
-bricks the LDS-staged k_frontier_lds) and a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
+chunk brick (CTWS_FRONTIER_CHUNK2D / _3D) and a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
 non-converged re-queue path runs) must reproduce the oracle's flood model bit for bit on every
 parity case, as the default schedule does (test_gpu_parity.py::test_flood_matches_model_exactly).
 The knobs are read when a handle is opened.
@@ -23,11 +22,7 @@ VARIANTS = {
     'bricks_b': {'CTWS_FRONTIER_CHUNK2D': '8x8x1', 'CTWS_FRONTIER_CHUNK3D': '4x4x4'},
     'bricks_c': {'CTWS_FRONTIER_CHUNK2D': '2x32x1', 'CTWS_FRONTIER_CHUNK3D': '1x16x4'},
     'rows_3d_one_sweep': {'CTWS_FRONTIER_CHUNK3D': '8x8x1', 'CTWS_FRONTIER_REPS': '1'},
-    # k_frontier (keys gathered from global memory) instead of the default LDS-staged bricks
-    'global_64': {'CTWS_FRONTIER_CHUNK2D': '1x64x1', 'CTWS_FRONTIER_CHUNK3D': '1x8x8'},
-    # other LDS-staged bricks, and one sweep per launch on them
-    'lds_b': {'CTWS_FRONTIER_CHUNK2D': '1x16x1', 'CTWS_FRONTIER_CHUNK3D': '1x8x4'},
-    'lds_one_sweep': {'CTWS_FRONTIER_REPS': '1'},
+    'one_sweep': {'CTWS_FRONTIER_REPS': '1'},
 }
 
 
