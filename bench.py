@@ -116,26 +116,37 @@ def blocking(shape, block_shape, halo):
     return out
 
 
-def volume_geometry(cfg, rank=0, world=1):
-    """The rank's share of the workload (weak scaling: the per-GPU work is fixed).
+def volume_geometry(cfg, rank=0, world=1, scaling='weak'):
+    """The rank's share of the workload.
 
-    Every rank owns a z-slab of cfg['shape'] of one volume: config 5's slabs are those of the
-    2048^3 volume (slab cfg['slab'] on one GPU, slab `rank` on N); the other configs stack N
-    slabs into an (N * Z, Y, X) volume of the same synthetic map.  A rank processes the
-    blocks of the volume's global block grid whose inner block lies in its slab, with their
-    full halos (the input of a halo that reaches into a neighbouring slab is generated from
-    the same map), and global block ids.  Returns full (volume shape), z0 (slab start),
+    weak (the per-GPU work is fixed): every rank owns a z-slab of cfg['shape'] of one volume:
+    config 5's slabs are those of the 2048^3 volume (slab cfg['slab'] on one GPU, slab `rank`
+    on N); the other configs stack N slabs into an (N * Z, Y, X) volume of the same map.
+    strong (the volume is fixed): the config's whole volume (cfg['full_shape'] or
+    cfg['shape']: config 4's 1024^3, config 5's 2048^3) is cut into N z-slabs along the block
+    grid, each rank a contiguous range of block rows (SURVEY.md §8(e) partitioning).
+    A rank processes the blocks of the volume's global block grid whose inner block lies in
+    its slab, with their full halos (a halo that reaches into a neighbouring slab is generated
+    from the same map), and global block ids.  Returns full (volume shape), z0 (slab start),
     g0 / gshape (the generated region: slab + z halos) and the blocks with bounding boxes in
     region coordinates.
     """
     Z, Y, X = cfg['shape']
-    if 'full_shape' in cfg:
-        full = tuple(cfg['full_shape'])
-        slab = cfg['slab'] if world == 1 else rank % (full[0] // Z)
+    if scaling == 'strong':
+        full = tuple(cfg.get('full_shape', cfg['shape']))
+        bz = cfg['block_shape'][0]
+        nzb = (full[0] + bz - 1) // bz
+        r0, r1 = nzb * rank // world, nzb * (rank + 1) // world
+        z0, z1 = r0 * bz, min(full[0], r1 * bz)
     else:
-        full = (Z * world, Y, X)
-        slab = rank
-    z0 = slab * Z
+        if 'full_shape' in cfg:
+            full = tuple(cfg['full_shape'])
+            slab = cfg['slab'] if world == 1 else rank % (full[0] // Z)
+        else:
+            full = (Z * world, Y, X)
+            slab = rank
+        z0, z1 = slab * Z, slab * Z + Z
+    Z = z1 - z0
     hz = cfg['halo'][0]
     g0, g1 = max(0, z0 - hz), min(full[0], z0 + Z + hz)
     blocks = []
@@ -293,6 +304,9 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe-inclusive) pass')
     ap.add_argument('--cpu-cores', type=int, default=0, help='cap on the CPU baseline jobs (0: usable cores)')
+    ap.add_argument('--scaling', choices=('weak', 'strong'), default='weak',
+                    help='weak: every rank runs the config\'s single-GPU workload (default); strong: the '
+                         'config\'s whole volume (config 4: 1024^3, config 5: 2048^3) in z-slabs over the ranks')
     ap.add_argument('--streams', type=int, default=3,
                     help='library handles (one HIP stream each) per GPU, driven from host threads; '
                          'the blocks are split between them so their launch-bound phases overlap')
@@ -320,7 +334,7 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
 
     shape = tuple(cfg['shape'])
-    geo = volume_geometry(cfg, rank, world)
+    geo = volume_geometry(cfg, rank, world, args.scaling)
     full = geo['full']
     origin = (geo['g0'], 0, 0)
     gen = dict(seed=cfg['seed'], device=dev, dtype=cfg.get('dtype', 'float32'), pitch=cfg.get('pitch', (24, 24, 24)),
@@ -375,8 +389,6 @@ def main():
     handles = [ctws.Handle(local_rank) for _ in range(nstreams)]
     pool = ThreadPoolExecutor(nstreams) if nstreams > 1 else None
     nblocks = len(blocks)
-    counts = torch.zeros(nblocks, dtype=torch.int64, device=dev)
-    gathered = torch.zeros(nblocks * world, dtype=torch.int64, device=dev)
     stage_ms = {}
     offsets = {}
 
@@ -411,12 +423,8 @@ def main():
         if not two_pass:
             # compact global id offsets: exclusive scan of the per-block distinct-id counts of
             # all ranks (relabel/find_labeling.py:104-116 over RCCL instead of .npy files)
-            counts.copy_(torch.tensor([k for _, _, k in res], dtype=torch.int64))
-            if world > 1:
-                dist.all_gather_into_tensor(gathered, counts)
-            else:
-                gathered.copy_(counts)
-            offsets['scan'] = torch.cumsum(gathered, 0) - gathered
+            allc = sharded.gather_counts([k for _, _, k in res], device=dev)
+            offsets['scan'], offsets['n_ids'] = sharded.compact_offsets(allc)
         return res
 
     progress('inputs staged: %d blocks, %d outer voxels' % (len(blocks), outer_vox))
@@ -449,7 +457,12 @@ def main():
     else:
         stage_1 = stage_ms
 
-    total_vox = inner_vox * world * args.steps
+    inner_all = inner_vox
+    if world > 1:
+        t = torch.tensor([inner_vox], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        inner_all = int(t.item())
+    total_vox = inner_all * args.steps
     value = total_vox / dt / 1e9
     ms_per_step = dt / args.steps * 1e3
 
@@ -524,13 +537,16 @@ def main():
             'metric': 'Gvoxel/s DT-watershed (node, 1/2/4/8 GPU) + % HBM roofline; VI vs ref',
             'value': round(value, 4), 'unit': 'Gvoxel/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': cfg.get('dtype', 'float32').replace('float', 'f'),
+            'scaling': args.scaling, 'vs_baseline': None, 'dtype': cfg.get('dtype', 'float32').replace('float', 'f'),
             'data': 'synthetic',
             'config': {'workload': cfg['workload'], 'volume': list(shape), 'full_volume': list(full),
                        'block_shape': list(cfg['block_shape']),
                        'halo': list(cfg['halo']), 'blocks_per_gpu': nblocks, 'passes': len(passes),
                        'inner_voxels_per_gpu': inner_vox, 'outer_voxels_per_gpu': outer_vox,
-                       'streams_per_gpu': nstreams, 'parallelism': 'blocks sharded, %d GPU(s)' % world,
+                       'streams_per_gpu': nstreams,
+                       'parallelism': 'z-slabs of the block grid, one process per GPU, %d GPU(s), %s scaling'
+                                      % (world, args.scaling),
+                       'inner_voxels_all_gpus': inner_all,
                        'pass2_order': ('relaxed: every pass-2 block reads ds_out[input_bb] before any pass-2 '
                                        'write (the reference with n_jobs >= n_blocks); the workflow serialises '
                                        'overlapping halo corners (watershed.make_batches)') if two_pass else None},
@@ -549,7 +565,7 @@ def main():
             'stage_ms': {k: round(v, 3) for k, v in stage_ms.items()},
             'stage_ms_1stream': {k: round(v, 3) for k, v in stage_1.items()},
             'stage_gbs': stage_gbs,
-            'global_ids': int(offsets['scan'][-1].item() + gathered[-1].item()) if 'scan' in offsets else None,
+            'global_ids': offsets.get('n_ids'),
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)

@@ -16,7 +16,6 @@
 //   2-D slice offsets / mask                         [k_post]    (_apply_watershed)
 //   halo crop CC + uint64 offset                     [k_cc]      (_ws_block :326-341)
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -163,9 +162,6 @@ struct ctws_handle {
     DevBuf p2_hint_dev;
     int p2_depth = 0;
     std::vector<uint8_t> last_bare;  // run_batch: per block, an in-mask voxel got the bare offset
-    // RCCL
-    ncclComm_t comm = nullptr;
-    int nranks = 1, rank = 0;
 };
 
 namespace {
@@ -2212,7 +2208,6 @@ void ctws_close(ctws_handle* h) {
     }
     if (h->s_in) hipStreamDestroy(h->s_in);
     if (h->s_out) hipStreamDestroy(h->s_out);
-    if (h->comm) ncclCommDestroy(h->comm);
     hipStreamDestroy(h->stream);
     delete h;
 }
@@ -2582,57 +2577,6 @@ int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, 
     if (!on_device) HIPCHK(hipMemcpyAsync(labels, dl, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     if (n_missing) *n_missing = (int64_t)hm;
-    return CTWS_OK;
-}
-
-int ctws_comm_unique_id(ctws_handle* h, void* unique_id_128) {
-    if (!h || !unique_id_128) return CTWS_EINVAL;
-    ncclUniqueId id;
-    if (ncclGetUniqueId(&id) != ncclSuccess) {
-        h->err = "ncclGetUniqueId failed";
-        return CTWS_ECOMM;
-    }
-    std::memcpy(unique_id_128, &id, sizeof(id) < 128 ? sizeof(id) : 128);
-    return CTWS_OK;
-}
-
-int ctws_comm_init(ctws_handle* h, int nranks, int rank, const void* unique_id_128) {
-    if (!h || !unique_id_128 || nranks < 1 || rank < 0 || rank >= nranks) return CTWS_EINVAL;
-    HIPCHK(hipSetDevice(h->device));
-    ncclUniqueId id;
-    std::memcpy(&id, unique_id_128, sizeof(id));
-    ncclResult_t rr = ncclCommInitRank(&h->comm, nranks, id, rank);
-    if (rr != ncclSuccess) {
-        h->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(rr);
-        return CTWS_ECOMM;
-    }
-    h->nranks = nranks;
-    h->rank = rank;
-    return CTWS_OK;
-}
-
-int ctws_allgather_counts(ctws_handle* h, const int64_t* local_counts, int64_t n_local, int64_t* all_counts) {
-    if (!h || !local_counts || !all_counts || n_local < 0) return CTWS_EINVAL;
-    if (!h->comm) {
-        std::memcpy(all_counts, local_counts, sizeof(int64_t) * (size_t)n_local);
-        return CTWS_OK;
-    }
-    HIPCHK(hipSetDevice(h->device));
-    int64_t *d_in = nullptr, *d_out = nullptr;
-    HIPCHK(hipMalloc(&d_in, sizeof(int64_t) * std::max<int64_t>(1, n_local)));
-    HIPCHK(hipMalloc(&d_out, sizeof(int64_t) * std::max<int64_t>(1, n_local) * h->nranks));
-    HIPCHK(hipMemcpyAsync(d_in, local_counts, sizeof(int64_t) * n_local, hipMemcpyHostToDevice, h->stream));
-    ncclResult_t rr = ncclAllGather(d_in, d_out, (size_t)n_local, ncclInt64, h->comm, h->stream);
-    if (rr != ncclSuccess) {
-        hipFree(d_in);
-        hipFree(d_out);
-        h->err = std::string("ncclAllGather: ") + ncclGetErrorString(rr);
-        return CTWS_ECOMM;
-    }
-    HIPCHK(hipMemcpyAsync(all_counts, d_out, sizeof(int64_t) * n_local * h->nranks, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    hipFree(d_in);
-    hipFree(d_out);
     return CTWS_OK;
 }
 

@@ -47,9 +47,6 @@ def lib():
                     'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end'):
                 getattr(L, fn).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_last_timings.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
-            L.ctws_comm_unique_id.argtypes = [C.c_void_p, C.c_void_p]
-            L.ctws_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
-            L.ctws_allgather_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]
             L.ctws_unique_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
                                           C.POINTER(C.c_int64)]
             L.ctws_unique_counts_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p,
@@ -67,8 +64,7 @@ def lib():
 
 
 EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
-                    'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_comm_unique_id', 'ctws_comm_init',
-                    'ctws_allgather_counts', 'ctws_unique_u64', 'ctws_unique_counts_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
+                    'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_unique_u64', 'ctws_unique_counts_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
                     'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
                     'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end')
 
@@ -363,18 +359,3 @@ class Handle:
         return int(miss.value)
 
     # ---- multi-GPU label-count exchange (RCCL) ------------------------------------------
-    def comm_unique_id(self):
-        buf = (C.c_char * 128)()
-        self._check(lib().ctws_comm_unique_id(self._h, buf), 'ctws_comm_unique_id')
-        return bytes(buf)
-
-    def comm_init(self, nranks, rank, unique_id):
-        buf = (C.c_char * 128).from_buffer_copy(unique_id)
-        self._check(lib().ctws_comm_init(self._h, int(nranks), int(rank), buf), 'ctws_comm_init')
-
-    def allgather_counts(self, counts, nranks):
-        counts = np.ascontiguousarray(counts, dtype=np.int64)
-        out = np.zeros(len(counts) * nranks, dtype=np.int64)
-        self._check(lib().ctws_allgather_counts(self._h, counts.ctypes.data, len(counts), out.ctypes.data),
-                    'ctws_allgather_counts')
-        return out

@@ -18,8 +18,9 @@ without communication.  There are exactly two exchanges:
   slab boundary belong to another rank; after pass 1 each rank sends its first / last
   halo[0] rows of labels to the neighbouring ranks (point-to-point over xGMI).
 
-Single-process use (world 1) needs no process group: the functions fall back to local
-computation.
+Single-process use needs no process group: the functions fall back to local computation.
+With a process group (any world size, including 1) the exchanges go through it -- RCCL
+(backend "nccl") on MI355X, gloo on CPU.
 """
 import numpy as np
 
@@ -46,7 +47,7 @@ def gather_counts(local_counts, device=None):
     import torch
     dist = _dist()
     local = torch.as_tensor(np.asarray(local_counts, dtype=np.int64), device=device)
-    if dist is None or dist.get_world_size() == 1:
+    if dist is None:
         return local.cpu().numpy()
     world = dist.get_world_size()
     n = torch.tensor([local.numel()], dtype=torch.int64, device=device)

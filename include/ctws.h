@@ -29,11 +29,11 @@
  *       process-level setup; the reference has none (vigra is stateless).  One handle per
  *       (process, GPU), as LocalTask runs one process per job (cluster_tasks.py:507-529).
  *
- *   ctws_comm_init / ctws_allgather_counts
- *       the per-block label-count exchange that assigns compact global id offsets
- *       (RelabelWorkflow FindUniques -> FindLabeling, relabel/find_labeling.py:104-116,
- *       and the offsets scan of thresholded_components/merge_offsets.py:111-119), done
- *       over RCCL instead of .npy/.json files on a shared filesystem.
+ *   (multi-GPU) the library holds no communicator: the per-block label counts it returns
+ *       (ctws_block.n_ids) are all-gathered and exclusively scanned by the host over
+ *       torch.distributed (RCCL, cluster_tools_amd/watershed/sharded.py), replacing the
+ *       FindUniques -> FindLabeling file exchange (relabel/find_labeling.py:104-116,
+ *       thresholded_components/merge_offsets.py:111-119).
  *
  * Conventions
  *   - all arrays are C-contiguous numpy-order arrays (axis 0 = z slowest, axis 2 = x fastest)
@@ -191,16 +191,6 @@ int ctws_eval_end(ctws_handle* h, double* scores /* [4] */, int64_t* n_points);
  * handle's stream (milliseconds).  names[i] is a static string.  Returns the count.
  */
 int ctws_last_timings(const ctws_handle* h, const char** names, float* ms, int max_entries);
-
-/*
- * Multi-GPU: join an RCCL communicator (unique_id = 128 bytes from ctws_comm_unique_id on
- * rank 0, distributed by the caller), then all-gather one int64 count per block so every
- * rank can compute the exclusive scan of label counts (compact global id offsets).
- */
-int ctws_comm_unique_id(ctws_handle* h, void* unique_id_128);
-int ctws_comm_init(ctws_handle* h, int nranks, int rank, const void* unique_id_128);
-int ctws_allgather_counts(ctws_handle* h, const int64_t* local_counts, int64_t n_local,
-                          int64_t* all_counts /* nranks * n_local */);
 
 /*
  * RelabelWorkflow (relabel/find_uniques.py:93-159, find_labeling.py:84-126,

@@ -120,3 +120,24 @@ def test_two_ranks_gloo_offsets_and_halo_exchange(tmp_path):
     assert (h0[Z + hz:] == h1[hz:2 * hz]).all()            # rank 1's first own rows
     assert (h1[:hz] == h0[Z:Z + hz]).all()                 # rank 0's last own rows
     assert (h1[Z + hz:] == -1).all()
+
+
+@pytest.mark.parametrize('cfg_id', [2, 3, 4, 5])
+@pytest.mark.parametrize('world', [1, 2, 3, 8])
+def test_strong_scaling_partition(cfg_id, world):
+    """bench.py --scaling strong: the ranks' z-slabs partition the config's whole block grid --
+    every block of the volume on exactly one rank, with its full halo inside the rank's
+    generated region."""
+    import bench
+    cfg = bench.CONFIGS[cfg_id]
+    full = tuple(cfg.get('full_shape', cfg['shape']))
+    every = {b['block_id'] for b in bench.blocking(full, cfg['block_shape'], cfg['halo'])}
+    seen = []
+    for r in range(world):
+        geo = bench.volume_geometry(cfg, r, world, 'strong')
+        assert geo['full'] == full
+        for b in geo['blocks']:
+            assert 0 <= b['obeg'][0] and b['oend'][0] <= geo['gshape'][0]
+            assert geo['lo'] <= b['beg'][0] < geo['gshape'][0] - geo['hi']
+        seen += [b['block_id'] for b in geo['blocks']]
+    assert sorted(seen) == sorted(every)
