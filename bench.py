@@ -287,6 +287,85 @@ def pcie_rates(dev, nbytes=1 << 30, reps=4):
     return out
 
 
+def end_to_end(cfg_id, dev, z_extent=64, max_jobs=4, threads=4):
+    """The product path from file to file: WatershedWorkflow
+    (target 'local', GPU jobs) from an n5 gzip input to the relabelled n5 uint64 output
+    (Watershed -> FindUniques -> FindLabeling -> Write), on a z_extent x Y x X sub-volume of the
+    config (the whole config 3 volume would take minutes of gzip alone).  Run twice: with the
+    datasets gzip-compressed (n5 default, watershed.py:80-83) and uncompressed; the difference
+    is the gzip share.  The input file is written before the timed region."""
+    import json as _json
+    import shutil
+    import subprocess
+    import tempfile
+    import torch
+    from cluster_tools_amd.synthetic import boundary_map_torch
+    from cluster_tools_amd.utils import volume_utils as vu
+    cfg = CONFIGS[cfg_id]
+    shape = (min(z_extent, cfg['shape'][0]),) + tuple(cfg['shape'][1:])
+    x = boundary_map_torch(shape, seed=cfg['seed'], device=dev, dtype=cfg.get('dtype', 'float32'),
+                           pitch=cfg.get('pitch', (24, 24, 24))).cpu().numpy()
+    out = {'volume': list(shape), 'block_shape': list(cfg['block_shape']), 'max_jobs': max_jobs,
+           'threads_per_job': threads, 'workflow': 'WatershedWorkflow(target=local) + RelabelWorkflow, GPU jobs'}
+    root = tempfile.mkdtemp(prefix='ctws_e2e_')
+    try:
+        for comp in ('gzip', 'raw'):
+            d = os.path.join(root, comp)
+            os.makedirs(os.path.join(d, 'configs'))
+            env = dict(os.environ, CTWS_N5_COMPRESSION=comp)
+            inp = os.path.join(d, 'data.n5')
+            os.environ['CTWS_N5_COMPRESSION'] = comp
+            with vu.file_reader(inp) as f:
+                ds = f.create_dataset('boundaries', shape=shape, dtype=x.dtype,
+                                      chunks=tuple(b // 2 for b in cfg['block_shape']))
+                ds.n_threads = 16
+                ds[...] = x
+            os.environ.pop('CTWS_N5_COMPRESSION', None)
+            glob = {'block_shape': list(cfg['block_shape']), 'shebang': '#! ' + sys.executable,
+                    'roi_begin': None, 'roi_end': None, 'max_num_retries': 0, 'block_list_path': None}
+            with open(os.path.join(d, 'configs', 'global.config'), 'w') as f:
+                _json.dump(glob, f)
+            from cluster_tools_amd.watershed.watershed import WatershedLocal
+            tc = WatershedLocal.default_task_config()
+            tc.update(cfg['task'])
+            tc['threads_per_job'] = threads
+            with open(os.path.join(d, 'configs', 'watershed.config'), 'w') as f:
+                _json.dump(tc, f)
+            for name in ('find_uniques', 'find_labeling', 'write'):
+                with open(os.path.join(d, 'configs', name + '.config'), 'w') as f:
+                    _json.dump({'threads_per_job': threads}, f)
+            code = ('import sys; sys.path.insert(0, %r)\n'
+                    'from cluster_tools_amd import luigi_compat as luigi\n'
+                    'from cluster_tools_amd.watershed import WatershedWorkflow\n'
+                    'wf = WatershedWorkflow(input_path=%r, input_key="boundaries", output_path=%r, output_key="ws", '
+                    'config_dir=%r, tmp_folder=%r, target="local", max_jobs=%d)\n'
+                    'sys.exit(0 if luigi.build([wf], local_scheduler=True) else 1)\n'
+                    % (HERE, inp, os.path.join(d, 'ws.n5'), os.path.join(d, 'configs'), os.path.join(d, 'tmp'),
+                       max_jobs))
+            t0 = time.perf_counter()
+            rc = subprocess.call([sys.executable, '-c', code], env=env, stdout=subprocess.DEVNULL,
+                                 stderr=subprocess.DEVNULL)
+            t = time.perf_counter() - t0
+            if rc != 0:
+                out['error_' + comp] = 'workflow failed (rc %d)' % rc
+                continue
+            n = int(np.prod(shape))
+            out[comp] = {'s': round(t, 2), 'gvoxel_s': round(n / t / 1e9, 4),
+                         'input_bytes_on_disk': int(sum(os.path.getsize(os.path.join(dp, fn))
+                                                        for dp, _, fs in os.walk(inp) for fn in fs)),
+                         'output_bytes_on_disk': int(sum(os.path.getsize(os.path.join(dp, fn))
+                                                         for dp, _, fs in os.walk(os.path.join(d, 'ws.n5'))
+                                                         for fn in fs))}
+            shutil.rmtree(d, ignore_errors=True)
+        if 'gzip' in out and 'raw' in out:
+            out['gzip_share'] = round(1.0 - out['raw']['s'] / out['gzip']['s'], 3)
+            out['value'] = out['gzip']['gvoxel_s']
+            out['unit'] = 'Gvoxel/s'
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return out
+
+
 def progress(msg):
     """A line on stderr per phase: long profiler passes show they are alive."""
     print('[bench %.1fs] %s' % (time.time() - _T0, msg), file=sys.stderr, flush=True)
@@ -303,6 +382,8 @@ def main():
     ap.add_argument('--config', type=int, default=DEFAULT_CONFIG, choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe-inclusive) pass')
+    ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end n5 workflow run')
+    ap.add_argument('--e2e-z', type=int, default=64, help='z extent of the end-to-end sub-volume')
     ap.add_argument('--cpu-cores', type=int, default=0, help='cap on the CPU baseline jobs (0: usable cores)')
     ap.add_argument('--scaling', choices=('weak', 'strong'), default='weak',
                     help='weak: every rank runs the config\'s single-GPU workload (default); strong: the '
@@ -495,6 +576,17 @@ def main():
                 'phases_ms': phases, 'pcie': pcie_rates(dev), 'matches_device_path': bool(same)}
         del hb
 
+    # ---- end to end: n5 gzip in -> WatershedWorkflow (GPU jobs) + relabel -> n5 out --------
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e and not two_pass:
+        progress('end-to-end workflow run')
+        for hh in handles:
+            hh.close()
+        handles = []
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        e2e = end_to_end(args.config, dev, z_extent=args.e2e_z)
+
     # ---- VI of the GPU output vs the oracle on the CPU baseline's first block ---------------
     vi = None
     if ref_block is not None and ref_block[1] is not None and ref_block[0] in blocks:
@@ -561,6 +653,7 @@ def main():
                                   'achieved': round(pipe, 1), 'unit': 'GB/s',
                                   'frac': round(pipe / HBM_PEAK_GBS, 4)},
             'host_resident': host,
+            'end_to_end': e2e,
             'vi_vs_oracle': vi,
             'stage_ms': {k: round(v, 3) for k, v in stage_ms.items()},
             'stage_ms_1stream': {k: round(v, 3) for k, v in stage_1.items()},

@@ -295,6 +295,9 @@ class Group:
         os.makedirs(p)
         comp = compression if compression in ('gzip', 'zlib', 'raw', None) else 'gzip'
         comp = 'raw' if comp is None else comp
+        # measurement hook (bench.py end_to_end): store every new dataset uncompressed, to
+        # separate the gzip share of an end-to-end run
+        comp = os.environ.get('CTWS_N5_COMPRESSION', comp)
         if self.fmt == 'n5':
             meta = {'dimensions': list(shape)[::-1], 'blockSize': list(chunks)[::-1],
                     'dataType': _N5_DTYPES[dtype.name],
