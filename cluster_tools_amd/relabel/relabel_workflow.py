@@ -14,11 +14,15 @@ class RelabelWorkflow(WorkflowBase):
     assignment_key = luigi.Parameter()
     output_path = luigi.Parameter(default='')
     output_key = luigi.Parameter(default='')
+    # not in the reference: per-block uniques written by the producing watershed task
+    # (WatershedBase.uniques_path), so FindUniques skips reading those blocks
+    uniques_path = luigi.Parameter(default='')
 
     def requires(self):
         unique_task = getattr(unique_tasks, self._get_task_name('FindUniques'))
         dep = unique_task(tmp_folder=self.tmp_folder, max_jobs=self.max_jobs, config_dir=self.config_dir,
-                          input_path=self.input_path, input_key=self.input_key, dependency=self.dependency)
+                          input_path=self.input_path, input_key=self.input_key, dependency=self.dependency,
+                          uniques_path=self.uniques_path)
         labeling_task = getattr(labeling_tasks, self._get_task_name('FindLabeling'))
         dep = labeling_task(tmp_folder=self.tmp_folder, max_jobs=self.max_jobs, config_dir=self.config_dir,
                             dependency=dep, input_path=self.input_path, input_key=self.input_key,

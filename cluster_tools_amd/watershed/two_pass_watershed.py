@@ -27,6 +27,7 @@ class TwoPassWatershedBase(luigi.Task):
     output_key = luigi.Parameter()
     mask_path = luigi.Parameter(default='')
     mask_key = luigi.Parameter(default='')
+    uniques_path = luigi.Parameter(default='')   # see WatershedBase.uniques_path
 
     @staticmethod
     def default_task_config():

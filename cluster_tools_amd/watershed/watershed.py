@@ -11,6 +11,7 @@ writes of the previous one overlap the GPU work of the current batch.
 """
 import json
 import os
+import shutil
 import sys
 from concurrent import futures
 
@@ -35,6 +36,9 @@ class WatershedBase(luigi.Task):
     output_key = luigi.Parameter()
     mask_path = luigi.Parameter(default='')
     mask_key = luigi.Parameter(default='')
+    # not in the reference: a folder for the per-block uniques of the written labels, which a
+    # following FindUniques (RelabelWorkflow's uniques_path) reads instead of the volume
+    uniques_path = luigi.Parameter(default='')
 
     @staticmethod
     def default_task_config():
@@ -69,7 +73,16 @@ def ws_task_setup(task, block_shape):
     if task.mask_path != '':
         assert task.mask_key != ''
         cfg.update(mask_path=task.mask_path, mask_key=task.mask_key)
+    if task.uniques_path != '':
+        # every block of this run rewrites its file; files of an earlier run must not survive
+        shutil.rmtree(task.uniques_path, ignore_errors=True)
+        os.makedirs(task.uniques_path)
+        cfg['uniques_path'] = task.uniques_path
     return shape, cfg
+
+
+def block_uniques_file(folder, block_id):
+    return os.path.join(folder, 'block_%i.npy' % block_id)
 
 
 class WatershedLocal(WatershedBase, LocalTask):
@@ -185,12 +198,18 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
     def read_batch(ids):
         return [_read_block(blocking, bid, ds_in, ds_out, mask, config, pass_id) for bid in ids]
 
-    def write_batch(blocks, results, error):
-        for b, r in zip(blocks, results):
+    uniques_path = config.get('uniques_path')
+
+    def write_batch(blocks, results, error, uniques):
+        for b, r, u in zip(blocks, results, uniques):
             if r is not None and r['status'] == ctws.CTWS_BLOCK_FAILED:
                 raise ctws.CtwsError("block %i: %s" % (b['block_id'], error))
             if r is not None and r['status'] in (0, 2):   # written / empty block: constant offset
                 ds_out[b['output_bb']] = r['output']
+            if u is not None:
+                # after the block's data: a file never describes labels that are not written.
+                # A block that writes nothing gets no file (FindUniques reads what it holds).
+                np.save(block_uniques_file(uniques_path, b['block_id']), u)
             fu.log_block_success(b['block_id'])
 
     with ctws.Handle(_device()) as h, futures.ThreadPoolExecutor(2) as io:
@@ -207,9 +226,12 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
             res = h.ws_blocks(lib_config, block_shape, todo, pass_id=pass_id) if todo else []
             error = h.last_error()
             by_id = {b['block_id']: r for b, r in zip(todo, res)}
+            results = [by_id.get(b['block_id']) for b in blocks]
+            uniques = [h.unique_u64(r['output']) if uniques_path and r is not None and r['status'] in (0, 2)
+                       else None for r in results]
             if pending_write is not None:
                 pending_write.result()
-            pending_write = io.submit(write_batch, blocks, [by_id.get(b['block_id']) for b in blocks], error)
+            pending_write = io.submit(write_batch, blocks, results, error, uniques)
             if pass_id == 1:
                 # the next batch's halos may hold this batch's outputs: read after the write
                 pending_write.result()

@@ -5,6 +5,8 @@ Watershed{Local,Slurm,LSF} (or TwoPassWatershed* with two_pass=True), then Relab
 output_path/'relabel_watershed').  The optional post-watershed agglomeration of the reference
 (agglomeration=True, nifty RAG + clustering) is out of scope for this build and raises.
 """
+import os
+
 from cluster_tools_amd import luigi_compat as luigi
 from cluster_tools_amd.cluster_tasks import WorkflowBase
 from cluster_tools_amd.watershed import watershed as watershed_tasks
@@ -30,14 +32,17 @@ class WatershedWorkflow(WorkflowBase):
             ws_task = getattr(two_pass_tasks, self._get_task_name('TwoPassWatershed'))
         else:
             ws_task = getattr(watershed_tasks, self._get_task_name('Watershed'))
+        # the watershed jobs keep the uniques of the blocks they write; FindUniques reads those
+        # instead of the label volume
+        uniques_path = os.path.join(self.tmp_folder, 'watershed_block_uniques')
         dep = ws_task(tmp_folder=self.tmp_folder, max_jobs=self.max_jobs, config_dir=self.config_dir,
                       input_path=self.input_path, input_key=self.input_key,
                       output_path=self.output_path, output_key=self.output_key,
-                      mask_path=self.mask_path, mask_key=self.mask_key)
+                      mask_path=self.mask_path, mask_key=self.mask_key, uniques_path=uniques_path)
         return RelabelWorkflow(tmp_folder=self.tmp_folder, max_jobs=self.max_jobs, config_dir=self.config_dir,
                                target=self.target, input_path=self.output_path, input_key=self.output_key,
                                assignment_path=self.output_path, assignment_key='relabel_watershed',
-                               dependency=dep)
+                               dependency=dep, uniques_path=uniques_path)
 
     @staticmethod
     def get_config():

@@ -126,6 +126,19 @@ def test_watershed_workflow(tmp_path, name, with_mask):
     start = 0 if uniq[0] == 0 else 1
     np.testing.assert_array_equal(table[:, 0], uniq)
     np.testing.assert_array_equal(table[:, 1], np.arange(start, start + len(uniq), dtype='uint64'))
+    # the watershed jobs' per-block uniques that FindUniques read instead of the volume: one
+    # file per written block (mask-skipped blocks have none and are read), each np.unique of
+    # the block's raw labels
+    from cluster_tools_amd.watershed.watershed import block_uniques_file
+    blocking = Blocking([0, 0, 0], list(SHAPE), BLOCK_SHAPE)
+    folder = str(tmp_path / 'tmp' / 'watershed_block_uniques')
+    n_files = 0
+    for bid in range(blocking.numberOfBlocks):
+        path = block_uniques_file(folder, bid)
+        if os.path.exists(path):
+            n_files += 1
+            np.testing.assert_array_equal(np.load(path), np.unique(raw[vu.block_to_bb(blocking.getBlock(bid))]))
+    assert n_files == blocking.numberOfBlocks or (with_mask and n_files > 0)
 
 
 def _reference_relabel(raw):
