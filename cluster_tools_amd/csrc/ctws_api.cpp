@@ -66,6 +66,8 @@ struct Workspace {
     // frontier bitmaps of the descent flood
     int64_t cap_front = 0;
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
+    uint64_t* fplat = nullptr;   // plateau fill (k_plateau.hip): the plateau voxels
+    uint32_t* plev = nullptr;    // per block: the plateau height (0: none)
     uint32_t* fflags = nullptr;
     uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: generation of its last change
     uint32_t *wl0 = nullptr, *wl1 = nullptr, *qgen = nullptr;  // chunk worklists, queued generation
@@ -126,6 +128,7 @@ struct ctws_handle {
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
+    int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int words_per_wave = 32;    // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels
@@ -274,6 +277,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(front0, front);
         ALLOC(front1, front);
         ALLOC(fopen, front);
+        ALLOC(fplat, front);
         ALLOC(fchunk0, (front >> kChunkShift) + 1);
         ALLOC(fchunk1, (front >> kChunkShift) + 1);
         ALLOC(wl0, (front >> kChunkShift) + 1);
@@ -285,6 +289,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
     if (!w.wlcnt) ALLOC(wlcnt, kFrontierMaxItersCap + 2);
     if (blocks > w.cap_fstat) {
         ALLOC(fstat, 2 * blocks);
+        ALLOC(plev, blocks);
         w.cap_fstat = blocks;
     }
     if (!w.counter) ALLOC(counter, kCounterBytes / 4);
@@ -1170,7 +1175,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         LAUNCHCHK();
         // plateaus (equal-valued maxima candidates) and the seed CC: LDS tile union-find
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
-        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0};
+        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, nullptr};
         if (pl.nd_ws == 3) {
             using T = CcTile<3>;
             const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
@@ -1279,10 +1284,37 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_descent_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
                                                   w.front0, fst);
         LAUNCHCHK();
+        // masked blocks: their plateau leaves the open set until the rest is flooded (k_plateau.hip)
+        bool any_mask = false;
+        for (int i = 0; i < nb; ++i) any_mask |= desc[i].mask != nullptr;
+        const bool plat_fill = h->plateau_fill && packed && any_mask;
+        if (plat_fill) {
+            HIPCHK(hipMemsetAsync(w.plev, 0, sizeof(uint32_t) * (size_t)nb, h->stream));
+            HIPCHK(hipMemsetAsync(w.fplat, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+            k_plat_level<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.fopen, w.plev);
+            k_plat_mark<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.plev, w.fopen, w.fplat);
+            LAUNCHCHK();
+        }
         mark("flood_descent");
         // frontier relaxation of the remaining voxels (k_frontier, one voxel per lane)
         if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
             return r;
+        if (plat_fill) {
+            // the plateau: entries, min-plus runs along x, y (, z), then the frontier from there
+            if (pl.nd_ws == 3) k_plat_entry<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fplat, w.plev);
+            else k_plat_entry<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fplat, w.plev);
+            const unsigned rows_g = (unsigned)std::min<int64_t>(((int64_t)maxZ * maxY + 3) / 4, 4096);
+            const unsigned cols_g = (unsigned)std::min<int64_t>(((int64_t)std::max(maxZ, maxY) * ((maxX + 63) / 64) + 3) / 4, 4096);
+            k_plat_scan_x<<<dim3(rows_g, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.fplat, w.plev);
+            k_plat_scan_col<1><<<dim3(cols_g, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.fplat, w.plev);
+            if (pl.nd_ws == 3)
+                k_plat_scan_col<2><<<dim3(cols_g, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.fplat, w.plev);
+            k_plat_restore<<<dim3((unsigned)std::min<int64_t>(((int64_t)maxZ * maxY * ((maxX + 63) / 64) + 255) / 256, 4096), nb), 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, w.fplat,
+                                                                                  w.front0);
+            LAUNCHCHK();
+            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
+                return r;
+        }
         mark("flood_relax");
         if (fst) {
             std::vector<uint32_t> hs(2 * (size_t)nb);
@@ -1485,7 +1517,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
         // ---- halo crop CC (labelVolumeWithBackground) + uint64 output --------------------------
         if (any_crop) {
-            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final};
+            // tile roots of the crop CC marked in the (free) frontier bitmap front0
+            HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0};
             const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;
@@ -1499,7 +1533,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 k_tile_merge<2, CC_CROP><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             }
             HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-            k_flatten_roots_w<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W);
+            k_flatten_tile_roots<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0, w.W);
             k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
             k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
             k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
@@ -2137,6 +2171,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_GAUSS_YX")) h->gauss_yx = std::atoi(t);
     if (const char* t = std::getenv("CTWS_HOST_BATCH_VOXELS")) h->host_batch_voxels = std::max<int64_t>(1, std::atoll(t));
     if (const char* t = std::getenv("CTWS_HOST_RAMP")) h->host_ramp = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_PLATEAU_FILL")) h->plateau_fill = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_MODE")) h->h2d_mode = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_WGS")) h->h2d_wgs = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_HOST_BATCH_BLOCKS")) h->host_batch_blocks = std::max(0, std::atoi(t));

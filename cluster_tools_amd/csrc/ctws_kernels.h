@@ -89,6 +89,18 @@ __global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*,
 __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uint32_t*);
 __global__ void k_flatten_roots(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
 __global__ void k_flatten_roots_w(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
+__global__ void k_flatten_tile_roots(const BlockDesc*, const BlockStat*, uint32_t*, const uint64_t*, uint64_t*);
+
+// k_plateau.hip: the flood across a masked block's plateau (entries + min-plus run scans)
+__global__ void k_plat_level(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, uint32_t*);
+__global__ void k_plat_mark(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint64_t*);
+template <int ND>
+__global__ void k_plat_entry(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
+                             const uint32_t*);
+__global__ void k_plat_scan_x(const BlockDesc*, const BlockStat*, uint64_t*, const uint64_t*, const uint32_t*);
+template <int AX>
+__global__ void k_plat_scan_col(const BlockDesc*, const BlockStat*, uint64_t*, const uint64_t*, const uint32_t*);
+__global__ void k_plat_restore(const BlockDesc*, const BlockStat*, uint64_t*, const uint64_t*, uint64_t*);
 __global__ void k_bitmap_csum(const BlockDesc*, const BlockStat*, int, const uint64_t*, uint32_t*);
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
 __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uint64_t*, const uint32_t*, uint32_t*);
@@ -108,6 +120,7 @@ struct CcArgs {
     const uint32_t* lab;   // CROP: flood labels (non-packed)
     const uint64_t* key;   // CROP: packed keys
     int packed;            // CROP
+    uint64_t* troot;       // CROP: tile-root bitmap (inner C index, per block at fbase), zeroed
 };
 template <int ND>
 struct CcTile;

@@ -377,8 +377,17 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
         if (active) {
             uint32_t l;
             if (B.crop) {
+                // member -> its tile root -> (the tile root's global root, k_flatten_tile_roots)
                 const uint32_t p = gbl(P)[iq];
-                l = p == kNoParent ? 0u : cc_label(P, p);
+                l = 0u;
+                if (p != kNoParent) {
+                    if (p & kRootBit) {
+                        l = p & ~kRootBit;
+                    } else {
+                        const uint32_t q = P[p];
+                        l = (q & kRootBit) ? (q & ~kRootBit) : (P[q] & ~kRootBit);
+                    }
+                }
             } else {
                 l = packed ? (uint32_t)(gbl(key)[B.base + o] & kLabelMask) : (gbl(lab)[B.base + o] & ~kFixedBit);
                 if (packed && gbl(key)[B.base + o] == kInfKey) l = 0u;
@@ -456,6 +465,38 @@ __global__ void __launch_bounds__(256) k_flatten_roots(const BlockDesc* __restri
             } else {
                 const uint32_t r = uf_find(P, p);
                 if (r != p) P[i] = r;
+            }
+        }
+    }
+}
+
+// Crop CC: only the tile roots (bits of the tile-root bitmap TR, set by k_tile_cc<.., CC_CROP>)
+// are pointed at their global root; members keep pointing at their tile root, and k_output
+// follows member -> tile root -> root.  Global roots set their scan-key bit in W (zeroed).
+// One thread per bitmap word: the roots are few (a handful per tile), the voxels are not read.
+__global__ void __launch_bounds__(256) k_flatten_tile_roots(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                            uint32_t* __restrict__ PFg, const uint64_t* __restrict__ TR,
+                                                            uint64_t* __restrict__ Wg) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active || !B.crop) return;
+    uint32_t* P = PFg + B.ibase;
+    uint64_t* W = Wg + B.wbase;
+    const int64_t nw = B.NI / 64 + 1;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t bits = TR[B.fbase + w];
+        while (bits) {
+            const int b = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            const uint32_t i = (uint32_t)(w * 64 + b);
+            const uint32_t r = uf_find(P, i);
+            if (r != i) {
+                P[i] = r;
+            } else {
+                const int x = (int)(i % (uint32_t)B.IX);
+                const uint32_t t = i / (uint32_t)B.IX;
+                const int y = (int)(t % (uint32_t)B.IY), z = (int)(t / (uint32_t)B.IY);
+                const uint32_t f = (uint32_t)(z + B.IZ * (y + B.IY * x));
+                atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
             }
         }
     }

@@ -258,12 +258,16 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
         const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
         if (z >= nz || y >= ny || x >= nx) continue;
         uint32_t g = kNoParent;
+        const int64_t gi = ((int64_t)z * ny + y) * nx + x;
         if (vv[j] != kLNone) {
             const uint32_t r = lds_find(sp, (uint32_t)c);
             const int rx = (int)(r % TX), ry = (int)((r / TX) % TY), rz = (int)(r / (TX * TY));
             g = (uint32_t)(((int64_t)(z0 + rz) * ny + (y0 + ry)) * nx + (x0 + rx));
+            // CROP: the tile roots, so that only they are flattened (k_flatten_tile_roots)
+            if (MODE == CC_CROP && r == (uint32_t)c)
+                atomicOr((unsigned long long*)&a.troot[B.fbase + (gi >> 6)], 1ull << (gi & 63));
         }
-        P[((int64_t)z * ny + y) * nx + x] = g;
+        P[gi] = g;
     }
 }
 

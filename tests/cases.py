@@ -44,6 +44,11 @@ def make_cases():
     # dt with Y^2 + X^2 >= 2^24 (vigra's float arithmetic: k_edt_real_* with T = float)
     xw1100 = _x(seed=15, shape=(8, 10, 1100))
     xw4096 = _x(seed=16, shape=(2, 24, 4096))
+    # a mask of random blobs: the masked region is a non-convex plateau with holes, so the
+    # plateau fill's run scans (k_plateau.hip) miss paths that the frontier has to correct
+    rs = np.random.RandomState(17)
+    from scipy.ndimage import gaussian_filter
+    blobs = gaussian_filter(rs.rand(*SHAPE), (1.5, 4, 4)) > 0.5
     return {
         '3d_pitch_real': (dict(D3, pixel_pitch=(10.5, 1, 1)), dict(input=x)),
         '3d_pitch_frac': (dict(D3, pixel_pitch=(2.25, 0.75, 1.5)), dict(input=x)),
@@ -69,6 +74,8 @@ def make_cases():
                           dict(input=x, inner_begin=inner3[0], inner_shape=inner3[1], crop_relabel=True)),
         '3d_pitch': (dict(D3, pixel_pitch=(10, 1, 1)), dict(input=x)),
         '3d_mask': (dict(D3), dict(input=x, mask=m)),
+        '3d_mask_blobs': (dict(D3), dict(input=x, mask=blobs)),
+        '2d_mask_blobs': ({}, dict(input=x, mask=blobs)),
         '2d_mask': ({}, dict(input=x, mask=m)),
         '3d_mask_halo': (dict(D3), dict(input=x, mask=m, inner_begin=inner3[0], inner_shape=inner3[1],
                                         crop_relabel=True)),

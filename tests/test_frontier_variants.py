@@ -1,8 +1,8 @@
 """The frontier relaxation's schedule knobs change the order of work, never the result.
 
 The flood's fixpoint (K = f(min of the neighbours' keys), k_flood.hip) is unique, so every
-chunk brick (CTWS_FRONTIER_CHUNK2D / _3D) and a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
-non-converged re-queue path runs) must reproduce the oracle's flood model bit for bit on every
+chunk brick (CTWS_FRONTIER_CHUNK2D / _3D), a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
+non-converged re-queue path runs) and the masked-plateau fill switched off (CTWS_PLATEAU_FILL=0) must reproduce the oracle's flood model bit for bit on every
 parity case, as the default schedule does (test_gpu_parity.py::test_flood_matches_model_exactly).
 The knobs are read when a handle is opened.
 """
@@ -23,6 +23,8 @@ VARIANTS = {
     'bricks_c': {'CTWS_FRONTIER_CHUNK2D': '2x32x1', 'CTWS_FRONTIER_CHUNK3D': '1x16x4'},
     'rows_3d_one_sweep': {'CTWS_FRONTIER_CHUNK3D': '8x8x1', 'CTWS_FRONTIER_REPS': '1'},
     'one_sweep': {'CTWS_FRONTIER_REPS': '1'},
+    # masked blocks' plateaus relaxed hop by hop instead of filled by run scans (k_plateau.hip)
+    'no_plateau_fill': {'CTWS_PLATEAU_FILL': '0'},
 }
 
 

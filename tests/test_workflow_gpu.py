@@ -71,6 +71,19 @@ def _oracle_volume(x, c, mask):
     return out
 
 
+def _build(task, tmp_folder):
+    """luigi.build, and on failure the failed jobs' error logs in the assertion message."""
+    import glob
+    ok = luigi.build([task], local_scheduler=True)
+    if not ok:
+        msgs = []
+        for p in sorted(glob.glob(os.path.join(str(tmp_folder), 'error_logs', '*.err'))):
+            txt = open(p).read().strip()
+            if txt and 'amdgpu.ids' not in txt.splitlines()[-1]:
+                msgs.append('%s:\n%s' % (os.path.basename(p), txt[-2000:]))
+        raise AssertionError('workflow failed\n' + '\n'.join(msgs))
+
+
 def _n_ids_and_ccs(res):
     cc, _ = O.label_with_background(res.astype('uint32'))
     return len(np.unique(res)), len(np.unique(cc))
@@ -112,7 +125,7 @@ def test_watershed_workflow(tmp_path, name, with_mask):
     wf = WatershedWorkflow(input_path=inp, input_key='boundaries', output_path=out, output_key='ws',
                            config_dir=cfg_dir, tmp_folder=str(tmp_path / 'tmp'), target='local', max_jobs=2,
                            **mask_kw)
-    assert luigi.build([wf], local_scheduler=True)
+    _build(wf, tmp_path / 'tmp')
     with vu.file_reader(out, 'r') as f:
         res = f['ws'][:]
         assert f['ws'].attrs['maxId'] == int(res.max())
