@@ -67,6 +67,8 @@ struct Workspace {
     int64_t cap_front = 0;
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
     uint64_t* fplat = nullptr;   // plateau fill (k_plateau.hip): the plateau voxels
+    uint64_t* flake = nullptr;   // basin flood (k_basin.hip): the lake voxels
+    uint32_t* bctl = nullptr;    // basin flood: [0] edges, [1] lake voxels, [2 + it] relax sweep it changed a root
     uint32_t* plev = nullptr;    // per block: the plateau height (0: none)
     uint32_t* fflags = nullptr;
     uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: generation of its last change
@@ -81,6 +83,7 @@ constexpr int kFrontierBatch = 8;        // frontier iterations per host check
 constexpr int kFrontierWavesHost = 4;    // waves per workgroup of k_frontier (kFrontierWaves)
 constexpr int kFrontierMaxIters = 256;   // then the tile flood takes over
 constexpr int kFrontierMaxItersCap = 4096;  // CTWS_FRONTIER_ITERS upper bound (worklist counters)
+constexpr int kBasinMaxIters = 64;       // catchment-graph sweeps before the frontier relaxation takes over
 
 }  // namespace
 
@@ -129,6 +132,8 @@ struct ctws_handle {
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
+    int basin = 1;         // CTWS_BASIN=0: the open voxels by the frontier relaxation alone (k_basin.hip)
+    DevBuf basin_edges;    // basin flood: catchment pairs (root, root, pass height)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int words_per_wave = 32;    // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels
@@ -278,6 +283,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(front1, front);
         ALLOC(fopen, front);
         ALLOC(fplat, front);
+        ALLOC(flake, front);
         ALLOC(fchunk0, (front >> kChunkShift) + 1);
         ALLOC(fchunk1, (front >> kChunkShift) + 1);
         ALLOC(wl0, (front >> kChunkShift) + 1);
@@ -286,6 +292,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         w.cap_front = front;
     }
     if (!w.fflags) ALLOC(fflags, kFrontierBatch);
+    if (!w.bctl) ALLOC(bctl, 2 + kBasinMaxIters);
     if (!w.wlcnt) ALLOC(wlcnt, kFrontierMaxItersCap + 2);
     if (blocks > w.cap_fstat) {
         ALLOC(fstat, 2 * blocks);
@@ -715,6 +722,80 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
 }
 
 
+
+void add_timing(ctws_handle* h, const char* name, float v);
+
+// The open voxels of the descent flood on the catchment graph (k_basin.hip): catchment-root
+// passes (edges + Bellman-Ford sweeps over the root pairs), the keys' (C, d) (lake voxels by the
+// frontier relaxation), then the labels by parent chains.  *done = false when the pair list does
+// not fit or the sweeps do not converge: the keys of the open voxels are then still the
+// descent's (INF) and the caller runs the frontier relaxation instead.  Ties between two argmin
+// neighbours are left to the caller's checked repair (k_flood_verify with marks).
+int run_basin(ctws_handle* h, const Plan& pl, int nb, int64_t T, int64_t TF, int max_tiles, int64_t TT, bool packed,
+              const dim3& wtg, const dim3& tg, bool plat, bool* done, int* fiters, int* rounds, float* fkms) {
+    Workspace& w = h->ws;
+    *done = false;
+    if (T >= (int64_t)0xFFFFFFF0ll) return CTWS_OK;  // root pairs hold batch indices in 32 bits
+    const uint32_t ecap = (uint32_t)std::min<int64_t>(T / 8 + 4096, 0x7FFFFFFFll);
+    int r;
+    if ((r = grow(h, h->basin_edges, sizeof(uint4) * (size_t)ecap)) != CTWS_OK) return r;
+    uint4* edges = (uint4*)h->basin_edges.p;
+    uint32_t* cr = (uint32_t*)w.A;  // free between the hmap and the size filter
+    const uint64_t* fpl = plat ? w.fplat : nullptr;
+    HIPCHK(hipMemsetAsync(w.bctl, 0, sizeof(uint32_t) * (2 + kBasinMaxIters), h->stream));
+    if (pl.nd_ws == 3)
+        k_basin_edges<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, edges, w.bctl, ecap);
+    else
+        k_basin_edges<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, edges, w.bctl, ecap);
+    LAUNCHCHK();
+    const unsigned rgrid = (unsigned)std::min<int64_t>((int64_t)(ecap + 255) / 256, 2048);
+    int it = 0;
+    bool conv = false;
+    while (it < kBasinMaxIters && !conv) {
+        const int n = std::min(8, kBasinMaxIters - it);
+        for (int k = 0; k < n; ++k)
+            k_basin_relax<<<rgrid, 256, 0, h->stream>>>(edges, w.bctl, ecap, cr, w.bctl + 2, it + k);
+        LAUNCHCHK();
+        HIPCHK(hipMemcpyAsync(h->h_counter, w.bctl, sizeof(uint32_t) * (size_t)(2 + it + n), hipMemcpyDeviceToHost,
+                              h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        if (h->h_counter[0] > ecap) {
+            add_timing(h, "basin_overflow", 1.f);
+            return CTWS_OK;
+        }
+        for (int k = 0; k < n && !conv; ++k) {
+            ++it;
+            conv = h->h_counter[2 + it - 1] == 0u;
+        }
+    }
+    add_timing(h, "basin_edges", (float)h->h_counter[0]);
+    add_timing(h, "basin_sweeps", (float)it);
+    if (!conv) return CTWS_OK;
+    if (pl.nd_ws == 3)
+        k_basin_keys<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, w.key, w.flake,
+                                                    w.front0, w.bctl + 1);
+    else
+        k_basin_keys<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, w.key, w.flake,
+                                                    w.front0, w.bctl + 1);
+    LAUNCHCHK();
+    HIPCHK(hipMemcpyAsync(h->h_counter + 1, w.bctl + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    add_timing(h, "basin_lake", (float)h->h_counter[1]);
+    if (h->h_counter[1]) {
+        // the lake voxels' (C, d): the frontier relaxation with the lake as its open set and every
+        // other voxel as the first changed set
+        std::swap(w.fopen, w.flake);
+        r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, fiters, rounds, fkms);
+        std::swap(w.fopen, w.flake);
+        if (r != CTWS_OK) return r;
+    }
+    if (pl.nd_ws == 3) k_basin_tile<3><<<tg, 512, 0, h->stream>>>(w.desc, w.stat, w.key, w.fopen, fpl, w.P);
+    else k_basin_tile<2><<<tg, 512, 0, h->stream>>>(w.desc, w.stat, w.key, w.fopen, fpl, w.P);
+    k_basin_hop<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.P, w.fopen, w.key);
+    LAUNCHCHK();
+    *done = true;
+    return CTWS_OK;
+}
 
 int64_t words_of(int64_t n) { return n / 64 + 1; }
 int64_t chunks_of(int64_t n) { return (words_of(n) + 255) / 256; }
@@ -1271,18 +1352,20 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     uint32_t* fst = h->trace ? w.fstat : nullptr;
     if (descent) {
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
+        // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles; k_basin_tile: the same)
+        const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
+        const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
         {
-            // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
-            const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
-            const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
             if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
             else k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
             LAUNCHCHK();
         }
         mark("descent_tile");
         if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
+        // basin flood (k_basin.hip): the descent also records every open voxel's catchment root
+        const bool basin = h->basin && packed;
         k_descent_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
-                                                  w.front0, fst);
+                                                  w.front0, fst, basin ? (uint32_t*)w.A : nullptr);
         LAUNCHCHK();
         // masked blocks: their plateau leaves the open set until the rest is flooded (k_plateau.hip)
         bool any_mask = false;
@@ -1296,8 +1379,13 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             LAUNCHCHK();
         }
         mark("flood_descent");
-        // frontier relaxation of the remaining voxels (k_frontier, one voxel per lane)
-        if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
+        // the remaining voxels: on the catchment graph (k_basin.hip), else (or when its root pairs
+        // do not fit / converge) by the frontier relaxation (k_frontier, one voxel per lane)
+        bool basin_done = false;
+        if (basin && (r = run_basin(h, pl, nb, T, TF, max_tiles, TT, packed, wtg, dg, plat_fill, &basin_done, &fiters,
+                                    &rounds1, &fk1)) != CTWS_OK)
+            return r;
+        if (!basin_done && (r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
             return r;
         if (plat_fill) {
             // the plateau: entries, min-plus runs along x, y (, z), then the frontier from there
@@ -1330,16 +1418,37 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         // fixpoint check of every voxel (a guard: the descent argument and the frontier's
         // convergence make a violation impossible); on a violation the batch is flooded again
-        // from the seeds alone.  On by default (CTWS_VERIFY=0 turns it off).
-        if (h->verify) {
+        // from the seeds alone.  On by default (CTWS_VERIFY=0 turns it off).  After the basin
+        // flood the check always runs first with marks: the voxels whose label a tie between two
+        // argmin neighbours left too large (and everything below them) are repaired by the
+        // frontier relaxation from the marked voxels' neighbourhoods, then checked again.
+        auto verify = [&](uint64_t* marks) -> int {
             HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
+            if (marks) HIPCHK(hipMemsetAsync(marks, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
             if (pl.nd_ws == 3)
-                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter, marks);
             else
-                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter, marks);
             LAUNCHCHK();
             HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
+            return CTWS_OK;
+        };
+        bool checked = false;
+        if (basin_done) {
+            if ((r = verify(w.front0)) != CTWS_OK) return r;
+            checked = true;
+            add_timing(h, "basin_repair", h->h_counter[0] ? 1.f : 0.f);
+            if (h->h_counter[0]) {
+                if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters, &rounds1, &fk1)) != CTWS_OK)
+                    return r;
+                h->h_counter[0] = 0;
+                checked = h->verify != 0;
+                if (checked && (r = verify(nullptr)) != CTWS_OK) return r;
+            }
+        }
+        if (h->verify || checked) {
+            if (!checked && (r = verify(nullptr)) != CTWS_OK) return r;
             if (h->trace && h->h_counter[0]) {
                 fprintf(stderr, "[ctws] flood verify: violations at");
                 for (uint32_t k = 0; k < std::min(8u, h->h_counter[1]); ++k) fprintf(stderr, " %u", h->h_counter[2 + k]);
@@ -1438,9 +1547,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 // the regrow's fixpoint at the voxels it solved (the removed ones)
                 HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
                 if (pl.nd_ws == 3)
-                    k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+                    k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter, nullptr);
                 else
-                    k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+                    k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter, nullptr);
                 LAUNCHCHK();
                 HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
                 HIPCHK(hipStreamSynchronize(h->stream));
@@ -2172,6 +2281,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_HOST_BATCH_VOXELS")) h->host_batch_voxels = std::max<int64_t>(1, std::atoll(t));
     if (const char* t = std::getenv("CTWS_HOST_RAMP")) h->host_ramp = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PLATEAU_FILL")) h->plateau_fill = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_BASIN")) h->basin = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_MODE")) h->h2d_mode = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_WGS")) h->h2d_wgs = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_HOST_BATCH_BLOCKS")) h->host_batch_blocks = std::max(0, std::atoi(t));
@@ -2224,7 +2334,8 @@ void ctws_close(ctws_handle* h) {
                     h->rl_cnt.p, h->rl_offs.p, h->rl_out.p, h->rl_keys.p, h->rl_vals.p, h->rl_red.p,
                     h->edt_fh.p, h->edt_scratch.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
-                    h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p};
+                    h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p,
+                    w.fplat, w.plev, w.flake, w.bctl, h->basin_edges.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);

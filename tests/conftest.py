@@ -21,3 +21,17 @@ def gpu_handle():
     h = ctws.Handle(0)
     yield h
     h.close()
+
+
+def luigi_build(task, tmp_folder):
+    """luigi.build, and on failure the failed jobs' error logs in the assertion message."""
+    import glob
+    from cluster_tools_amd import luigi_compat as luigi
+    ok = luigi.build([task], local_scheduler=True)
+    if not ok:
+        msgs = []
+        for p in sorted(glob.glob(os.path.join(str(tmp_folder), 'error_logs', '*.err'))):
+            txt = open(p).read().strip()
+            if txt and 'amdgpu.ids' not in txt.splitlines()[-1]:
+                msgs.append('%s:\n%s' % (os.path.basename(p), txt[-2000:]))
+        raise AssertionError('workflow failed\n' + '\n'.join(msgs))

@@ -19,6 +19,8 @@ import sys
 import numpy as np
 import pytest
 
+from conftest import luigi_build
+
 from cluster_tools_amd import luigi_compat as luigi
 from cluster_tools_amd.utils import volume_utils as vu
 from cluster_tools_amd.utils.blocking import Blocking
@@ -138,7 +140,7 @@ def test_config1_reference_test_configs(tmp_path, name, two_pass):
     wf = WatershedWorkflow(input_path=inp, input_key='affinities', output_path=out, output_key='ws',
                            config_dir=cfg_dir, tmp_folder=str(tmp_path / 'tmp'), target='local',
                            max_jobs=1 if two_pass else 8, two_pass=two_pass)
-    assert luigi.build([wf], local_scheduler=True)
+    luigi_build(wf, tmp_path / 'tmp')
     with vu.file_reader(out, 'r') as f:
         res = f['ws'][:].astype('uint64')
         table = f['relabel_watershed'][:]

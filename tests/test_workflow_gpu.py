@@ -9,6 +9,8 @@ import sys
 import numpy as np
 import pytest
 
+from conftest import luigi_build
+
 from cluster_tools_amd import luigi_compat as luigi
 from cluster_tools_amd.utils import volume_utils as vu
 from cluster_tools_amd.utils.blocking import Blocking
@@ -72,16 +74,7 @@ def _oracle_volume(x, c, mask):
 
 
 def _build(task, tmp_folder):
-    """luigi.build, and on failure the failed jobs' error logs in the assertion message."""
-    import glob
-    ok = luigi.build([task], local_scheduler=True)
-    if not ok:
-        msgs = []
-        for p in sorted(glob.glob(os.path.join(str(tmp_folder), 'error_logs', '*.err'))):
-            txt = open(p).read().strip()
-            if txt and 'amdgpu.ids' not in txt.splitlines()[-1]:
-                msgs.append('%s:\n%s' % (os.path.basename(p), txt[-2000:]))
-        raise AssertionError('workflow failed\n' + '\n'.join(msgs))
+    luigi_build(task, tmp_folder)
 
 
 def _n_ids_and_ccs(res):
