@@ -132,7 +132,7 @@ struct ctws_handle {
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
-    int basin = 1;         // CTWS_BASIN=0: the open voxels by the frontier relaxation alone (k_basin.hip)
+    int basin = 0;         // CTWS_BASIN=1: the open voxels on the catchment graph (k_basin.hip) instead of the frontier relaxation
     DevBuf basin_edges;    // basin flood: catchment pairs (root, root, pass height)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel

@@ -127,15 +127,22 @@ _Pragma("unroll")
     }
 };
 
-// Phase 2a: C(root) from final neighbours (atomicMin), catchment pairs into the edge list.
+// Phase 2a: C(root) from final neighbours (atomicMin), catchment pairs into the edge list.  The
+// pairs of a workgroup collect in LDS and go out with one atomicAdd on the list length per
+// workgroup (one per wave and direction serialised on that one address: 59 ms per batch).
+constexpr int kEdgeStage = 2048;
 template <int ND>
 __global__ void __launch_bounds__(256) k_basin_edges(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                      const float* __restrict__ h, const uint32_t* __restrict__ par,
                                                      const uint64_t* __restrict__ open, const uint64_t* __restrict__ plat,
                                                      uint32_t* __restrict__ cr, uint4* __restrict__ edges,
                                                      uint32_t* __restrict__ ecnt, uint32_t ecap) {
+    __shared__ uint4 sbuf[kEdgeStage];
+    __shared__ uint32_t scnt, sbase;
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
+    if (threadIdx.x == 0) scnt = 0u;
+    __syncthreads();
     const gptr_t<float> hb = gbl(h + B.base);
     const gptr_t<uint32_t> pr = gbl(par + B.base);
     WORD_TILES(B.Z, B.Y, B.X, {
@@ -180,15 +187,32 @@ _Pragma("unroll")
                 const bool app = end && eb[k] != 0xFFFFFFFFu;
                 const uint64_t am = __ballot(app);
                 if (!am) continue;
+                const uint32_t n = (uint32_t)__popcll(am);
+                const uint32_t rank = (uint32_t)__popcll(am & ((1ull << lane) - 1ull));
                 uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(ecnt, (uint32_t)__popcll(am));
+                if (lane == 0) base = atomicAdd(&scnt, n);  // LDS
                 base = (uint32_t)__shfl((int)base, 0);
-                const uint32_t slot = base + (uint32_t)__popcll(am & ((1ull << lane) - 1ull));
-                if (app && slot < ecap)
-                    edges[slot] = make_uint4((uint32_t)(B.base + A), (uint32_t)(B.base + eb[k]), wm, 0u);
+                const bool to_lds = base + n <= (uint32_t)kEdgeStage;
+                const uint4 ev = make_uint4((uint32_t)(B.base + A), (uint32_t)(B.base + eb[k]), wm, 0u);
+                if (to_lds) {
+                    if (app) sbuf[base + rank] = ev;
+                } else {
+                    // stage full: straight out; the reserved stage slots get a self-pair (no effect)
+                    if (app && base + rank < (uint32_t)kEdgeStage) sbuf[base + rank] = make_uint4(0u, 0u, 0xFFFFFFFFu, 0u);
+                    uint32_t gb = 0;
+                    if (lane == 0) gb = atomicAdd(ecnt, n);
+                    gb = (uint32_t)__shfl((int)gb, 0);
+                    if (app && gb + rank < ecap) edges[gb + rank] = ev;
+                }
             }
         }
     })
+    __syncthreads();
+    const uint32_t ns = min(scnt, (uint32_t)kEdgeStage);
+    if (threadIdx.x == 0) sbase = ns ? atomicAdd(ecnt, ns) : 0u;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < ns; t += blockDim.x)
+        if (sbase + t < ecap) edges[sbase + t] = sbuf[t];
 }
 
 // Phase 2b: one Bellman-Ford sweep over the catchment pairs; flags[it] = a root's C changed.
