@@ -771,12 +771,13 @@ int run_basin(ctws_handle* h, const Plan& pl, int nb, int64_t T, int64_t TF, int
     add_timing(h, "basin_edges", (float)h->h_counter[0]);
     add_timing(h, "basin_sweeps", (float)it);
     if (!conv) return CTWS_OK;
+    k_basin_c<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, w.key);
     if (pl.nd_ws == 3)
-        k_basin_keys<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, w.key, w.flake,
-                                                    w.front0, w.bctl + 1);
+        k_basin_keys<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.fopen, w.key, w.flake, w.front0, w.bctl + 1);
     else
-        k_basin_keys<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, w.key, w.flake,
-                                                    w.front0, w.bctl + 1);
+        k_basin_keys<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.fopen, w.key, w.flake, w.front0, w.bctl + 1);
+    k_basin_lake_reset<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0, h->stream>>>(
+        w.desc, w.stat, w.flake, w.key);
     LAUNCHCHK();
     HIPCHK(hipMemcpyAsync(h->h_counter + 1, w.bctl + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));

@@ -162,9 +162,12 @@ template <int ND>
 __global__ void k_basin_edges(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint64_t*,
                               const uint64_t*, uint32_t*, uint4*, uint32_t*, uint32_t);
 __global__ void k_basin_relax(const uint4*, const uint32_t*, uint32_t, uint32_t*, uint32_t*, int);
+__global__ void k_basin_c(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint64_t*,
+                          const uint64_t*, const uint32_t*, uint64_t*);
 template <int ND>
-__global__ void k_basin_keys(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint64_t*,
-                             const uint64_t*, const uint32_t*, uint64_t*, uint64_t*, uint64_t*, uint32_t*);
+__global__ void k_basin_keys(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint64_t*,
+                             uint64_t*, uint64_t*, uint32_t*);
+__global__ void k_basin_lake_reset(const BlockDesc*, const BlockStat*, const uint64_t*, uint64_t*);
 template <int ND>
 __global__ void k_basin_tile(const BlockDesc*, const BlockStat*, const uint64_t*, const uint64_t*, const uint64_t*,
                              uint32_t*);

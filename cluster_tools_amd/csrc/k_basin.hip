@@ -143,35 +143,134 @@ __global__ void __launch_bounds__(256) k_basin_edges(const BlockDesc* __restrict
     if (!S[blockIdx.y].active) return;
     if (threadIdx.x == 0) scnt = 0u;
     __syncthreads();
+    // word columns as k_flood_verify: a unit is U vertically adjacent words of one 64-voxel column;
+    // its U + 2 rows of par / h / bitmap words are loaded once (all in flight) and serve as centre,
+    // upper and lower rows; x-neighbours are lane shuffles, lane 0 / 63 load the voxel beyond
+    constexpr int U = 4, R = U + 2, K = 2 * ND;
     const gptr_t<float> hb = gbl(h + B.base);
     const gptr_t<uint32_t> pr = gbl(par + B.base);
-    WORD_TILES(B.Z, B.Y, B.X, {
-        const uint64_t ow = gbl(open)[B.fbase + w_];
-        if (ow) {
-            const uint64_t pw = plat ? gbl(plat)[B.fbase + w_] : 0ull;
-            const bool me = valid && ((ow >> lane) & 1ull);
-            const WordNbrs<ND> N(B, open, plat, w_, wpr, z, y, xw, lane, ow, pw);
-            const uint32_t ic = me ? (uint32_t)i : 0u;
-            const uint32_t hq = ordf(hb[ic]);
-            const uint64_t* pbb = plat ? plat + B.fbase : nullptr;
-            uint32_t A = me ? basin_root(pr[ic], ic) : 0xFFFFFFFFu;
+    const uint64_t* ob = open + B.fbase;
+    const uint64_t* pbb = plat ? plat + B.fbase : nullptr;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const int wpr = (B.X + 63) >> 6;
+    const int ngy = (B.Y + U - 1) / U;
+    const int64_t nunits = (int64_t)B.Z * wpr * ngy;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t per = (nunits + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t ubeg = wid * per, uend = min(nunits, ubeg + per);
+    for (int64_t un = ubeg; un < uend; ++un) {
+        const int gy = (int)(un % ngy);
+        const int64_t strip = un / ngy;
+        const int xw = (int)(strip % wpr), z = (int)(strip / wpr);
+        const int y0 = gy * U;
+        const int64_t wrow0 = (int64_t)z * B.Y * wpr + xw;  // word of row y = 0 of the column
+        uint64_t ow[R], pw[R];
+        bool any = false;
+_Pragma("unroll")
+        for (int q = 0; q < R; ++q) {
+            const int yy = y0 - 1 + q;
+            const bool in = yy >= 0 && yy < B.Y;
+            ow[q] = in ? gbl(ob)[wrow0 + (int64_t)yy * wpr] : 0ull;
+            pw[q] = (in && pbb) ? gbl(pbb)[wrow0 + (int64_t)yy * wpr] : 0ull;
+            if (q >= 1 && q <= U) any |= ow[q] != 0ull;
+        }
+        if (!any) continue;
+        const int x = xw * 64 + lane;
+        const int xc = min(x, B.X - 1);
+        const int xe = lane == 0 ? max(xc - 1, 0) : min(xc + 1, B.X - 1);
+        const int64_t zb = (int64_t)z * YX;
+        uint32_t pv[R];
+        float hv[R];
+_Pragma("unroll")
+        for (int q = 0; q < R; ++q) {
+            const int yy = min(max(y0 - 1 + q, 0), B.Y - 1);
+            pv[q] = pr[zb + (int64_t)yy * B.X + xc];
+            hv[q] = hb[zb + (int64_t)yy * B.X + xc];
+        }
+        uint32_t pe[U], pzm[U], pzp[U];
+        float he[U], hzm[U], hzp[U];
+        uint64_t owe[U], pwe[U], owzm[U], pwzm[U], owzp[U], pwzp[U];
+_Pragma("unroll")
+        for (int u = 0; u < U; ++u) {
+            const int yy = min(y0 + u, B.Y - 1);
+            const int64_t ic = zb + (int64_t)yy * B.X + xc;
+            pe[u] = pr[zb + (int64_t)yy * B.X + xe];
+            he[u] = hb[zb + (int64_t)yy * B.X + xe];
+            // the bitmap word beyond the lane's word edge (lane 0: left, the others: right)
+            const int xwe = lane == 0 ? xw - 1 : xw + 1;
+            const bool ine = xwe >= 0 && xwe < wpr;
+            const int64_t we = (int64_t)z * B.Y * wpr + (int64_t)yy * wpr + (ine ? xwe : xw);
+            owe[u] = ine ? gbl(ob)[we] : 0ull;
+            pwe[u] = (ine && pbb) ? gbl(pbb)[we] : 0ull;
+            if (ND == 3) {
+                const int64_t wz = wrow0 + (int64_t)yy * wpr;
+                const int64_t sw = (int64_t)B.Y * wpr;
+                pzm[u] = pr[z > 0 ? ic - YX : ic];
+                pzp[u] = pr[z + 1 < B.Z ? ic + YX : ic];
+                hzm[u] = hb[z > 0 ? ic - YX : ic];
+                hzp[u] = hb[z + 1 < B.Z ? ic + YX : ic];
+                owzm[u] = z > 0 ? gbl(ob)[wz - sw] : 0ull;
+                owzp[u] = z + 1 < B.Z ? gbl(ob)[wz + sw] : 0ull;
+                pwzm[u] = (z > 0 && pbb) ? gbl(pbb)[wz - sw] : 0ull;
+                pwzp[u] = (z + 1 < B.Z && pbb) ? gbl(pbb)[wz + sw] : 0ull;
+            }
+        }
+_Pragma("unroll")
+        for (int u = 0; u < U; ++u) {
+            const int y = y0 + u;
+            const bool me = y < B.Y && x < B.X && ((ow[u + 1] >> lane) & 1ull);
+            const uint32_t i = (uint32_t)(zb + (int64_t)y * B.X + x);
+            // x-neighbours from the neighbouring lanes (every lane shuffles)
+            const uint32_t pxm = (uint32_t)__shfl_up((int)pv[u + 1], 1), pxp = (uint32_t)__shfl_down((int)pv[u + 1], 1);
+            const float hxm = __shfl_up(hv[u + 1], 1), hxp = __shfl_down(hv[u + 1], 1);
+            uint32_t A = me ? basin_root(pv[u + 1], i) : 0xFFFFFFFFu;
             const bool live = me && !in_plat(pbb, B, wpr, A);
             if (!live) A = 0xFFFFFFFFu;
+            const uint32_t hq = ordf(hv[u + 1]);
+            int cls[K];
+            uint32_t np[K], nj[K];
+            float nh[K];
+            cls[0] = x > 0 ? (lane > 0 ? nclass(ow[u + 1], pw[u + 1], lane - 1) : nclass(owe[u], pwe[u], 63)) : 2;
+            np[0] = lane > 0 ? pxm : pe[u];
+            nh[0] = lane > 0 ? hxm : he[u];
+            nj[0] = i - 1u;
+            cls[1] = x + 1 < B.X ? (lane < 63 ? nclass(ow[u + 1], pw[u + 1], lane + 1) : nclass(owe[u], pwe[u], 0)) : 2;
+            np[1] = lane < 63 ? pxp : pe[u];
+            nh[1] = lane < 63 ? hxp : he[u];
+            nj[1] = i + 1u;
+            cls[2] = y > 0 ? nclass(ow[u], pw[u], lane) : 2;
+            np[2] = pv[u];
+            nh[2] = hv[u];
+            nj[2] = i - (uint32_t)B.X;
+            cls[3] = y + 1 < B.Y ? nclass(ow[u + 2], pw[u + 2], lane) : 2;
+            np[3] = pv[u + 2];
+            nh[3] = hv[u + 2];
+            nj[3] = i + (uint32_t)B.X;
+            if (ND == 3) {
+                cls[4] = z > 0 ? nclass(owzm[u], pwzm[u], lane) : 2;
+                np[4] = pzm[u];
+                nh[4] = hzm[u];
+                nj[4] = i - (uint32_t)YX;
+                cls[5] = z + 1 < B.Z ? nclass(owzp[u], pwzp[u], lane) : 2;
+                np[5] = pzp[u];
+                nh[5] = hzp[u];
+                nj[5] = i + (uint32_t)YX;
+            }
             uint32_t mres = 0xFFFFFFFFu;
-            uint32_t eb[WordNbrs<ND>::K], ew[WordNbrs<ND>::K];
+            uint32_t eb[K], ew[K];
 _Pragma("unroll")
-            for (int k = 0; k < WordNbrs<ND>::K; ++k) {
+            for (int k = 0; k < K; ++k) {
                 eb[k] = 0xFFFFFFFFu;
                 ew[k] = 0xFFFFFFFFu;
-                const int c = live ? N.cls[k] : 2;
+                const int c = live ? cls[k] : 2;
                 if (c == 2) continue;
-                const uint32_t j = N.idx[k];
-                const uint32_t hp = ordf(hb[j]);
-                const uint32_t w2 = max(hq, hp);
+                const uint32_t w2 = max(hq, ordf(nh[k]));
                 if (c == 0) {
                     mres = min(mres, w2);
                 } else {
-                    const uint32_t Bj = basin_root(pr[j], j);
+                    const uint32_t Bj = basin_root(np[k], nj[k]);
                     if (Bj != A && !in_plat(pbb, B, wpr, Bj)) {
                         eb[k] = Bj;
                         ew[k] = w2;
@@ -182,7 +281,7 @@ _Pragma("unroll")
             const uint32_t m = run_min(A, 0u, mres, lane, end);
             if (end && live && m != 0xFFFFFFFFu) atomic_min_if(&cr[B.base + A], m);
 _Pragma("unroll")
-            for (int k = 0; k < WordNbrs<ND>::K; ++k) {
+            for (int k = 0; k < K; ++k) {
                 const uint32_t wm = run_min(A, eb[k], ew[k], lane, end);
                 const bool app = end && eb[k] != 0xFFFFFFFFu;
                 const uint64_t am = __ballot(app);
@@ -206,7 +305,7 @@ _Pragma("unroll")
                 }
             }
         }
-    })
+    }
     __syncthreads();
     const uint32_t ns = min(scnt, (uint32_t)kEdgeStage);
     if (threadIdx.x == 0) sbase = ns ? atomicAdd(ecnt, ns) : 0u;
@@ -234,70 +333,181 @@ __global__ void __launch_bounds__(256) k_basin_relax(const uint4* __restrict__ e
     if (__ballot(ch) && (threadIdx.x & 63) == 0) atomicOr(&flags[it], 1u);
 }
 
-// Phase 3: keys of the open voxels with d = 0 ((C, 0, 0); the label comes in phase 4), the lake
-// bitmap `lake` (open for the lake relaxation) and `chg` = every voxel outside it (its first
-// frontier: the lake voxels next to a key).  nlake[0] += lake voxels.
-template <int ND>
-__global__ void __launch_bounds__(256) k_basin_keys(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                    const float* __restrict__ h, const uint32_t* __restrict__ par,
-                                                    const uint64_t* __restrict__ open, const uint64_t* __restrict__ plat,
-                                                    const uint32_t* __restrict__ cr, uint64_t* __restrict__ key,
-                                                    uint64_t* __restrict__ lake, uint64_t* __restrict__ chg,
-                                                    uint32_t* __restrict__ nlake) {
+// Phase 3a: C of every open voxel, key (C, 0, 0) (INF for a catchment without a pass to a seed,
+// or whose root is a masked-plateau voxel).  Contiguous word ranges per wave, U words in flight
+// (the root's C is a dependent gather).
+__global__ void __launch_bounds__(256) k_basin_c(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                 const float* __restrict__ h, const uint32_t* __restrict__ par,
+                                                 const uint64_t* __restrict__ open, const uint64_t* __restrict__ plat,
+                                                 const uint32_t* __restrict__ cr, uint64_t* __restrict__ key) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
-    const gptr_t<float> hb = gbl(h + B.base);
+    constexpr int U = 4;
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
     const gptr_t<uint32_t> pr = gbl(par + B.base);
+    const gptr_t<float> hb = gbl(h + B.base);
     const gptr_t<uint32_t> crb = gbl(cr + B.base);
-    uint32_t cnt = 0;
-    WORD_TILES(B.Z, B.Y, B.X, {
-        const uint64_t ow = gbl(open)[B.fbase + w_];
-        const uint64_t vm = (B.X - xw * 64 >= 64) ? ~0ull : ((1ull << (B.X - xw * 64)) - 1ull);
-        uint64_t lw = 0ull;
-        if (ow) {
-            const uint64_t pw = plat ? gbl(plat)[B.fbase + w_] : 0ull;
-            const bool me = valid && ((ow >> lane) & 1ull);
-            const WordNbrs<ND> N(B, open, plat, w_, wpr, z, y, xw, lane, ow, pw);
-            const uint32_t ic = me ? (uint32_t)i : 0u;
-            const uint32_t hq = ordf(hb[ic]);
-            const uint64_t* pbb = plat ? plat + B.fbase : nullptr;
-            const uint32_t rq = basin_root(pr[ic], ic);
-            const uint32_t crq = (me && in_plat(pbb, B, wpr, rq)) ? 0xFFFFFFFFu : crb[rq];
-            uint32_t minc = 0xFFFFFFFFu;
+    const uint64_t* pbb = plat ? plat + B.fbase : nullptr;
+    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
+        uint64_t ow[U];
+        bool any = false;
 _Pragma("unroll")
-            for (int k = 0; k < WordNbrs<ND>::K; ++k) {
-                const int c = me ? N.cls[k] : 2;
-                if (c == 2) continue;
-                const uint32_t j = N.idx[k];
-                const uint32_t hp = ordf(hb[j]);
-                uint32_t cp = hp;
-                if (c == 1) {
-                    const uint32_t rj = basin_root(pr[j], j);
-                    cp = in_plat(pbb, B, wpr, rj) ? 0xFFFFFFFFu : max(hp, crb[rj]);
-                }
-                minc = min(minc, cp);
+        for (int u = 0; u < U; ++u) {
+            ow[u] = w0 + u < wend ? gbl(open)[B.fbase + w0 + u] : 0ull;
+            any |= ow[u] != 0ull;
+        }
+        if (!any) continue;
+        uint32_t gi[U], pv[U];
+        bool me[U];
+        float hv[U];
+_Pragma("unroll")
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = (w0 + u) / wpr;
+            const int x = (int)(w0 + u - row * wpr) * 64 + lane;
+            me[u] = ((ow[u] >> lane) & 1ull) && x < B.X;
+            gi[u] = me[u] ? (uint32_t)(row * B.X + x) : 0u;
+            pv[u] = pr[gi[u]];
+            hv[u] = hb[gi[u]];
+        }
+        uint32_t rt[U], cv[U];
+_Pragma("unroll")
+        for (int u = 0; u < U; ++u) {
+            rt[u] = basin_root(pv[u], gi[u]);
+            cv[u] = crb[rt[u]];
+        }
+_Pragma("unroll")
+        for (int u = 0; u < U; ++u) {
+            if (!me[u]) continue;
+            const bool dead = cv[u] == 0xFFFFFFFFu || in_plat(pbb, B, wpr, rt[u]);
+            key[B.base + gi[u]] = dead ? kPackInf : ((uint64_t)max(ordf(hv[u]), cv[u]) << 32);
+        }
+    }
+}
+
+// Phase 3b: the lake voxels (open, reached, h(q) <= min_p C(p)) -> the lake bitmap (the open set of
+// the lake relaxation), `chg` = every other voxel (its first changed set).  A stencil over the
+// keys of 3a (C of every voxel: h of a final one, INF at walls): word columns as k_flood_verify.
+// The lake keys are reset to INF afterwards (k_basin_lake_reset), not here: the neighbours still
+// read them.  nlake[0] += lake voxels.
+template <int ND>
+__global__ void __launch_bounds__(256) k_basin_keys(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                    const float* __restrict__ h, const uint64_t* __restrict__ open,
+                                                    const uint64_t* __restrict__ key, uint64_t* __restrict__ lake,
+                                                    uint64_t* __restrict__ chg, uint32_t* __restrict__ nlake) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    constexpr int U = 4, R = U + 2;
+    const gptr_t<uint64_t> k = gbl(key + B.base);
+    const gptr_t<float> hb = gbl(h + B.base);
+    const int64_t YX = (int64_t)B.Y * B.X;
+    const int wpr = (B.X + 63) >> 6;
+    const int ngy = (B.Y + U - 1) / U;
+    const int64_t nunits = (int64_t)B.Z * wpr * ngy;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t per = (nunits + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t ubeg = wid * per, uend = min(nunits, ubeg + per);
+    uint32_t cnt = 0;
+    for (int64_t un = ubeg; un < uend; ++un) {
+        const int gy = (int)(un % ngy);
+        const int64_t strip = un / ngy;
+        const int xw = (int)(strip % wpr), z = (int)(strip / wpr);
+        const int y0 = gy * U;
+        const uint64_t vm = (B.X - xw * 64 >= 64) ? ~0ull : ((1ull << (B.X - xw * 64)) - 1ull);
+        uint64_t ow[U], lw[U];
+        bool any = false;
+_Pragma("unroll")
+        for (int u = 0; u < U; ++u) {
+            ow[u] = y0 + u < B.Y ? gbl(open)[B.fbase + ((int64_t)z * B.Y + y0 + u) * wpr + xw] : 0ull;
+            any |= ow[u] != 0ull;
+            lw[u] = 0ull;
+        }
+        if (any) {
+            const int x = xw * 64 + lane;
+            const int xc = min(x, B.X - 1);
+            const int xe = lane == 0 ? max(xc - 1, 0) : min(xc + 1, B.X - 1);
+            const int64_t zb = (int64_t)z * YX;
+            uint64_t rk[R];
+_Pragma("unroll")
+            for (int q = 0; q < R; ++q) {
+                const int yy = min(max(y0 - 1 + q, 0), B.Y - 1);
+                rk[q] = k[zb + (int64_t)yy * B.X + xc];
             }
-            const uint32_t cq = max(hq, crq);
-            bool isl = false;
-            if (me) {
-                if (cq == 0xFFFFFFFFu) {
-                    // unreached catchment (no pass to a seed): stays INF
-                } else if (hq > minc) {
-                    key[B.base + i] = (uint64_t)cq << 32;
-                } else {
-                    isl = true;  // lake voxel: key from the lake relaxation
+            uint64_t ke[U], kzm[U], kzp[U];
+            float hv[U];
+_Pragma("unroll")
+            for (int u = 0; u < U; ++u) {
+                const int yy = min(y0 + u, B.Y - 1);
+                const int64_t ic = zb + (int64_t)yy * B.X + xc;
+                ke[u] = k[zb + (int64_t)yy * B.X + xe];
+                hv[u] = hb[ic];
+                if (ND == 3) {
+                    kzm[u] = k[z > 0 ? ic - YX : ic];
+                    kzp[u] = k[z + 1 < B.Z ? ic + YX : ic];
                 }
             }
-            lw = __ballot(isl);
+_Pragma("unroll")
+            for (int u = 0; u < U; ++u) {
+                const int y = y0 + u;
+                const bool valid = y < B.Y && x < B.X;
+                const uint64_t o = valid ? rk[u + 1] : kPackInf;
+                uint64_t l = shfl_up_u64(o, 1), r = shfl_down_u64(o, 1);
+                const uint64_t ker = shfl_u64(ke[u], 63);
+                if (lane == 0) l = (x > 0) ? ke[u] : kPackInf;
+                if (lane == 63) r = ker;
+                if (x + 1 >= B.X) r = kPackInf;
+                uint64_t m = min(l, r);
+                if (y > 0) m = min(m, rk[u]);
+                if (y + 1 < B.Y) m = min(m, rk[u + 2]);
+                if (ND == 3) {
+                    if (z > 0) m = min(m, kzm[u]);
+                    if (z + 1 < B.Z) m = min(m, kzp[u]);
+                }
+                const bool isl = valid && ((ow[u] >> lane) & 1ull) && o != kPackInf &&
+                                 ordf(hv[u]) <= (uint32_t)(m >> 32);
+                lw[u] = __ballot(isl);
+            }
         }
         if (lane == 0) {
-            lake[B.fbase + w_] = lw;
-            chg[B.fbase + w_] = ~lw & vm;
-            cnt += (uint32_t)__popcll(lw);
+_Pragma("unroll")
+            for (int u = 0; u < U; ++u) {
+                if (y0 + u >= B.Y) continue;
+                const int64_t w = ((int64_t)z * B.Y + y0 + u) * wpr + xw;
+                lake[B.fbase + w] = lw[u];
+                chg[B.fbase + w] = ~lw[u] & vm;
+                cnt += (uint32_t)__popcll(lw[u]);
+            }
         }
-    })
+    }
     cnt = wg_reduce_u32(cnt, OpAdd());
     if (threadIdx.x == 0 && cnt) atomicAdd(nlake, cnt);
+}
+
+// Phase 3c: the lake voxels' keys -> INF (the lake relaxation's starting point: upper bounds)
+__global__ void __launch_bounds__(256) k_basin_lake_reset(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                          const uint64_t* __restrict__ lake, uint64_t* __restrict__ key) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t nw = (int64_t)B.Z * B.Y * wpr;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t bits = lake[B.fbase + w];
+        if (!bits) continue;
+        const int64_t row = w / wpr;
+        const int xw = (int)(w - row * wpr);
+        while (bits) {
+            const int b = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            key[B.base + row * B.X + xw * 64 + b] = kPackInf;
+        }
+    }
 }
 
 // Phase 4a: parents by argmin (C, d) and their chains inside a tile (tile + 1-voxel halo of keys
@@ -510,12 +720,10 @@ template __global__ void k_basin_edges<2>(const BlockDesc*, const BlockStat*, co
                                           const uint64_t*, const uint64_t*, uint32_t*, uint4*, uint32_t*, uint32_t);
 template __global__ void k_basin_edges<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
                                           const uint64_t*, const uint64_t*, uint32_t*, uint4*, uint32_t*, uint32_t);
-template __global__ void k_basin_keys<2>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                         const uint64_t*, const uint64_t*, const uint32_t*, uint64_t*, uint64_t*,
-                                         uint64_t*, uint32_t*);
-template __global__ void k_basin_keys<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                         const uint64_t*, const uint64_t*, const uint32_t*, uint64_t*, uint64_t*,
-                                         uint64_t*, uint32_t*);
+template __global__ void k_basin_keys<2>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
+                                         const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
+template __global__ void k_basin_keys<3>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
+                                         const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
 template __global__ void k_basin_tile<2>(const BlockDesc*, const BlockStat*, const uint64_t*, const uint64_t*,
                                          const uint64_t*, uint32_t*);
 template __global__ void k_basin_tile<3>(const BlockDesc*, const BlockStat*, const uint64_t*, const uint64_t*,
