@@ -132,6 +132,7 @@ struct ctws_handle {
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
+    int output_tile = 1;   // CTWS_OUTPUT_TILE=0: cropped blocks through the word-tiled k_output
     int basin = 0;         // CTWS_BASIN=1: the open voxels on the catchment graph (k_basin.hip) instead of the frontier relaxation
     DevBuf basin_edges;    // basin flood: catchment pairs (root, root, pass height)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
@@ -1363,19 +1364,20 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         mark("descent_tile");
         if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
-        // basin flood (k_basin.hip): the descent also records every open voxel's catchment root
-        const bool basin = h->basin && packed;
-        k_descent_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
-                                                  w.front0, fst, basin ? (uint32_t*)w.A : nullptr);
-        LAUNCHCHK();
-        // masked blocks: their plateau leaves the open set until the rest is flooded (k_plateau.hip)
+        // masked blocks: their plateau leaves the open set until the rest is flooded (k_plateau.hip);
+        // the plateau level comes out of the descent pass
         bool any_mask = false;
         for (int i = 0; i < nb; ++i) any_mask |= desc[i].mask != nullptr;
         const bool plat_fill = h->plateau_fill && packed && any_mask;
+        if (plat_fill) HIPCHK(hipMemsetAsync(w.plev, 0, sizeof(uint32_t) * (size_t)nb, h->stream));
+        // basin flood (k_basin.hip): the descent also records every open voxel's catchment root
+        const bool basin = h->basin && packed;
+        k_descent_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
+                                                  w.front0, fst, basin ? (uint32_t*)w.A : nullptr,
+                                                  plat_fill ? w.plev : nullptr);
+        LAUNCHCHK();
         if (plat_fill) {
-            HIPCHK(hipMemsetAsync(w.plev, 0, sizeof(uint32_t) * (size_t)nb, h->stream));
             HIPCHK(hipMemsetAsync(w.fplat, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-            k_plat_level<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.fopen, w.plev);
             k_plat_mark<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.plev, w.fopen, w.fplat);
             LAUNCHCHK();
         }
@@ -1655,8 +1657,22 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         for (int i = 0; i < nb; ++i) any_plain |= desc[i].crop == 0;
         // uncropped blocks count their distinct ids in W (cropped blocks: n_cc of the crop CC)
         if (any_plain) HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-        k_output<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
-                                             (unsigned long long*)w.W);
+        // cropped blocks: one workgroup per crop-CC tile, labels through LDS (k_output_crop)
+        const bool crop_tiles = any_crop && h->output_tile;
+        if (any_plain || !crop_tiles)
+            k_output<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
+                                                 (unsigned long long*)w.W, crop_tiles ? 1 : 0);
+        if (crop_tiles) {
+            if (pl.nd_ws == 3) {
+                using T = CcTile<3>;
+                const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
+                k_output_crop<3><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0);
+            } else {
+                using T = CcTile<2>;
+                const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
+                k_output_crop<2><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0);
+            }
+        }
         if (any_plain) k_count_ids<<<dim3(64, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.W);
         LAUNCHCHK();
         mark("output");
@@ -2283,6 +2299,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_HOST_RAMP")) h->host_ramp = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PLATEAU_FILL")) h->plateau_fill = std::atoi(t);
     if (const char* t = std::getenv("CTWS_BASIN")) h->basin = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_OUTPUT_TILE")) h->output_tile = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_MODE")) h->h2d_mode = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_WGS")) h->h2d_wgs = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_HOST_BATCH_BLOCKS")) h->host_batch_blocks = std::max(0, std::atoi(t));

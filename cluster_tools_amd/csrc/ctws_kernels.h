@@ -92,7 +92,6 @@ __global__ void k_flatten_roots_w(const BlockDesc*, const BlockStat*, int, uint3
 __global__ void k_flatten_tile_roots(const BlockDesc*, const BlockStat*, uint32_t*, const uint64_t*, uint64_t*);
 
 // k_plateau.hip: the flood across a masked block's plateau (entries + min-plus run scans)
-__global__ void k_plat_level(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, uint32_t*);
 __global__ void k_plat_mark(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint64_t*);
 template <int ND>
 __global__ void k_plat_entry(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
@@ -108,7 +107,7 @@ __global__ void k_root_label(const BlockDesc*, const BlockStat*, int, uint32_t*,
 __global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const float*, uint32_t*, uint64_t*,
                              uint8_t*, int);
 __global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
-                         const uint32_t*, const uint32_t*, unsigned long long*);
+                         const uint32_t*, const uint32_t*, unsigned long long*, int);
 __global__ void k_count_ids(const BlockDesc*, BlockStat*, const uint64_t*);
 
 // k_tilecc.hip: LDS block-based union-find (plateaus, seed CC, halo-crop CC)
@@ -134,6 +133,8 @@ struct CcTile<2> {
 };
 template <int ND, int MODE>
 __global__ void k_tile_cc(const BlockDesc*, const BlockStat*, CcArgs, uint32_t*);
+template <int ND>
+__global__ void k_output_crop(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*);
 template <int ND, int MODE>
 __global__ void k_tile_merge(const BlockDesc*, const BlockStat*, CcArgs, uint32_t*);
 
@@ -152,7 +153,7 @@ template <int ND>
 __global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
                                uint32_t*);
 __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, uint32_t*, uint64_t*, uint8_t*,
-                               uint64_t*, uint64_t*, uint32_t*, uint32_t*);
+                               uint64_t*, uint64_t*, uint32_t*, uint32_t*, uint32_t*);
 template <int ND, int CW, int CY, int CZ>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,

@@ -754,10 +754,15 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
                                                       const float* __restrict__ h, uint32_t* __restrict__ par,
                                                       uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
                                                       uint64_t* __restrict__ open, uint64_t* __restrict__ chg,
-                                                      uint32_t* __restrict__ nopen, uint32_t* __restrict__ cr) {
+                                                      uint32_t* __restrict__ nopen, uint32_t* __restrict__ cr,
+                                                      uint32_t* __restrict__ plev) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     uint32_t cnt_open = 0;  // statistics (CTWS_TRACE): voxels left to the relaxation
+    // masked blocks (k_plateau.hip): the largest height of an open masked-out voxel (the plateau
+    // level, plev[block]; the plateau fill's k_plat_level folded into this pass)
+    const bool want_lev = plev && B.mask;
+    uint32_t lev = 0;
     // word tiles (a wave's ballot is exactly one word of the open / changed bitmaps), U words
     // per step: the U chains of a lane hop together, so U dependent-load latencies overlap
     constexpr int U = 4;
@@ -807,6 +812,7 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
             if (valid[u]) {
                 key[gi[u]] = res ? (((uint64_t)ordf(hv[u]) << 32) | (uint64_t)lr) : kPackInf;
                 fixedv[gi[u]] = res ? 1 : 0;
+                if (want_lev && !res && !gbl(B.mask)[gi[u] - B.base]) lev = max(lev, ordf(hv[u]));
                 if (cr && !res) {
                     if (e0[u] & kDescRes) cr[gi[u]] = 0xFFFFFFFFu;       // a root: no catchment pass yet
                     else if (last[u] != e0[u]) par[gi[u]] = last[u];  // -> its root
@@ -824,6 +830,10 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
     if (nopen) {
         cnt_open = wg_reduce_u32(cnt_open, OpAdd());
         if (threadIdx.x == 0 && cnt_open) atomicAdd(&nopen[blockIdx.y], cnt_open);
+    }
+    if (want_lev) {
+        lev = wg_reduce_u32(lev, OpMax());
+        if (threadIdx.x == 0 && lev) atomic_max_if(&plev[blockIdx.y], lev);
     }
 }
 
@@ -1214,7 +1224,25 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
     const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int64_t ubeg = wid * per, uend = min(nunits, ubeg + per);
     bool bad = false;
-    for (int64_t un = ubeg; un < uend; ++un) {
+    // 64 units at a time: lane l loads the open words of unit un0 + l, and only the units with an
+    // open voxel are visited (the regrow's open set is a few removed segments: most units skip)
+    for (int64_t un0 = ubeg; un0 < uend; un0 += 64) {
+      uint64_t lw[U];
+      {
+        const int64_t ul = un0 + lane;
+        const int gyl = (int)(ul % ngy);
+        const int64_t sl = ul / ngy;
+        const int xwl = (int)(sl % wpr), zl = (int)(sl / wpr);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            lw[u] = (ul < uend && gyl * U + u < B.Y) ? gbl(open)[B.fbase + ((int64_t)zl * B.Y + gyl * U + u) * wpr + xwl]
+                                                     : 0ull;
+      }
+      uint64_t todo = __ballot((lw[0] | lw[1] | lw[2] | lw[3]) != 0ull);
+      while (todo) {
+        const int src = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const int64_t un = un0 + src;
         const int gy = (int)(un % ngy);
         const int64_t strip = un / ngy;
         const int xw = (int)(strip % wpr), z = (int)(strip / wpr);
@@ -1222,12 +1250,7 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
         // open words of the unit's rows
         uint64_t ow[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            ow[u] = y0 + u < B.Y ? gbl(open)[B.fbase + ((int64_t)z * B.Y + y0 + u) * wpr + xw] : 0ull;
-        bool any = false;
-#pragma unroll
-        for (int u = 0; u < U; ++u) any |= ow[u] != 0ull;
-        if (!any) continue;  // every voxel of the unit descent-resolved / kept
+        for (int u = 0; u < U; ++u) ow[u] = shfl_u64(lw[u], src);
         const int x = xw * 64 + lane;
         const int xc = min(x, B.X - 1);
         const int xe = lane == 0 ? max(xc - 1, 0) : min(xc + 1, B.X - 1);
@@ -1293,6 +1316,7 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
                 }
             }
         }
+      }
     }
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }

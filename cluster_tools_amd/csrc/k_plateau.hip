@@ -12,7 +12,7 @@
 // a multi-source BFS.  The frontier relaxation crosses it one hop per local sweep (a plateau
 // hundreds of voxels wide costs tens of launches).  Here instead:
 //   1. P = the open voxels (not resolved by the descent) of height H = the largest height of an
-//      open masked voxel of the block (k_plat_level, k_plat_mark); P is taken out of the open
+//      open masked voxel of the block (k_descent_init's plev, k_plat_mark); P is taken out of the open
 //      set and the frontier floods the rest of the block first.
 //   2. entries: every P voxel gets f(min of its neighbours' keys) (k_plat_entry);
 //   3. min-plus scans along x, then y, then z restricted to runs of P voxels (k_plat_scan_x,
@@ -33,24 +33,6 @@ __device__ __forceinline__ uint64_t key_hops(uint64_t k, uint32_t n) {
     const uint32_t d = (uint32_t)((k & kDMask) >> kLabelBits);
     const uint32_t d2 = min(d + n, 4095u);
     return (k & ~kDMask) | ((uint64_t)d2 << kLabelBits);
-}
-
-// plev[b] = the largest ordered height of an open masked voxel of block b (0: none)
-__global__ void __launch_bounds__(256) k_plat_level(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                    const float* __restrict__ h, const uint64_t* __restrict__ open,
-                                                    uint32_t* __restrict__ plev) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || !B.mask) return;
-    uint32_t mx = 0;
-    WORD_TILES(B.Z, B.Y, B.X, {
-        const uint64_t ow = open[B.fbase + w_];
-        if (ow) {
-            const bool o = valid && ((ow >> lane) & 1ull);
-            if (o && !gbl(B.mask)[i]) mx = max(mx, ordf(h[B.base + i]));
-        }
-    })
-    mx = wg_reduce_u32(mx, OpMax());
-    if (threadIdx.x == 0 && mx) atomicMax(&plev[blockIdx.y], mx);
 }
 
 // P bitmap (zeroed beforehand) and open &= ~P
