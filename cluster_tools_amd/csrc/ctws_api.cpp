@@ -1659,9 +1659,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (any_plain) HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
         // cropped blocks: one workgroup per crop-CC tile, labels through LDS (k_output_crop)
         const bool crop_tiles = any_crop && h->output_tile;
-        if (any_plain || !crop_tiles)
-            k_output<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
-                                                 (unsigned long long*)w.W, crop_tiles ? 1 : 0);
+        // (k_output still writes the uncropped blocks and the empty ones: constant offset)
+        k_output<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
+                                             (unsigned long long*)w.W, crop_tiles ? 1 : 0);
         if (crop_tiles) {
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;

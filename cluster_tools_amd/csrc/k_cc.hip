@@ -359,9 +359,10 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
                                                 const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
                                                 int packed, const uint32_t* __restrict__ PFg,
                                                 const uint32_t* __restrict__ sb, const uint32_t* __restrict__ soff,
-                                                unsigned long long* W) {
+                                                unsigned long long* W, int skip_crop) {
     const BlockDesc& B = D[blockIdx.y];
     const bool active = S[blockIdx.y].active;
+    if (skip_crop && active && B.crop) return;  // k_output_crop writes it
     const uint32_t* P = PFg + B.ibase;
     const gwptr_t<uint64_t> out = gblw(B.out);
     uint32_t mx = 0;
@@ -418,6 +419,87 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
     if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);
     if (__ballot(zero_in) && (threadIdx.x & 63) == 0 && !S[blockIdx.y]._p[0]) atomicOr(&S[blockIdx.y]._p[0], 1u);
 }
+
+// k_output for the cropped blocks, one workgroup per crop-CC tile (CcTile): a member of a tile
+// component points at its tile root (k_tile_cc<.., CC_CROP>), the tile roots (bits of TR) at
+// their global root or carry the label (k_flatten_tile_roots, k_root_label).  The tile roots'
+// labels are resolved first (one dependent load each) into LDS, then every member reads its
+// root's label from LDS: no dependent global load per member (k_output: two).
+template <int ND>
+__global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict__ D, BlockStat* S,
+                                                     const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ TR) {
+    using T = CcTile<ND>;
+    constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, TN = TZ * TY * TX, PER = TN / 256;
+    __shared__ uint32_t sl[TN];
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active || !B.crop) return;
+    const int nz = B.IZ, ny = B.IY, nx = B.IX;
+    const int ntx = (nx + TX - 1) / TX, nty = (ny + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
+    const int t = blockIdx.x;
+    if (t >= ntx * nty * ntz) return;
+    const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
+    const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
+    const gptr_t<uint32_t> P = gbl(PFg + B.ibase);
+    uint32_t e[PER];
+    int64_t gi[PER];
+    bool in[PER], root[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int c = threadIdx.x + j * 256;
+        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+        const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
+        in[j] = z < nz && y < ny && x < nx;
+        gi[j] = ((int64_t)min(z, nz - 1) * ny + min(y, ny - 1)) * nx + min(x, nx - 1);
+        e[j] = P[gi[j]];
+        root[j] = (gbl(TR)[B.fbase + (gi[j] >> 6)] >> (gi[j] & 63)) & 1ull;
+    }
+    // tile roots: their label (a global root carries it; the others point at their global root)
+    uint32_t rl[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const bool need = in[j] && root[j] && e[j] != kNoParent && !(e[j] & kRootBit);
+        rl[j] = P[need ? e[j] : 0u];  // unconditional: all in flight
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (!(in[j] && root[j])) continue;
+        const uint32_t l = (e[j] & kRootBit) ? (e[j] & ~kRootBit) : (rl[j] & ~kRootBit);
+        sl[threadIdx.x + j * 256] = l;
+    }
+    __syncthreads();
+    const gwptr_t<uint64_t> out = gblw(B.out);
+    uint32_t mx = 0;
+    bool zero_in = false;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (!in[j]) continue;
+        uint32_t l = 0u;
+        if (e[j] != kNoParent) {
+            if (root[j]) {
+                l = sl[threadIdx.x + j * 256];
+            } else {
+                // member: its tile root lies in this tile
+                const uint32_t r = e[j];
+                const int rx = (int)(r % (uint32_t)nx), rr = (int)(r / (uint32_t)nx);
+                const int ry = rr % ny, rz = rr / ny;
+                l = sl[((rz - z0) * TY + (ry - y0)) * TX + (rx - x0)];
+            }
+        }
+        const int c = threadIdx.x + j * 256;
+        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+        const int64_t o = outer_of_inner(B, z0 + lz, y0 + ly, x0 + lx);
+        const bool inm = !B.mask || gbl(B.mask)[o];
+        mx = max(mx, l);
+        if (B.out32) gblw(B.out32)[gi[j]] = l;
+        else out[gi[j]] = inm ? (uint64_t)l + B.id_offset : (uint64_t)l;
+        zero_in |= inm && l == 0u;
+    }
+    mx = wg_reduce_u32(mx, OpMax());
+    if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);
+    if (__ballot(zero_in) && (threadIdx.x & 63) == 0 && !S[blockIdx.y]._p[0]) atomicOr(&S[blockIdx.y]._p[0], 1u);
+}
+template __global__ void k_output_crop<2>(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*);
+template __global__ void k_output_crop<3>(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*);
 
 // distinct ids of an uncropped block: popcount of its label bitmap (k_output) -> n_cc
 __global__ void __launch_bounds__(256) k_count_ids(const BlockDesc* __restrict__ D, BlockStat* S,

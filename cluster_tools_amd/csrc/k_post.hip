@@ -225,9 +225,11 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
             lb[u] = kv[u] == kInfKey ? 0u : (uint32_t)(kv[u] & kLab);
             cnt[u] = counts[B.base + lb[u]];
             ex[u] = excl ? excl[B.base + lb[u]] != 0 : false;
-            // the height only where a relaxed voxel may become a seed (descent-resolved voxels
-            // are seeds already; ~10 % of the voxels on config 3): words without one skip it
-            hv[u] = __ballot(valid[u] && !fx[u] && lb[u] != 0) ? h[gi[u]] : 0.0f;
+            // the height only where a relaxed voxel's key is not (h, 0, label) already: a key
+            // with d = 0 is (h, 0, label) (f resets to the voxel's own height), so only the
+            // voxels flooded over an equal-C plateau (d > 0: a few per cent of the relaxed ones)
+            // need it; words without one skip the load
+            hv[u] = __ballot(valid[u] && !fx[u] && lb[u] != 0 && (kv[u] & kDMask) != 0ull) ? h[gi[u]] : 0.0f;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -235,7 +237,7 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
             if (valid[u]) {
                 if (keep) {
                     if (!fx[u]) {
-                        key[gi[u]] = ((uint64_t)ordf(hv[u]) << 32) | (uint64_t)lb[u];
+                        if (kv[u] & kDMask) key[gi[u]] = ((uint64_t)ordf(hv[u]) << 32) | (uint64_t)lb[u];
                         fixedv[gi[u]] = 1;
                     }
                 } else {

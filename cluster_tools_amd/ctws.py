@@ -13,7 +13,8 @@ import numpy as np
 from ._abi import CtwsBlock, make_cfg, dtype_code, CTWS_OK, CTWS_BLOCK_FAILED, CTWS_BLOCK_WRITTEN  # noqa: F401
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libctws.so')
+# CTWS_LIB: another build of the library (A/B of build variants in one process tree)
+LIB_PATH = os.environ.get('CTWS_LIB') or os.path.join(_HERE, 'libctws.so')
 
 _lib = None
 _lock = threading.Lock()

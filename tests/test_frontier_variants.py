@@ -29,6 +29,8 @@ VARIANTS = {
     # the open voxels on the catchment graph instead of by the frontier relaxation (k_basin.hip)
     'basin': {'CTWS_BASIN': '1'},
     'basin_no_plateau_fill': {'CTWS_BASIN': '1', 'CTWS_PLATEAU_FILL': '0'},
+    # cropped blocks' uint64 output through the word-tiled k_output instead of k_output_crop
+    'output_words': {'CTWS_OUTPUT_TILE': '0'},
 }
 
 
