@@ -68,6 +68,7 @@ struct Workspace {
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
     uint64_t* fplat = nullptr;   // plateau fill (k_plateau.hip): the plateau voxels
     uint64_t* flake = nullptr;   // basin flood (k_basin.hip): the lake voxels
+    uint64_t* fseed = nullptr;   // seed CC members (the seed forest's parents are written for members only)
     uint32_t* bctl = nullptr;    // basin flood: [0] edges, [1] lake voxels, [2 + it] relax sweep it changed a root
     uint32_t* plev = nullptr;    // per block: the plateau height (0: none)
     uint32_t* fflags = nullptr;
@@ -133,6 +134,7 @@ struct ctws_handle {
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
     int output_tile = 1;   // CTWS_OUTPUT_TILE=0: cropped blocks through the word-tiled k_output
+    int fuse_localmax = 1; // CTWS_FUSE_LOCALMAX=0: 2-D local maxima by the separate k_localmax pass
     int basin = 0;         // CTWS_BASIN=1: the open voxels on the catchment graph (k_basin.hip) instead of the frontier relaxation
     DevBuf basin_edges;    // basin flood: catchment pairs (root, root, pass height)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
@@ -237,7 +239,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(sm, vox);
         ALLOC(hm, vox);
         ALLOC(cls, vox + 16);  // k_plateau_flag reads aligned 16-byte groups
-        ALLOC(P, vox + 4);   // + 4: 16-byte group reads (k_flatten_roots)
+        ALLOC(P, vox + 4);
         ALLOC(PF, vox + 4);
         ALLOC(lab, vox);
         ALLOC(key, vox);
@@ -285,6 +287,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(fopen, front);
         ALLOC(fplat, front);
         ALLOC(flake, front);
+        ALLOC(fseed, front);
         ALLOC(fchunk0, (front >> kChunkShift) + 1);
         ALLOC(fchunk1, (front >> kChunkShift) + 1);
         ALLOC(wl0, (front >> kChunkShift) + 1);
@@ -440,9 +443,13 @@ const GaussYxKernel kGaussYx[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_YX)};
 #undef CTWS_COL16
 #undef CTWS_COL8
 
+// lm_cls (2-D ws seed map): when the fused y + x tile kernel runs, it also writes the local-maximum
+// classes (k_localmax's) there and *lm_done is set
 int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, const float* src, float* dst,
-              int nb, int maxZ, int maxY, int maxX, HmapParams hp, int taps_slot) {
+              int nb, int maxZ, int maxY, int maxX, HmapParams hp, int taps_slot, uint8_t* lm_cls = nullptr,
+              bool* lm_done = nullptr) {
     Workspace& w = h->ws;
+    if (lm_done) *lm_done = false;
     int axes[3], na = 0;
     for (int a = (pl.nd_ws == 3 ? 0 : 1); a < 3; ++a)
         if (sig[a] > 0.0) axes[na++] = a;
@@ -477,12 +484,16 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
                 std::memcpy(htx, tx.data(), sizeof(double) * tx.size());
                 HIPCHK(hipMemcpyAsync(dtx, htx, sizeof(double) * tx.size(), hipMemcpyHostToDevice, h->stream));
                 const int TX = 128 - 2 * r;
-                const int64_t ntiles = (int64_t)maxZ * ((maxY + kGaussYxTY - 1) / kGaussYxTY) * ((maxX + TX - 1) / TX);
+                const bool lm = lm_cls && pl.nd_ws == 2 && !hmap_src;
+                const int SY = lm ? kGaussYxTY - 2 : kGaussYxTY, SX = lm ? TX - 2 : TX;  // tile stride
+                const int64_t ntiles = (int64_t)maxZ * ((maxY + SY - 1) / SY) * ((maxX + SX - 1) / SX);
                 dim3 g((unsigned)ntiles, nb);
                 hipLaunchKernelGGL(kGaussYx[r], g, dim3(256), 0, h->stream, w.desc, w.stat, gp.hmap_src, hp,
                                    (const double*)dtaps, (const double*)dtx, in, (const float*)w.dt,
-                                   (const uint32_t*)w.smin, (const uint32_t*)w.smax, dst);
+                                   (const uint32_t*)w.smin, (const uint32_t*)w.smax, dst, lm ? lm_cls : nullptr,
+                                   w.stat);
                 LAUNCHCHK();
+                if (lm_done) *lm_done = lm;
                 return CTWS_OK;
             }
         }
@@ -1235,11 +1246,13 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     // ---- seed map smoothing, hmap -----------------------------------------------------------
     HmapParams hp{(float)cfg->alpha, (float)(1.0 - cfg->alpha), pl.nd_ws == 2 ? 1 : 0};
     const float* seedmap = w.dt;
+    bool lm_done = false;  // the local maxima came out of the seed-map Gaussian's tiles
     if (pl.seeds_smooth) {
         bool any = false;
         for (int a = (pl.nd_ws == 3 ? 0 : 1); a < 3; ++a) any |= pl.sig_seeds[a] > 0.0;
         if (any) {
-            if ((r = run_gauss(h, pl, pl.sig_seeds, false, w.dt, w.sm, nb, maxZ, maxY, maxX, hp, 0)) != CTWS_OK)
+            if ((r = run_gauss(h, pl, pl.sig_seeds, false, w.dt, w.sm, nb, maxZ, maxY, maxX, hp, 0,
+                               h->fuse_localmax ? w.cls : nullptr, &lm_done)) != CTWS_OK)
                 return r;
             seedmap = w.sm;
         }
@@ -1254,11 +1267,13 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
     {
-        k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.smax);
+        if (!lm_done) k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.smax);
         LAUNCHCHK();
         // plateaus (equal-valued maxima candidates) and the seed CC: LDS tile union-find
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
-        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, nullptr};
+        // the seed CC's member bitmap (CcArgs::troot for SEED): its parents are members-only
+        HIPCHK(hipMemsetAsync(w.fseed, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed};
         if (pl.nd_ws == 3) {
             using T = CcTile<3>;
             const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
@@ -1279,7 +1294,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         LAUNCHCHK();
     }
     HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-    k_flatten_roots<<<vg4, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W);
+    k_flatten_seeds<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0, h->stream>>>(
+        w.desc, w.stat, w.PF, w.fseed, w.W);
     k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
@@ -1289,7 +1305,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
         HIPCHK(hipMemsetAsync(w.hkey, 0xFF, sizeof(uint64_t) * (size_t)TH, h->stream));
         HIPCHK(hipMemsetAsync(w.hpos, 0xFF, sizeof(uint32_t) * (size_t)TH, h->stream));
-        k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.sb, (const uint32_t*)h->p2_hint_dev.p, w.key);
+        k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.fseed, w.sb, (const uint32_t*)h->p2_hint_dev.p,
+                                               w.key);
         k_p2_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.hkey, w.hpos);
         HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
         const dim3 hg((unsigned)std::min<int64_t>((maxH + 255) / 256, 4096), nb);
@@ -1335,7 +1352,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     } else {
         // the descent flood reads the seeds from the CC parents directly (cc_seeds)
         if (!cc_seeds)
-            k_seed_label<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.hm, w.lab, w.key, w.cls, packed ? 1 : 0);
+            k_seed_label<<<rg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.fseed, w.hm, w.lab, w.key, w.cls,
+                                                    packed ? 1 : 0);
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
     }
     LAUNCHCHK();
@@ -1358,8 +1376,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
         const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
         {
-            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
-            else k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.P);
+            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
+            else k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
             LAUNCHCHK();
         }
         mark("descent_tile");
@@ -1463,7 +1481,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             }
             if (h->h_counter[0] && !h->no_fallback) {
                 fallback = 1;
-                k_flood_reset<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.key, w.cls);
+                k_flood_reset<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.key, w.cls);
                 LAUNCHCHK();
                 if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK)
                     return r;
@@ -2300,6 +2318,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_PLATEAU_FILL")) h->plateau_fill = std::atoi(t);
     if (const char* t = std::getenv("CTWS_BASIN")) h->basin = std::atoi(t);
     if (const char* t = std::getenv("CTWS_OUTPUT_TILE")) h->output_tile = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FUSE_LOCALMAX")) h->fuse_localmax = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_MODE")) h->h2d_mode = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_WGS")) h->h2d_wgs = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_HOST_BATCH_BLOCKS")) h->host_batch_blocks = std::max(0, std::atoi(t));
@@ -2353,7 +2372,7 @@ void ctws_close(ctws_handle* h) {
                     h->edt_fh.p, h->edt_scratch.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
                     h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p,
-                    w.fplat, w.plev, w.flake, w.bctl, h->basin_edges.p};
+                    w.fplat, w.plev, w.flake, w.fseed, w.bctl, h->basin_edges.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);

@@ -172,6 +172,13 @@ __device__ __forceinline__ void uf_union_scan(uint32_t* P, uint32_t a, uint32_t 
     }
 }
 
+// voxel i of block B (outer C index) in a per-row-word bitmap (the frontier layout at fbase)
+__device__ __forceinline__ bool bit_of(const uint64_t* bits, const BlockDesc& B, int64_t i) {
+    const int64_t row = i / B.X;
+    const int x = (int)(i - row * B.X);
+    return (bits[B.fbase + row * ((B.X + 63) >> 6) + (x >> 6)] >> (x & 63)) & 1ull;
+}
+
 // label of a CC member from its parent slot p = P[i] after k_root_label (0: background)
 __device__ __forceinline__ uint32_t cc_label(const uint32_t* P, uint32_t p) {
     if (p == kNoParent) return 0u;

@@ -82,14 +82,13 @@ __global__ void k_gauss_row_r(const BlockDesc*, const BlockStat*, GaussParams, H
 constexpr int kGaussYxTY = 32;
 template <int R>
 __global__ void k_gauss_yx(const BlockDesc*, const BlockStat*, int, HmapParams, const double*, const double*,
-                           const float*, const float*, const uint32_t*, const uint32_t*, float*);
+                           const float*, const float*, const uint32_t*, const uint32_t*, float*, uint8_t*, BlockStat*);
 
 // k_cc.hip
 __global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, const uint32_t*);
 __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uint32_t*);
-__global__ void k_flatten_roots(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
-__global__ void k_flatten_roots_w(const BlockDesc*, const BlockStat*, int, uint32_t*, uint64_t*);
 __global__ void k_flatten_tile_roots(const BlockDesc*, const BlockStat*, uint32_t*, const uint64_t*, uint64_t*);
+__global__ void k_flatten_seeds(const BlockDesc*, const BlockStat*, uint32_t*, const uint64_t*, uint64_t*);
 
 // k_plateau.hip: the flood across a masked block's plateau (entries + min-plus run scans)
 __global__ void k_plat_mark(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint64_t*);
@@ -104,8 +103,8 @@ __global__ void k_bitmap_csum(const BlockDesc*, const BlockStat*, int, const uin
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
 __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uint64_t*, const uint32_t*, uint32_t*);
 __global__ void k_root_label(const BlockDesc*, const BlockStat*, int, uint32_t*, const uint64_t*, const uint32_t*);
-__global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const float*, uint32_t*, uint64_t*,
-                             uint8_t*, int);
+__global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const float*,
+                             uint32_t*, uint64_t*, uint8_t*, int);
 __global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
                          const uint32_t*, const uint32_t*, unsigned long long*, int);
 __global__ void k_count_ids(const BlockDesc*, BlockStat*, const uint64_t*);
@@ -119,7 +118,9 @@ struct CcArgs {
     const uint32_t* lab;   // CROP: flood labels (non-packed)
     const uint64_t* key;   // CROP: packed keys
     int packed;            // CROP
-    uint64_t* troot;       // CROP: tile-root bitmap (inner C index, per block at fbase), zeroed
+    uint64_t* troot;       // CROP: tile-root bitmap (inner C index, per block at fbase), zeroed;
+                           // SEED: the members (seed voxels; outer rows), zeroed.  The seed forest's
+                           // parents are written for members only: readers test this bitmap first
 };
 template <int ND>
 struct CcTile;
@@ -151,7 +152,7 @@ constexpr int kStatSlots = 64;  // flood statistics: counter[4 + slot * 4 + k]  
 __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
 template <int ND>
 __global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
-                               uint32_t*);
+                               const uint64_t*, uint32_t*);
 __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, uint32_t*, uint64_t*, uint8_t*,
                                uint64_t*, uint64_t*, uint32_t*, uint32_t*, uint32_t*);
 template <int ND, int CW, int CY, int CZ>
@@ -205,7 +206,7 @@ __global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*,
                                uint32_t*, uint64_t*);
 constexpr int kWordWaves = 4;  // waves per workgroup of the word-tiled kernels
 __global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
-                              uint64_t*, uint8_t*);
+                              const uint64_t*, uint64_t*, uint8_t*);
 
 // k_post.hip
 __global__ void k_slice_seed_base(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint32_t*);
@@ -231,8 +232,8 @@ __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t
 
 // k_pass2.hip (two-pass watershed, pass 2)
 __global__ void k_p2_zero_dt(const BlockDesc*, const BlockStat*, float*);
-__global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, const uint32_t*,
-                            uint64_t*);
+__global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
+                            const uint32_t*, uint64_t*);
 __global__ void k_p2_insert(const BlockDesc*, BlockStat*, const uint64_t*, uint64_t*, uint32_t*);
 __global__ void k_p2_roots(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint64_t*);
 __global__ void k_p2_label(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, const uint64_t*,

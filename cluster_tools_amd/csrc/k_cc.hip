@@ -325,15 +325,15 @@ __global__ void __launch_bounds__(256) k_root_label(const BlockDesc* __restrict_
 // ---- seed labels + flood initialisation --------------------------------------------------
 // labels = vigra label (| kFixedBit: seed), keys = (ordf(h) << 32) for seeds, INF otherwise.
 __global__ void __launch_bounds__(256) k_seed_label(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                    const uint32_t* __restrict__ PFg, const float* __restrict__ h,
-                                                    uint32_t* __restrict__ lab, uint64_t* __restrict__ key,
-                                                    uint8_t* __restrict__ fixedv, int packed) {
+                                                    const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ sbits,
+                                                    const float* __restrict__ h, uint32_t* __restrict__ lab,
+                                                    uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv, int packed) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const uint32_t* P = PFg + B.base;
     ROW_TILES(B.Z, B.Y, B.X, {
         const int64_t gi = B.base + i;
-        const uint32_t l = cc_label(P, P[i]);
+        const uint32_t l = bit_of(sbits, B, i) ? cc_label(P, P[i]) : 0u;
         uint64_t k = kInfKey;
         if (l) k = ((uint64_t)ordf(h[gi]) << 32) | (packed ? (uint64_t)l : 0ull);
         lab[gi] = l ? (l | kFixedBit) : 0u;
@@ -515,43 +515,6 @@ __global__ void __launch_bounds__(256) k_count_ids(const BlockDesc* __restrict__
     if (threadIdx.x == 0 && c) atomicAdd(&st.n_cc, c);
 }
 
-// point every element of a union-find forest directly at its root; roots set their scan-key
-// bit in the root bitmap W (zeroed beforehand).  Most entries are kNoParent or point at their
-// root already and cost only their load, so the pass streams the parent array 16 bytes per
-// lane: a thread takes an aligned group of 4 entries (global index), the entries outside the
-// block are skipped.
-__global__ void __launch_bounds__(256) k_flatten_roots(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
-                                                       uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || (inner && !B.crop)) return;
-    const int64_t base = inner ? B.ibase : B.base;
-    const int64_t n = inner ? B.NI : B.N;
-    uint32_t* P = PFg + base;
-    uint64_t* W = Wg + B.wbase;
-    const int ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
-    const int64_t g0 = base >> 2, g1 = (base + n + 3) >> 2;
-    const uint4* P4 = reinterpret_cast<const uint4*>(PFg);
-    for (int64_t g = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < g1; g += (int64_t)gridDim.x * blockDim.x) {
-        const uint4 q = P4[g];
-        const uint32_t pv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t i = g * 4 + k - base;  // block index
-            const uint32_t p = pv[k];
-            if (i < 0 || i >= n || p == kNoParent) continue;
-            if (p == (uint32_t)i) {
-                const int64_t row = i / nx;
-                const int x = (int)(i - row * nx), z = (int)(row / ny), y = (int)(row - (int64_t)z * ny);
-                const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
-                atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
-            } else {
-                const uint32_t r = uf_find(P, p);
-                if (r != p) P[i] = r;
-            }
-        }
-    }
-}
-
 // Crop CC: only the tile roots (bits of the tile-root bitmap TR, set by k_tile_cc<.., CC_CROP>)
 // are pointed at their global root; members keep pointing at their tile root, and k_output
 // follows member -> tile root -> root.  Global roots set their scan-key bit in W (zeroed).
@@ -584,55 +547,36 @@ __global__ void __launch_bounds__(256) k_flatten_tile_roots(const BlockDesc* __r
     }
 }
 
-// k_flatten_roots for dense forests (the crop CC: nearly every voxel a member, so nearly
-// every entry a find): word tiles, more threads in flight per voxel.  Points every element at
-// its root; roots set their scan-key
-// bit in the root bitmap W (zeroed beforehand).  Word tiles (wtg / wtig grid), U words per
-// step with their parent loads in flight together; most voxels are kNoParent or point at
-// their root already and cost the one load.
-__global__ void __launch_bounds__(256) k_flatten_roots_w(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
-                                                       uint32_t* __restrict__ PFg, uint64_t* __restrict__ Wg) {
+// The seed forest (k_tile_cc<.., CC_SEED> writes its members only): every member is pointed at
+// its root, roots set their scan-key bit in W (zeroed).  One thread per member-bitmap word: the
+// seeds are ~1 % of the voxels, the non-members are not read at all.
+__global__ void __launch_bounds__(256) k_flatten_seeds(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                       uint32_t* __restrict__ PFg, const uint64_t* __restrict__ bits,
+                                                       uint64_t* __restrict__ Wg) {
     const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active || (inner && !B.crop)) return;
-    uint32_t* P = PFg + (inner ? B.ibase : B.base);
+    if (!S[blockIdx.y].active) return;
+    uint32_t* P = PFg + B.base;
     uint64_t* W = Wg + B.wbase;
-    const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
-    constexpr int U = 4;
-    const int wpr = (nx + 63) >> 6;
-    const int64_t nwords = (int64_t)nz * ny * wpr;
-    const int lane = threadIdx.x & 63;
-    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const int64_t per = (nwords + nwaves - 1) / nwaves;
-    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
-    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
-        uint32_t pv[U];
-        int64_t ii[U];
-        int xx[U], yy[U], zz[U];
-        bool valid[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t wu = min(w0 + u, wend - 1);
-            const int64_t row = wu / wpr;
-            const int xw = (int)(wu - row * wpr);
-            zz[u] = (int)(row / ny);
-            yy[u] = (int)(row - (int64_t)zz[u] * ny);
-            xx[u] = xw * 64 + lane;
-            valid[u] = w0 + u < wend && xx[u] < nx;
-            ii[u] = row * nx + min(xx[u], nx - 1);
-            pv[u] = gbl(P)[ii[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!valid[u]) continue;
-            const uint32_t p = pv[u];
-            if (p == (uint32_t)ii[u]) {
-                const int z = zz[u], y = yy[u], x = xx[u];
-                const uint32_t f = inner ? (uint32_t)(z + B.IZ * (y + B.IY * x)) : scan_key_of(B, z, y, x);
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t nw = (int64_t)B.Z * B.Y * wpr;
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t m = bits[B.fbase + w];
+        if (!m) continue;
+        const int64_t row = w / wpr;
+        const int xw = (int)(w - row * wpr);
+        const int z = (int)(row / B.Y), y = (int)(row - (int64_t)z * B.Y);
+        while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            const int x = xw * 64 + b;
+            const uint32_t i = (uint32_t)(row * B.X + x);
+            const uint32_t p = P[i];
+            if (p == i) {
+                const uint32_t f = scan_key_of(B, z, y, x);
                 atomicOr((unsigned long long*)&W[f >> 6], 1ull << (f & 63));
-            } else if (p != kNoParent) {
+            } else {
                 const uint32_t r = uf_find(P, p);
-                if (r != p) P[ii[u]] = r;
+                if (r != p) P[i] = r;
             }
         }
     }

@@ -544,7 +544,7 @@ namespace ctws {
 // seed test / seed label: from the seed CC parents (pass 1: `cc` = PF after k_root_label) or,
 // when cc is null, from lab (kFixedBit; pass 2 and the fallbacks)
 __device__ __forceinline__ uint32_t seed_label(const uint32_t* lab, const uint32_t* cc, int64_t base, uint32_t r) {
-    if (cc) return cc_label(cc + base, cc[base + r]);
+    if (cc) return cc_label(cc + base, cc[base + r]);  // (a member: the caller tested the member bitmap)
     const uint32_t l = lab[base + r];
     return (l & kFixedBit) ? (l & ~kFixedBit) : 0u;
 }
@@ -566,7 +566,8 @@ struct DTile<2> {
 template <int ND>
 __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_eu(ND == 2 ? 8 : 6, 8))) k_descent_tile(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint32_t* __restrict__ lab,
-                                                      const uint32_t* __restrict__ cc, uint32_t* __restrict__ exitp) {
+                                                      const uint32_t* __restrict__ cc, const uint64_t* __restrict__ sbits,
+                                                      uint32_t* __restrict__ exitp) {
     using T = DTile<ND>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, HZ = T::HZ, HY = TY + 2, HX = TX + 2;
     constexpr int HN = HZ * HY * HX, TN = TZ * TY * TX;
@@ -590,7 +591,10 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
     // seed entries of the thread's voxels (cc parent or lab), then the halo heights: every load
     // unconditional (clamped index, global address space) so that all of them are in flight
     // together; out-of-block values are selected away afterwards
+    // cc (the seed forest): members only; their bits in sbits (one word per tile row and lane
+    // group), the forest entry loaded for the members alone
     const uint32_t* sdsrc = cc ? cc : lab;
+    const int wprs = (B.X + 63) >> 6;
     uint32_t inm = 0, seedm = 0;
     uint32_t sv[PER];
 #pragma unroll
@@ -599,7 +603,11 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = min(z0 + lz, B.Z - 1), gy = min(y0 + ly, B.Y - 1), gx = min(x0 + lx, B.X - 1);
         inm |= ((z0 + lz < B.Z && y0 + ly < B.Y && x0 + lx < B.X) ? 1u : 0u) << k;
-        sv[k] = gbl(sdsrc)[B.base + gz * YX + (int64_t)gy * B.X + gx];
+        // both loads unconditional, in flight with the halo's: a non-member's forest entry is
+        // stale and selected away by its bit
+        const uint64_t bw = cc ? gbl(sbits)[B.fbase + ((int64_t)gz * B.Y + gy) * wprs + (gx >> 6)] : ~0ull;
+        const uint32_t e = gbl(sdsrc)[B.base + gz * YX + (int64_t)gy * B.X + gx];
+        sv[k] = ((bw >> (gx & 63)) & 1ull) ? e : kNoParent;
     }
     {
         constexpr int NH = (HN + NT - 1) / NT;
@@ -738,9 +746,9 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
     }
 }
 template __global__ void k_descent_tile<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                           const uint32_t*, uint32_t*);
+                                           const uint32_t*, const uint64_t*, uint32_t*);
 template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                           const uint32_t*, uint32_t*);
+                                           const uint32_t*, const uint64_t*, uint32_t*);
 
 // voxels whose descent ends in a seed get their final key, fixed; the others wait for the
 // flood (INF key).  Bitmaps, one word per 64 voxels of a row (the 64 lanes of a wave cover
@@ -1328,12 +1336,12 @@ template __global__ void k_flood_verify<2>(const BlockDesc*, const BlockStat*, c
 // seeds only (fallback after a failed verification)
 __global__ void __launch_bounds__(256) k_flood_reset(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                      const float* __restrict__ h, const uint32_t* __restrict__ lab,
-                                                     const uint32_t* __restrict__ cc, uint64_t* __restrict__ key,
-                                                     uint8_t* __restrict__ fixedv) {
+                                                     const uint32_t* __restrict__ cc, const uint64_t* __restrict__ sbits,
+                                                     uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t l = seed_label(lab, cc, B.base, (uint32_t)i);
+        const uint32_t l = (!cc || bit_of(sbits, B, i)) ? seed_label(lab, cc, B.base, (uint32_t)i) : 0u;
         key[B.base + i] = l ? (((uint64_t)ordf(h[B.base + i]) << 32) | (uint64_t)l) : kPackInf;
         fixedv[B.base + i] = l ? 1 : 0;
     }

@@ -86,7 +86,8 @@ __global__ void __launch_bounds__(256) k_p2_zero_dt(const BlockDesc* __restrict_
 // per-voxel relabel key (kEmptyKey: unlabelled); written into `vkey`.  `hint` (2-D, blocks with
 // B.p2hint >= 0): the slice offsets of the previous run, new seeds keyed by their uint32 value
 __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                   const uint32_t* __restrict__ PFg, const uint32_t* __restrict__ sb,
+                                                   const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ sbits,
+                                                   const uint32_t* __restrict__ sb,
                                                    const uint32_t* __restrict__ hint, uint64_t* __restrict__ vkey) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
@@ -102,7 +103,7 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
             if ((uint32_t)u != 0)
                 k = (B.nd_ws == 3) ? (uint64_t)(uint32_t)u : (((uint64_t)z << 33) | kInitTag | (uint32_t)u);
         } else if (!B.mask || gbl(B.mask)[i]) {
-            const uint32_t gl = cc_label(PF, PF[i]);  // seed label (0: background)
+            const uint32_t gl = bit_of(sbits, B, i) ? cc_label(PF, PF[i]) : 0u;  // seed label (0: background)
             if (gl) {
                 if (B.nd_ws == 3) {
                     const uint32_t v = gl + (uint32_t)B.id_offset;  // wraps to 0: background

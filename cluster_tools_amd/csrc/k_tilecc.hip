@@ -18,7 +18,7 @@
 // The tile writes each member's global parent = its tile root (C-order block index), non-
 // members get kNoParent.  k_tile_merge then unions the tile roots across the tile faces with
 // the global (scan-key ordered) union-find; only face pairs whose local roots differ from the
-// previous lane's pair reach the atomics.  k_flatten_roots (k_cc.hip) finishes as before.
+// previous lane's pair reach the atomics.  k_flatten_seeds / k_flatten_tile_roots (k_cc.hip) finish.
 #include "ctws_kernels.h"
 
 namespace ctws {
@@ -171,7 +171,22 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             } else {
                 const int64_t i = B.base + ((int64_t)cz * B.Y + cy) * B.X + cx;
                 l0[j] = gbl(a.cls)[i];
-                l1[j] = MODE == CC_PLATEAU ? __float_as_uint(gbl(a.v)[i]) : 0u;
+                l1[j] = 0u;
+            }
+        }
+        if (MODE == CC_PLATEAU) {
+            // a tile without plateau voxels writes nothing (P is read only at plateau voxels:
+            // cc_is_max, k_plateau_flag, k_tile_merge check cls first) and skips the value loads
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) any |= ((inm >> j) & 1u) && (l0[j] & 2);
+            if (!__syncthreads_or(any)) return;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int c = threadIdx.x + j * 256;
+                const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
+                const int cz = min(z0 + lz, nz - 1), cy = min(y0 + ly, ny - 1), cx = min(x0 + lx, nx - 1);
+                l1[j] = (l0[j] & 2) ? __float_as_uint(gbl(a.v)[B.base + ((int64_t)cz * B.Y + cy) * B.X + cx]) : 0u;
             }
         }
 #pragma unroll
@@ -197,14 +212,6 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             }
             vv[j] = ((inm >> j) & 1u) ? v : kLNone;
         }
-    }
-    if (MODE == CC_PLATEAU) {
-        // a tile without plateau voxels writes nothing: P is read only at plateau voxels
-        // (cc_is_max, k_plateau_flag, k_tile_merge checks cls first)
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < PER; ++j) any |= vv[j] != kLNone;
-        if (!__syncthreads_or(any)) return;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) sv[threadIdx.x + j * 256] = vv[j];
@@ -249,13 +256,29 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
         }
     }
     __syncthreads();
-    // members -> global parent = C-order block index of the tile root
+    // members -> global parent = C-order block index of the tile root.  SEED: members only (the
+    // seed voxels are ~1 %), plus their bits in the member bitmap (a.troot): the readers of the
+    // seed forest test the bitmap first, and the stores of kNoParent (4 B per voxel) go away
     uint32_t* P = Pg + (MODE == CC_CROP ? B.ibase : B.base);
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const int c = threadIdx.x + j * 256;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
+        if (MODE == CC_SEED) {
+            // a wave's 64 positions are whole tile rows (TX = 64, or two rows of 32): one word
+            // (or two halves) of the member bitmap
+            const bool mem = z < nz && y < ny && x < nx && vv[j] != kLNone;
+            const uint64_t bm = __ballot(mem);
+            if ((lane == 0 || lane == TX) && bm) {
+                const uint64_t part = TX == 64 ? bm : ((lane == 0 ? bm : bm >> 32) & 0xFFFFFFFFull);
+                const int wpr = (nx + 63) >> 6;
+                if (part && z < nz && y < ny)
+                    atomicOr((unsigned long long*)&a.troot[B.fbase + ((int64_t)z * ny + y) * wpr + (x0 >> 6)],
+                             (unsigned long long)(part << (x0 & 63)));
+            }
+            if (!mem) continue;
+        }
         if (z >= nz || y >= ny || x >= nx) continue;
         uint32_t g = kNoParent;
         const int64_t gi = ((int64_t)z * ny + y) * nx + x;
@@ -310,8 +333,10 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                 const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
                 if (z < nz && y < ny && x < nx) {
                     const int64_t i = ((int64_t)z * ny + y) * nx + x;
-                    // PLATEAU: tiles without plateau voxels leave P unwritten
-                    const bool mi = MODE != CC_PLATEAU || (a.cls[B.base + i] & 2);
+                    // PLATEAU: tiles without plateau voxels leave P unwritten; SEED: P holds
+                    // the members only (the member bitmap a.troot says which)
+                    const bool mi = MODE == CC_SEED ? bit_of(a.troot, B, i)
+                                                    : (MODE != CC_PLATEAU || (a.cls[B.base + i] & 2));
                     const uint32_t pi = mi ? P[i] : kNoParent;
                     if (pi != kNoParent) {
                         // the backward neighbours of (z, y, x) that leave the tile through face f
@@ -325,6 +350,7 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                             if (!out || qz < 0 || qy < 0 || qx < 0 || qx >= nx) continue;
                             const int64_t q = ((int64_t)qz * ny + qy) * nx + qx;
                             if (MODE == CC_PLATEAU && !(a.cls[B.base + q] & 2)) continue;
+                            if (MODE == CC_SEED && !bit_of(a.troot, B, q)) continue;
                             const uint32_t pq = P[q];
                             if (pq == kNoParent) continue;
                             if (MODE != CC_SEED &&
