@@ -591,10 +591,12 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
     // seed entries of the thread's voxels (cc parent or lab), then the halo heights: every load
     // unconditional (clamped index, global address space) so that all of them are in flight
     // together; out-of-block values are selected away afterwards
-    // cc (the seed forest): members only; their bits in sbits (one word per tile row and lane
-    // group), the forest entry loaded for the members alone
+    // cc (the seed forest): members only, their bits in sbits; the tile's bitmap rows (a 32-bit
+    // half word per TX <= 32 voxels of a row) go to LDS with the halo, the entries are loaded
+    // unconditionally (a non-member's entry is stale and selected away by its bit)
+    constexpr int WPR32 = (TX + 31) / 32, NW32 = TZ * TY * WPR32;
+    __shared__ uint32_t sbm[NW32];
     const uint32_t* sdsrc = cc ? cc : lab;
-    const int wprs = (B.X + 63) >> 6;
     uint32_t inm = 0, seedm = 0;
     uint32_t sv[PER];
 #pragma unroll
@@ -603,11 +605,15 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = min(z0 + lz, B.Z - 1), gy = min(y0 + ly, B.Y - 1), gx = min(x0 + lx, B.X - 1);
         inm |= ((z0 + lz < B.Z && y0 + ly < B.Y && x0 + lx < B.X) ? 1u : 0u) << k;
-        // both loads unconditional, in flight with the halo's: a non-member's forest entry is
-        // stale and selected away by its bit
-        const uint64_t bw = cc ? gbl(sbits)[B.fbase + ((int64_t)gz * B.Y + gy) * wprs + (gx >> 6)] : ~0ull;
-        const uint32_t e = gbl(sdsrc)[B.base + gz * YX + (int64_t)gy * B.X + gx];
-        sv[k] = ((bw >> (gx & 63)) & 1ull) ? e : kNoParent;
+        sv[k] = gbl(sdsrc)[B.base + gz * YX + (int64_t)gy * B.X + gx];
+    }
+    static_assert(NW32 <= NT, "");
+    uint32_t bwv = ~0u;
+    if (cc && (int)threadIdx.x < NW32) {
+        const int r = threadIdx.x / WPR32, hw = threadIdx.x % WPR32;
+        const int gz = min(z0 + r / TY, B.Z - 1), gy = min(y0 + r % TY, B.Y - 1);
+        const int64_t row = B.fbase + ((int64_t)gz * B.Y + gy) * ((B.X + 63) >> 6);
+        bwv = gbl((const uint32_t*)sbits)[2 * row + (x0 >> 5) + hw];
     }
     {
         constexpr int NH = (HN + NT - 1) / NT;
@@ -631,12 +637,19 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
             }
         }
     }
+    if (cc && (int)threadIdx.x < NW32) sbm[threadIdx.x] = bwv;
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
+        if (cc) {
+            const int c = threadIdx.x + k * NT;
+            const int lx = c % TX, r = c / TX;
+            const int gx = x0 + lx;
+            if (!((sbm[r * WPR32 + (lx >> 5)] >> (gx & 31)) & 1u)) sv[k] = kNoParent;
+        }
         const bool sd = cc ? sv[k] != kNoParent : (sv[k] & kFixedBit) != 0u;
         seedm |= (((inm >> k) & 1u) && sd ? 1u : 0u) << k;
     }
-    __syncthreads();
     // parents
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
