@@ -164,6 +164,7 @@ struct ctws_handle {
     int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
     int cur_max[3] = {0, 0, 0};  // largest outer block extents (Z, Y, X) of the current batch
     int frontier_grid = 2048;  // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4)
+    int frontier_dir = 1;    // CTWS_FRONTIER_DIR: local sweeps queue only the neighbours a change may lower
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     std::vector<BlockDesc> last_desc;
@@ -684,7 +685,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
         k_frontier<ND, CW, CY, CZ><<<fg, 256, 0, h->stream>>>(                                                      \
             w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
-            h->frontier_reps);                                                                                      \
+            h->frontier_reps, h->frontier_dir);                                                                     \
         break;
             switch (fkind) {
                 CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
@@ -2349,6 +2350,7 @@ int ctws_open(int device, ctws_handle** out) {
     }
     if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
+    if (const char* t = std::getenv("CTWS_FRONTIER_DIR")) h->frontier_dir = std::atoi(t) ? 1 : 0;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * kTapSlot * sizeof(double), hipHostMallocDefault) != hipSuccess) {
@@ -2535,6 +2537,23 @@ int ctws_last_timings(const ctws_handle* h, const char** names, float* ms, int m
 int ctws_debug_set_stop(ctws_handle* h, int stage) {
     if (!h || stage < 0 || stage > 3) return CTWS_EINVAL;
     h->stop_after = stage;
+    return CTWS_OK;
+}
+
+int ctws_debug_sqrt_int(ctws_handle* h, uint32_t n0, uint32_t count, float* dst) {
+    if (!h || !dst || count == 0u || (uint64_t)n0 + count > (1ull << 24)) return CTWS_EINVAL;
+    HIPCHK(hipSetDevice(h->device));
+    float* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(float) * (size_t)count));
+    k_sqrt_int_check<<<(count + 255u) / 256u, 256, 0, h->stream>>>(n0, count, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, d, sizeof(float) * (size_t)count, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    hipFree(d);
+    if (e != hipSuccess) {
+        h->err = hipGetErrorString(e);
+        return CTWS_EHIP;
+    }
     return CTWS_OK;
 }
 

@@ -51,6 +51,7 @@ constexpr int kEdtSearchCap = 48;  // bounded-search steps before a column goes 
 template <int W>
 __global__ void k_edt_col(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*, uint32_t*,
                           uint32_t*, unsigned long long*, uint32_t*);
+__global__ void k_sqrt_int_check(uint32_t, uint32_t, float*);
 __global__ void k_edt_col_fh(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*, float*, uint32_t*,
                              uint32_t*, const unsigned long long*, const uint32_t*);
 template <class T>
@@ -158,7 +159,7 @@ __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*,
 template <int ND, int CW, int CY, int CZ>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
-                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
+                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int);
 // k_basin.hip: the descent flood's open voxels on the catchment graph
 template <int ND>
 __global__ void k_basin_edges(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint64_t*,

@@ -963,9 +963,16 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                                   uint32_t* __restrict__ gnext, int it, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ cnt, uint32_t* __restrict__ list_next,
                                                   uint32_t* __restrict__ cnt_next, uint32_t* __restrict__ qgen,
-                                                  uint32_t* __restrict__ nvisit, int reps) {
+                                                  uint32_t* __restrict__ nvisit, int reps, int dirf) {
     static_assert(ND == 3 || CZ == 1, "2-D ws: slices are independent, chunks are one slice deep");
     __shared__ uint64_t schg[kFrontierWaves][64];
+    // dirf: the local sweeps queue only the neighbours a change can lower.  f_q(K) > K for every
+    // key (h > C gives (h, 0) > (C, d); else d + 1), so a neighbour q whose key is <= the new key
+    // of p (read in the same visit: a stale read is >= the current key, keys only decrease)
+    // cannot take a lower key through p.  sdir[d]: changed voxels whose neighbour in direction d
+    // (-z, +z, -y, +y, -x, +x) may improve
+    constexpr int NDIR = ND == 3 ? 6 : 4;
+    __shared__ uint64_t sdir[kFrontierWaves][6][64];
     __shared__ uint64_t sfw[kFrontierWaves][64];
     __shared__ int spre[kFrontierWaves][64];
     __shared__ int srow[kFrontierWaves][64];
@@ -1063,6 +1070,10 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             if (total == 0) break;
             vis += (uint32_t)total;
             schg[wv][lane] = 0ull;
+            if (dirf) {
+#pragma unroll
+                for (int d = 0; d < NDIR; ++d) sdir[wv][d][lane] = 0ull;
+            }
             sfw[wv][lane] = f;
             spre[wv][lane] = incl - cnt_bits;
             srow[wv][lane] = row * 64 + xw;  // row < 2^25 (Z * Y <= 2^22)
@@ -1100,6 +1111,14 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                         if (k != own) {
                             kb[i] = k;
                             atomicOr((unsigned long long*)&schg[wv][j], 1ull << b);
+                            if (dirf) {
+                                // nb[] order: -z, +z, -y, +y, -x, +x (outside the block: INF,
+                                // its bit is shifted out of the chunk or masked by open)
+#pragma unroll
+                                for (int d = 0; d < 6; ++d)
+                                    if ((ND == 3 || d >= 2) && nb[d] > k)
+                                        atomicOr((unsigned long long*)&sdir[wv][ND == 3 ? d : d - 2][j], 1ull << b);
+                            }
                         }
                     }
                 }
@@ -1114,19 +1133,32 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                 break;
             }
             // local sweep: the neighbours of this sweep's changes inside the chunk; changes are
-            // also in acc, so the neighbours outside the chunk see them in the next launch
-            f = (c << 1) | (c >> 1);
-            const uint64_t cxm = __shfl(c, lx > 0 ? lane - 1 : lane);
-            const uint64_t cxp = __shfl(c, lx < CW - 1 ? lane + 1 : lane);
+            // also in acc, so the neighbours outside the chunk see them in the next launch.
+            // dirf: per direction, only the neighbours the change may lower (sdir)
+            uint64_t dzm = c, dzp = c, dym = c, dyp = c, dxm = c, dxp = c;
+            if (dirf) {
+                constexpr int o = ND == 3 ? 2 : 0;
+                if (ND == 3) {
+                    dzm = sdir[wv][0][lane];
+                    dzp = sdir[wv][1][lane];
+                }
+                dym = sdir[wv][o][lane];
+                dyp = sdir[wv][o + 1][lane];
+                dxm = sdir[wv][o + 2][lane];
+                dxp = sdir[wv][o + 3][lane];
+            }
+            f = (dxp << 1) | (dxm >> 1);
+            const uint64_t cxm = __shfl(dxp, lx > 0 ? lane - 1 : lane);
+            const uint64_t cxp = __shfl(dxm, lx < CW - 1 ? lane + 1 : lane);
             if (lx > 0) f |= cxm >> 63;
             if (lx < CW - 1 && xw + 1 < wpr) f |= cxp << 63;
-            const uint64_t cym = __shfl(c, ly > 0 ? lane - CW : lane);
-            const uint64_t cyp = __shfl(c, ly < CY - 1 ? lane + CW : lane);
+            const uint64_t cym = __shfl(dyp, ly > 0 ? lane - CW : lane);
+            const uint64_t cyp = __shfl(dym, ly < CY - 1 ? lane + CW : lane);
             if (ly > 0) f |= cym;
             if (ly < CY - 1 && yy + 1 < B.Y) f |= cyp;
             if (ND == 3 && CZ > 1) {
-                const uint64_t czm = __shfl(c, lz > 0 ? lane - CW * CY : lane);
-                const uint64_t czp = __shfl(c, lz < CZ - 1 ? lane + CW * CY : lane);
+                const uint64_t czm = __shfl(dzp, lz > 0 ? lane - CW * CY : lane);
+                const uint64_t czp = __shfl(dzm, lz < CZ - 1 ? lane + CW * CY : lane);
                 if (lz > 0) f |= czm;
                 if (lz < CZ - 1 && zz + 1 < B.Z) f |= czp;
             }
@@ -1167,7 +1199,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
                                                         const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,  \
                                                         uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*,   \
-                                                        uint32_t*, uint32_t*, uint32_t*, int);
+                                                        uint32_t*, uint32_t*, uint32_t*, int, int);
 #define CTWS_LIST0_INST(CW, CY, CZ)                                                                             \
     template __global__ void k_frontier_list0<CW, CY, CZ>(const BlockDesc*, const BlockStat*, const uint64_t*, \
                                                           uint32_t*, uint32_t*);

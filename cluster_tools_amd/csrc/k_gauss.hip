@@ -464,8 +464,9 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
     const float NEG = -__builtin_huge_valf();
     const bool pos = smax[B.sbase + z] > 0x80000000u;  // ordf(+0.0f)
     uint32_t nplat = 0;
-    for (int v = tid; v < SY * SX; v += 256) {
-        const int pp = 1 + v / SX, xx = 1 + v % SX;
+    constexpr int LSY = kYxTY - 2, LSX = TX - 2;  // (= SY, SX: constants for the index split)
+    for (int v = tid; v < LSY * LSX; v += 256) {
+        const int pp = 1 + v / LSX, xx = 1 + v % LSX;
         const int y = y0 + pp, x = x0 + xx;
         if (y >= Y || x >= X) continue;
         const int64_t gi = sbase + (int64_t)y * X + x;
