@@ -414,18 +414,30 @@ __device__ __forceinline__ float sqrt_rn_f(float x) {
     return r;
 }
 
+// correctly rounded sqrtf of an integer n < 2^24 without double arithmetic: v_sqrt_f32 (1 ulp)
+// gives r, the correctly rounded value is r - 1 ulp, r or r + 1 ulp, chosen by exact integer tests
+// of the midpoints.  r = R 2^-k (R the 24-bit significand): the upper midpoint is (2R + 1)
+// 2^-(k+1), below sqrt(n) iff (2R + 1)^2 < n 2^(2k+2); both sides are about 4 R^2 < 2^50.
 __device__ __forceinline__ float sqrt_rn_int(uint32_t n) {
-    float r = (float)__dsqrt_rn((double)n);
-    const double dn = (double)n;
-    const float up = __uint_as_float(__float_as_uint(r) + 1u);
-    const double mhi = 0.5 * ((double)r + (double)up);
-    if (mhi * mhi < dn) return up;
-    if (r > 0.0f) {
-        const float lo = __uint_as_float(__float_as_uint(r) - 1u);
-        const double mlo = 0.5 * ((double)r + (double)lo);
-        if (mlo * mlo > dn) return lo;
-    }
+    if (n == 0u) return 0.0f;
+    const float r = __builtin_amdgcn_sqrtf((float)n);  // n < 2^24: exact conversion
+    const uint32_t bits = __float_as_uint(r);
+    const uint64_t R = (uint64_t)((bits & 0x7FFFFFu) | 0x800000u);
+    const int k = 150 - (int)(bits >> 23);  // r = R 2^-k, 12 <= k <= 23 for 1 <= n < 2^24
+    const uint64_t n4 = (uint64_t)n << (2 * k + 2);
+    if ((2 * R + 1) * (2 * R + 1) < n4) return __uint_as_float(bits + 1u);
+    // lower midpoint: (2R - 1) 2^-(k+1), or (2^25 - 1) 2^-(k+2) when r is a power of two
+    const bool pow2 = R == 0x800000ull;
+    const uint64_t ml = pow2 ? (1ull << 25) - 1ull : 2 * R - 1;
+    if (ml * ml > (pow2 ? n4 << 2 : n4)) return __uint_as_float(bits - 1u);
     return r;
+}
+
+// device self-check of sqrt_rn_int over [n0, n0 + count) (tests: every n < 2^24 against the
+// correctly rounded float sqrt)
+__global__ void __launch_bounds__(256) k_sqrt_int_check(uint32_t n0, uint32_t count, float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < count) out[i] = sqrt_rn_int(n0 + i);
 }
 
 // ---- EDT pass along y (stride X) or z (stride Y*X), LDS-staged columns -----------------

@@ -60,13 +60,14 @@ def lib():
             L.ctws_eval_end.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
             L.ctws_debug_set_stop.argtypes = [C.c_void_p, C.c_int]
             L.ctws_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_int64]
+            L.ctws_debug_sqrt_int.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
             _lib = L
         return _lib
 
 
 EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
                     'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_unique_u64', 'ctws_unique_counts_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
-                    'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
+                    'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_debug_sqrt_int', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
                     'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end')
 
 
@@ -128,6 +129,12 @@ class Handle:
         out = np.empty(shape, dtype=dt)
         self._check(lib().ctws_debug_read(self._h, array.encode(), int(block), out.ctypes.data, out.nbytes),
                     'ctws_debug_read')
+        return out
+
+    def debug_sqrt_int(self, n0, count):
+        """The EDT's integer sqrt (k_edt.hip sqrt_rn_int) of n0 .. n0 + count - 1, as float32."""
+        out = np.empty(int(count), dtype=np.float32)
+        self._check(lib().ctws_debug_sqrt_int(self._h, int(n0), int(count), out.ctypes.data), 'ctws_debug_sqrt_int')
         return out
 
     # ---- host (numpy) blocks ------------------------------------------------------------

@@ -16,6 +16,7 @@ Chunk (de)compression runs on a thread pool of ``n_threads`` (zlib releases the 
 """
 import json
 import os
+import threading
 import zlib
 from concurrent import futures
 from itertools import product
@@ -64,6 +65,16 @@ def _decompress(data, compression):
     return data
 
 
+def _dump_json(path, obj):
+    """Write a metadata / attributes file atomically (temp file + rename): in N5 the attributes
+    share attributes.json with the dataset metadata, and jobs open the dataset (reading it) while
+    job 0 sets attrs (write.py's maxId) — a truncate-and-rewrite would let them read it empty."""
+    tmp = '%s.tmp%d.%d' % (path, os.getpid(), threading.get_ident())
+    with open(tmp, 'w') as f:
+        json.dump(obj, f)
+    os.replace(tmp, path)
+
+
 class Attributes:
     def __init__(self, path, fmt):
         self._path = path
@@ -84,8 +95,7 @@ class Attributes:
     def __setitem__(self, k, v):
         a = self._load()
         a[k] = v
-        with open(self._file(), 'w') as f:
-            json.dump(a, f)
+        _dump_json(self._file(), a)
 
     def __contains__(self, k):
         return k in self._load()
@@ -271,8 +281,7 @@ class Group:
         p = os.path.join(self.path, key)
         os.makedirs(p, exist_ok=True)
         if self.fmt == 'zarr' and not os.path.exists(os.path.join(p, '.zgroup')):
-            with open(os.path.join(p, '.zgroup'), 'w') as f:
-                json.dump({'zarr_format': 2}, f)
+            _dump_json(os.path.join(p, '.zgroup'), {'zarr_format': 2})
         return Group(p, self.fmt, self.mode)
 
     create_group = require_group
@@ -303,14 +312,12 @@ class Group:
                     'dataType': _N5_DTYPES[dtype.name],
                     'compression': {'type': comp} if comp == 'raw' else
                     {'type': 'gzip', 'level': 5, 'useZlib': comp == 'zlib'}}
-            with open(os.path.join(p, 'attributes.json'), 'w') as f:
-                json.dump(meta, f)
+            _dump_json(os.path.join(p, 'attributes.json'), meta)
         else:
             meta = {'chunks': list(chunks), 'compressor': None if comp == 'raw' else {'id': comp, 'level': 5},
                     'dtype': dtype.str, 'fill_value': fillvalue, 'filters': None, 'order': 'C',
                     'shape': list(shape), 'zarr_format': 2}
-            with open(os.path.join(p, '.zarray'), 'w') as f:
-                json.dump(meta, f)
+            _dump_json(os.path.join(p, '.zarray'), meta)
         ds = Dataset(p, self.fmt)
         if data is not None:
             ds[...] = data
@@ -338,11 +345,9 @@ class File(Group):
                 raise OSError("%s does not exist" % path)
             os.makedirs(path)
             if fmt == 'n5':
-                with open(os.path.join(path, 'attributes.json'), 'w') as f:
-                    json.dump({'n5': '2.0.0'}, f)
+                _dump_json(os.path.join(path, 'attributes.json'), {'n5': '2.0.0'})
             else:
-                with open(os.path.join(path, '.zgroup'), 'w') as f:
-                    json.dump({'zarr_format': 2}, f)
+                _dump_json(os.path.join(path, '.zgroup'), {'zarr_format': 2})
         super().__init__(path, fmt, mode)
 
     def __enter__(self):

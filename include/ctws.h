@@ -230,6 +230,8 @@ int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, 
 #define CTWS_STOP_WS    3  /* after the size filter + 2-D offsets + masking     */
 int ctws_debug_set_stop(ctws_handle* h, int stage);
 int ctws_debug_read(ctws_handle* h, const char* array, int block, void* dst, int64_t nbytes);
+/* the EDT's correctly rounded sqrt of integers n0 .. n0 + count - 1 (< 2^24) into host dst */
+int ctws_debug_sqrt_int(ctws_handle* h, uint32_t n0, uint32_t count, float* dst);
 
 #ifdef __cplusplus
 }

@@ -200,3 +200,14 @@ def test_refusals_are_per_block(gpu_handle):
     ref = O.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=4)])[0]
     vis, vim = vi_scores(res[2]['output'], ref['output'])
     assert vis + vim <= VI_TOL
+
+
+def test_edt_integer_sqrt_exhaustive(gpu_handle):
+    """The EDT's final sqrt (k_edt.hip sqrt_rn_int: v_sqrt_f32 + exact integer midpoint tests)
+    equals the correctly rounded float32 sqrt (vigra: sqrt on the float32 dest) for every squared
+    distance n < 2^24."""
+    n = 1 << 24
+    got = gpu_handle.debug_sqrt_int(0, n)
+    want = np.sqrt(np.arange(n, dtype=np.float64)).astype(np.float32)  # double sqrt -> float: correctly rounded
+    bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
+    assert bad.size == 0, (bad[:10], got[bad[:10]], want[bad[:10]])
