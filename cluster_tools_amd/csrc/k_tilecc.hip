@@ -320,59 +320,6 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
     // face voxels: the low z / y / x planes (and, for 2-D plateaus, the high x plane below),
     // enumerated per face so that consecutive lanes walk consecutive face voxels
     const int fsz[3] = {TY * TX, TZ * TX, TZ * TY};  // z-face (y, x), y-face (z, x), x-face (z, y)
-    if constexpr (!(ND == 2 && MODE == CC_PLATEAU)) {
-        // axial neighbourhoods: exactly one backward neighbour leaves the tile through face f,
-        // so a lane's pair (i, q) is known up front and every load of it (the two parents, the
-        // membership and the values) is issued together, unconditionally (clamped index), instead
-        // of the dependent chain parent -> neighbour parent -> values
-        for (int f = (ND == 3 ? 0 : 1); f < 3; ++f) {
-            const int n = fsz[f];
-            for (int e0 = 0; e0 < n; e0 += 256) {
-                const int e = e0 + (int)threadIdx.x;
-                int lz, ly, lx;
-                if (f == 0) { lz = 0; ly = e / TX; lx = e % TX; }
-                else if (f == 1) { lz = e / TX; ly = 0; lx = e % TX; }
-                else { lz = e / TY; ly = e % TY; lx = 0; }
-                const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
-                const int qz = z - (f == 0 ? 1 : 0), qy = y - (f == 1 ? 1 : 0), qx = x - (f == 2 ? 1 : 0);
-                const bool ok = e < n && z < nz && y < ny && x < nx && qz >= 0 && qy >= 0 && qx >= 0;
-                const int cz = ok ? z : 0, cy = ok ? y : 0, cx = ok ? x : 0;
-                const int dz = ok ? qz : 0, dy = ok ? qy : 0, dx = ok ? qx : 0;
-                const int64_t i = ((int64_t)cz * ny + cy) * nx + cx;
-                const int64_t q = ((int64_t)dz * ny + dy) * nx + dx;
-                const uint32_t pi = gbl(P)[i], pq = gbl(P)[q];
-                bool pair;
-                if (MODE == CC_CROP) {
-                    // members: P != kNoParent (k_tile_cc writes every domain voxel); both
-                    // members are unmasked with a label, equal labels connect
-                    const int64_t oi = ((int64_t)(cz + B.iz0) * B.Y + (cy + B.iy0)) * B.X + (cx + B.ix0);
-                    const int64_t oq = ((int64_t)(dz + B.iz0) * B.Y + (dy + B.iy0)) * B.X + (dx + B.ix0);
-                    const uint32_t li = flood_label(a.lab, a.key, a.packed, B.base + oi);
-                    const uint32_t lq = flood_label(a.lab, a.key, a.packed, B.base + oq);
-                    pair = ok && pi != kNoParent && pq != kNoParent && li == lq;
-                } else if (MODE == CC_PLATEAU) {
-                    // members: cls bit 2 (P is unwritten in tiles without plateau voxels)
-                    const uint8_t ci = gbl(a.cls)[B.base + i], cq = gbl(a.cls)[B.base + q];
-                    uint32_t vi = __float_as_uint(gbl(a.v)[B.base + i]), vq = __float_as_uint(gbl(a.v)[B.base + q]);
-                    vi = vi == 0x80000000u ? 0u : vi;  // -0.0 == +0.0
-                    vq = vq == 0x80000000u ? 0u : vq;
-                    pair = ok && (ci & 2) && (cq & 2) && vi == vq && pi != kNoParent && pq != kNoParent;
-                } else {
-                    // members: the member bitmap (P holds the members only)
-                    pair = ok && bit_of(a.troot, B, i) && bit_of(a.troot, B, q);
-                }
-                const uint32_t ra = pair ? pi : kNoParent, rb = pair ? pq : kNoParent;
-                // skip the pair of the previous lane (runs along a face share their tile roots)
-                const uint32_t pa = (uint32_t)__shfl_up((int)ra, 1), pb = (uint32_t)__shfl_up((int)rb, 1);
-                const bool dup = ((threadIdx.x & 63) != 0) && pa == ra && pb == rb;
-                if (ra != kNoParent && !dup) {
-                    if (MODE == CC_PLATEAU) uf_union(P, ra, rb);
-                    else uf_union_scan(P, ra, rb, B, inner);
-                }
-            }
-        }
-        continue;
-    }
     for (int f = (ND == 3 ? 0 : 1); f < 3; ++f) {
         const int n = fsz[f];
         for (int e0 = 0; e0 < n; e0 += 256) {
