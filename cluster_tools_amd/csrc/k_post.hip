@@ -38,6 +38,20 @@ __global__ void __launch_bounds__(256) k_hist_zero(const BlockDesc* __restrict__
         counts[B.base + i] = 0;
 }
 
+// count a wave's labels: one add per run of equal labels in consecutive lanes (voxels along x
+// mostly share their label, so a mixed wave is a few runs, not 64 atomics on the same bins).
+// ok: the lane holds a label to count (the invalid lanes are a tail of the wave)
+template <class Add>
+__device__ __forceinline__ void count_label_runs(uint32_t l, bool ok, int lane, Add add) {
+    const uint32_t prev = (uint32_t)__shfl_up((int)l, 1);
+    const uint64_t act = __ballot(ok);
+    const uint64_t starts = __ballot(ok && (lane == 0 || prev != l));
+    if (!((starts >> lane) & 1ull)) return;
+    const uint64_t ends = (starts | ~act) & ~((2ull << lane) - 1ull);  // run boundaries above the lane
+    const int next = ends ? __builtin_ctzll(ends) : 64;
+    add(l, (uint32_t)(next - lane));
+}
+
 // label counts over the whole outer block (3-D) / slice (2-D: labels are slice-unique).
 // Each workgroup counts a contiguous range in an LDS histogram of `bins` entries (dynamic
 // LDS, sized by the host to the batch's largest seed count so that a few thousand labels do
@@ -81,20 +95,10 @@ __global__ void __launch_bounds__(256) k_hist(const BlockDesc* __restrict__ D, c
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t l = lv[u];
-            const bool ok = l != 0xFFFFFFFFu;
-            // a wave of equal labels (the common case) costs one atomic
-            const uint32_t l0 = __shfl(l, 0);
-            const uint64_t same = __ballot(ok && l == l0);
-            const uint64_t act = __ballot(ok);
-            if (same == act) {
-                if (lane == 0 && act) {
-                    if (use_lds) atomicAdd(&sh[l0], (uint32_t)__popcll(act));
-                    else atomicAdd(&c[l0], (uint32_t)__popcll(act));
-                }
-            } else if (ok) {
-                if (use_lds) atomicAdd(&sh[l], 1u);
-                else atomicAdd(&c[l], 1u);
-            }
+            count_label_runs(l, l != 0xFFFFFFFFu, lane, [&](uint32_t lb, uint32_t n) {
+                if (use_lds) atomicAdd(&sh[lb], n);
+                else atomicAdd(&c[lb], n);
+            });
         }
     }
     if (!use_lds) return;
@@ -150,19 +154,12 @@ __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t l = lv[u];
-            const bool ok = l > b0 && l <= b1;  // 0 (unreached) is not counted
-            const uint32_t l0 = __shfl(l, 0);
-            const uint64_t same = __ballot(ok && l == l0);
-            const uint64_t act = __ballot(ok);
-            if (same == act) {
-                if (lane == 0 && act) {
-                    if (use_lds) atomicAdd(&sh[l0 - b0 - 1], (uint32_t)__popcll(act));
-                    else atomicAdd(&c[l0 - b0 - 1], (uint32_t)__popcll(act));
-                }
-            } else if (ok) {
-                if (use_lds) atomicAdd(&sh[l - b0 - 1], 1u);
-                else atomicAdd(&c[l - b0 - 1], 1u);
-            }
+            // 0 (unreached) is not counted: a run of its own, dropped
+            count_label_runs(l, l != 0xFFFFFFFFu, lane, [&](uint32_t lb, uint32_t n) {
+                if (lb <= b0 || lb > b1) return;
+                if (use_lds) atomicAdd(&sh[lb - b0 - 1], n);
+                else atomicAdd(&c[lb - b0 - 1], n);
+            });
         }
     }
     if (!use_lds) return;
