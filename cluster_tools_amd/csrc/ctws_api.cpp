@@ -1201,6 +1201,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const unsigned gfh = (unsigned)std::min<int64_t>((ncols + 255) / 256, 1024);
         auto launch_col = [&](int W, dim3 g, size_t lds, EdtColParams p, const uint32_t* gin, uint32_t* gout,
                               uint32_t* cnt) {
+            if (lds > 65536)  // gfx950: up to 160 KiB of LDS per workgroup, above 64 KiB by opt-in
+                (void)hipFuncSetAttribute((const void*)(W == 32 ? k_edt_col<32> : W == 16 ? k_edt_col<16> : k_edt_col<8>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (W == 32)
                 k_edt_col<32><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list,
                                                           cnt);
