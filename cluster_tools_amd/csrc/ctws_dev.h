@@ -121,10 +121,23 @@ __device__ __forceinline__ uint32_t uf_find_compress(uint32_t* P, uint32_t a) {
     }
     return r;
 }
+// find with path halving for the unions: a non-root's parent becomes its grandparent on the
+// way up (benign races: a non-root never becomes a root again and every store is an ancestor),
+// so the chains the merges build over many tiles stay short for the later finds
+__device__ __forceinline__ uint32_t uf_find_halve(uint32_t* P, uint32_t a) {
+    while (true) {
+        const uint32_t p = P[a];
+        if (p == a) return a;
+        const uint32_t gp = P[p];
+        if (gp == p) return p;
+        P[a] = gp;
+        a = gp;
+    }
+}
 __device__ __forceinline__ void uf_union(uint32_t* P, uint32_t a, uint32_t b) {
     while (true) {
-        a = uf_find(P, a);
-        b = uf_find(P, b);
+        a = uf_find_halve(P, a);
+        b = uf_find_halve(P, b);
         if (a == b) return;
         if (a > b) {
             uint32_t t = a;
@@ -158,8 +171,8 @@ __device__ __forceinline__ uint32_t scan_key_idx(const BlockDesc& B, int inner, 
 // component's first voxel in vigra scan order
 __device__ __forceinline__ void uf_union_scan(uint32_t* P, uint32_t a, uint32_t b, const BlockDesc& B, int inner) {
     while (true) {
-        a = uf_find(P, a);
-        b = uf_find(P, b);
+        a = uf_find_halve(P, a);
+        b = uf_find_halve(P, b);
         if (a == b) return;
         if (scan_key_idx(B, inner, a) > scan_key_idx(B, inner, b)) {
             const uint32_t t = a;
