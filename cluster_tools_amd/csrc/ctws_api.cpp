@@ -152,6 +152,7 @@ struct ctws_handle {
     int host_ramp = 1;          // CTWS_HOST_RAMP=0: equal batches (no smaller first / last batches)
     int host_batch_blocks = 0;  // CTWS_HOST_BATCH_BLOCKS: cap on blocks per host-path batch (0: voxel cap)
     int64_t host_batch_voxels = (int64_t)256 << 20;  // CTWS_HOST_BATCH_VOXELS: smaller batches pipeline better
+    int edt_wz = 0;  // CTWS_EDT_WZ: the same for the z pass alone (3-D DT)
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words).
     // 3-D batches with a mask default to 1x32x2 instead of 1x8x8: a masked region is one flat
@@ -412,7 +413,10 @@ int col_width(int L) { return L <= 512 ? 32 : (L <= 1024 ? 16 : 8); }
 // EDT columns: 16 x positions (64-B row segments) beat 32 — half the LDS per tile, twice the
 // tiles per CU, and the bounded search's per-lane trip counts vary less per wave (r01 sweep:
 // y+z passes 1.60 ms at 32, 1.44 at 16, 1.77 at 8 for config 2)
-int edt_col_width(int L) { return L <= 1024 ? 16 : 8; }
+// EDT column tile width: 32 x positions (full 128-B rows) while the column tile fits 32 KiB
+// of LDS (config 4/5 z pass, 80-deep lines: 14.9 -> 13.8 / 14.3 -> 12.7 ms of EDT per step);
+// 16 up to 1024-long lines (a 576-long y line at 32 wide, 74 KiB, measured 9.1 vs 5.6 ms)
+int edt_col_width(int L) { return L <= 256 ? 32 : L <= 1024 ? 16 : 8; }
 
 void record(ctws_handle* h, size_t idx) {
     while (h->events.size() <= idx) {
@@ -1218,7 +1222,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         launch_col(Wy, gy, ldsy, ep, (uint32_t*)w.A, (uint32_t*)w.Bf, fh_cnt);
         LAUNCHCHK();
         if (!pl.dt_2d) {
-            const int Wz = h->edt_w ? h->edt_w : edt_col_width(maxZ);
+            const int Wz = h->edt_wz ? h->edt_wz : h->edt_w ? h->edt_w : edt_col_width(maxZ);
             dim3 gz((unsigned)((int64_t)maxY * ((maxX + Wz - 1) / Wz)), nb);
             const size_t ldsz = (size_t)maxZ * Wz * 4;
             EdtColParams ez{2, pl.pitch[0] * pl.pitch[0], 1, 0, 0u};
@@ -2337,6 +2341,10 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_EDT_W")) {
         const int v = std::atoi(t);
         h->edt_w = (v == 8 || v == 16 || v == 32) ? v : 0;
+    }
+    if (const char* t = std::getenv("CTWS_EDT_WZ")) {
+        const int v = std::atoi(t);
+        h->edt_wz = (v == 8 || v == 16 || v == 32) ? v : 0;
     }
     auto parse_chunk = [](const char* t, int* c, bool three_d) {
         int a = 0, b = 0, d = 0;
