@@ -134,7 +134,10 @@ struct ctws_handle {
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
     int output_tile = 1;   // CTWS_OUTPUT_TILE=0: cropped blocks through the word-tiled k_output
-    int fuse_localmax = 1; // CTWS_FUSE_LOCALMAX=0: 2-D local maxima by the separate k_localmax pass
+    // CTWS_FUSE_LOCALMAX=1: 2-D local maxima in the seed-map Gaussian's epilogue (overlapping
+    // tiles).  Off by default: measured 0.65 ms per step slower on config 3 than the Gaussian +
+    // the separate k_localmax pass (7.3 + 5.6 vs 3.8 + 8.4 ms, profiles/r03/u*_1stream_c3.json)
+    int fuse_localmax = 0;
     int basin = 0;         // CTWS_BASIN=1: the open voxels on the catchment graph (k_basin.hip) instead of the frontier relaxation
     DevBuf basin_edges;    // basin flood: catchment pairs (root, root, pass height)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile

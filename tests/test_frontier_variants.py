@@ -31,8 +31,8 @@ VARIANTS = {
     'basin_no_plateau_fill': {'CTWS_BASIN': '1', 'CTWS_PLATEAU_FILL': '0'},
     # cropped blocks' uint64 output through the word-tiled k_output instead of k_output_crop
     'output_words': {'CTWS_OUTPUT_TILE': '0'},
-    # 2-D local maxima by the separate k_localmax pass instead of the seed-map Gaussian's tiles
-    'localmax_pass': {'CTWS_FUSE_LOCALMAX': '0'},
+    # 2-D local maxima in the seed-map Gaussian's tiles (opt-in) instead of the separate k_localmax pass
+    'localmax_fused': {'CTWS_FUSE_LOCALMAX': '1'},
 }
 
 
