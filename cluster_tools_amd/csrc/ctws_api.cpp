@@ -67,9 +67,7 @@ struct Workspace {
     int64_t cap_front = 0;
     uint64_t *front0 = nullptr, *front1 = nullptr, *fopen = nullptr;
     uint64_t* fplat = nullptr;   // plateau fill (k_plateau.hip): the plateau voxels
-    uint64_t* flake = nullptr;   // basin flood (k_basin.hip): the lake voxels
     uint64_t* fseed = nullptr;   // seed CC members (the seed forest's parents are written for members only)
-    uint32_t* bctl = nullptr;    // basin flood: [0] edges, [1] lake voxels, [2 + it] relax sweep it changed a root
     uint32_t* plev = nullptr;    // per block: the plateau height (0: none)
     uint32_t* fflags = nullptr;
     uint32_t *fchunk0 = nullptr, *fchunk1 = nullptr;  // per 64-word chunk: generation of its last change
@@ -84,7 +82,6 @@ constexpr int kFrontierBatch = 8;        // frontier iterations per host check
 constexpr int kFrontierWavesHost = 4;    // waves per workgroup of k_frontier (kFrontierWaves)
 constexpr int kFrontierMaxIters = 256;   // then the tile flood takes over
 constexpr int kFrontierMaxItersCap = 4096;  // CTWS_FRONTIER_ITERS upper bound (worklist counters)
-constexpr int kBasinMaxIters = 64;       // catchment-graph sweeps before the frontier relaxation takes over
 
 }  // namespace
 
@@ -134,12 +131,6 @@ struct ctws_handle {
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
     int output_tile = 1;   // CTWS_OUTPUT_TILE=0: cropped blocks through the word-tiled k_output
-    // CTWS_FUSE_LOCALMAX=1: 2-D local maxima in the seed-map Gaussian's epilogue (overlapping
-    // tiles).  Off by default: measured 0.65 ms per step slower on config 3 than the Gaussian +
-    // the separate k_localmax pass (7.3 + 5.6 vs 3.8 + 8.4 ms, profiles/r03/u*_1stream_c3.json)
-    int fuse_localmax = 0;
-    int basin = 0;         // CTWS_BASIN=1: the open voxels on the catchment graph (k_basin.hip) instead of the frontier relaxation
-    DevBuf basin_edges;    // basin flood: catchment pairs (root, root, pass height)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int words_per_wave = 32;    // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels
@@ -291,7 +282,6 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         ALLOC(front1, front);
         ALLOC(fopen, front);
         ALLOC(fplat, front);
-        ALLOC(flake, front);
         ALLOC(fseed, front);
         ALLOC(fchunk0, (front >> kChunkShift) + 1);
         ALLOC(fchunk1, (front >> kChunkShift) + 1);
@@ -301,7 +291,6 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
         w.cap_front = front;
     }
     if (!w.fflags) ALLOC(fflags, kFrontierBatch);
-    if (!w.bctl) ALLOC(bctl, 2 + kBasinMaxIters);
     if (!w.wlcnt) ALLOC(wlcnt, kFrontierMaxItersCap + 2);
     if (blocks > w.cap_fstat) {
         ALLOC(fstat, 2 * blocks);
@@ -381,9 +370,12 @@ int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
                 return CTWS_EINVAL;
             }
             p.pitchd[k] = v;
-            // vigra: int(pitch) != pitch selects the real-valued path (multi_distance.hxx)
-            if (v != std::floor(v) || v > 4096.0) p.real_pitch = true;
-            else p.pitch[k] = (int)v;
+            // vigra: int(pitch) != pitch selects the real-valued (double) path (multi_distance.hxx);
+            // a large integer pitch stays integer: its dmax >= 2^24 selects the float path per batch
+            // (run_batch), as the oracle's distance_transform does.  (The int copy is only read by
+            // the exact integer path, which such a pitch never takes.)
+            if (v != std::floor(v)) p.real_pitch = true;
+            else p.pitch[k] = (int)std::min(v, 65536.0);
         }
     }
     auto sig = [&](const double* s, int is_list, double* out, bool& en) -> int {
@@ -451,13 +443,9 @@ const GaussYxKernel kGaussYx[kGaussMaxR + 1] = {nullptr, CTWS_R12(CTWS_YX)};
 #undef CTWS_COL16
 #undef CTWS_COL8
 
-// lm_cls (2-D ws seed map): when the fused y + x tile kernel runs, it also writes the local-maximum
-// classes (k_localmax's) there and *lm_done is set
 int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, const float* src, float* dst,
-              int nb, int maxZ, int maxY, int maxX, HmapParams hp, int taps_slot, uint8_t* lm_cls = nullptr,
-              bool* lm_done = nullptr) {
+              int nb, int maxZ, int maxY, int maxX, HmapParams hp, int taps_slot) {
     Workspace& w = h->ws;
-    if (lm_done) *lm_done = false;
     int axes[3], na = 0;
     for (int a = (pl.nd_ws == 3 ? 0 : 1); a < 3; ++a)
         if (sig[a] > 0.0) axes[na++] = a;
@@ -492,16 +480,12 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
                 std::memcpy(htx, tx.data(), sizeof(double) * tx.size());
                 HIPCHK(hipMemcpyAsync(dtx, htx, sizeof(double) * tx.size(), hipMemcpyHostToDevice, h->stream));
                 const int TX = 128 - 2 * r;
-                const bool lm = lm_cls && pl.nd_ws == 2 && !hmap_src;
-                const int SY = lm ? kGaussYxTY - 2 : kGaussYxTY, SX = lm ? TX - 2 : TX;  // tile stride
-                const int64_t ntiles = (int64_t)maxZ * ((maxY + SY - 1) / SY) * ((maxX + SX - 1) / SX);
+                const int64_t ntiles = (int64_t)maxZ * ((maxY + kGaussYxTY - 1) / kGaussYxTY) * ((maxX + TX - 1) / TX);
                 dim3 g((unsigned)ntiles, nb);
                 hipLaunchKernelGGL(kGaussYx[r], g, dim3(256), 0, h->stream, w.desc, w.stat, gp.hmap_src, hp,
                                    (const double*)dtaps, (const double*)dtx, in, (const float*)w.dt,
-                                   (const uint32_t*)w.smin, (const uint32_t*)w.smax, dst, lm ? lm_cls : nullptr,
-                                   w.stat);
+                                   (const uint32_t*)w.smin, (const uint32_t*)w.smax, dst);
                 LAUNCHCHK();
-                if (lm_done) *lm_done = lm;
                 return CTWS_OK;
             }
         }
@@ -511,6 +495,9 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
                 // rows longer than a wave's registers hold: the generic row kernel
                 dim3 g((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
                 const size_t lds = 2 * 128 * 4 + 4 * (size_t)maxX * 4;
+                if (lds > 65536)  // gfx950: up to 160 KiB of LDS per workgroup, above 64 KiB by opt-in
+                    (void)hipFuncSetAttribute((const void*)k_gauss_row, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)lds);
                 k_gauss_row<<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax, out);
             } else if (a == 2) {
                 // rows per wave shrink with X: size the grid for the widest block
@@ -533,6 +520,8 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
         } else if (a == 2) {
             dim3 g((unsigned)(((int64_t)maxZ * maxY + 3) / 4), nb);
             const size_t lds = 2 * 128 * 4 + 4 * (size_t)maxX * 4;
+            if (lds > 65536)
+                (void)hipFuncSetAttribute((const void*)k_gauss_row, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             k_gauss_row<<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax, out);
         } else {
             const int Lm = a == 0 ? maxZ : maxY;
@@ -745,79 +734,6 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
 
 void add_timing(ctws_handle* h, const char* name, float v);
 
-// The open voxels of the descent flood on the catchment graph (k_basin.hip): catchment-root
-// passes (edges + Bellman-Ford sweeps over the root pairs), the keys' (C, d) (lake voxels by the
-// frontier relaxation), then the labels by parent chains.  *done = false when the pair list does
-// not fit or the sweeps do not converge: the keys of the open voxels are then still the
-// descent's (INF) and the caller runs the frontier relaxation instead.  Ties between two argmin
-// neighbours are left to the caller's checked repair (k_flood_verify with marks).
-int run_basin(ctws_handle* h, const Plan& pl, int nb, int64_t T, int64_t TF, int max_tiles, int64_t TT, bool packed,
-              const dim3& wtg, const dim3& tg, bool plat, bool* done, int* fiters, int* rounds, float* fkms) {
-    Workspace& w = h->ws;
-    *done = false;
-    if (T >= (int64_t)0xFFFFFFF0ll) return CTWS_OK;  // root pairs hold batch indices in 32 bits
-    const uint32_t ecap = (uint32_t)std::min<int64_t>(T / 8 + 4096, 0x7FFFFFFFll);
-    int r;
-    if ((r = grow(h, h->basin_edges, sizeof(uint4) * (size_t)ecap)) != CTWS_OK) return r;
-    uint4* edges = (uint4*)h->basin_edges.p;
-    uint32_t* cr = (uint32_t*)w.A;  // free between the hmap and the size filter
-    const uint64_t* fpl = plat ? w.fplat : nullptr;
-    HIPCHK(hipMemsetAsync(w.bctl, 0, sizeof(uint32_t) * (2 + kBasinMaxIters), h->stream));
-    if (pl.nd_ws == 3)
-        k_basin_edges<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, edges, w.bctl, ecap);
-    else
-        k_basin_edges<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, edges, w.bctl, ecap);
-    LAUNCHCHK();
-    const unsigned rgrid = (unsigned)std::min<int64_t>((int64_t)(ecap + 255) / 256, 2048);
-    int it = 0;
-    bool conv = false;
-    while (it < kBasinMaxIters && !conv) {
-        const int n = std::min(8, kBasinMaxIters - it);
-        for (int k = 0; k < n; ++k)
-            k_basin_relax<<<rgrid, 256, 0, h->stream>>>(edges, w.bctl, ecap, cr, w.bctl + 2, it + k);
-        LAUNCHCHK();
-        HIPCHK(hipMemcpyAsync(h->h_counter, w.bctl, sizeof(uint32_t) * (size_t)(2 + it + n), hipMemcpyDeviceToHost,
-                              h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-        if (h->h_counter[0] > ecap) {
-            add_timing(h, "basin_overflow", 1.f);
-            return CTWS_OK;
-        }
-        for (int k = 0; k < n && !conv; ++k) {
-            ++it;
-            conv = h->h_counter[2 + it - 1] == 0u;
-        }
-    }
-    add_timing(h, "basin_edges", (float)h->h_counter[0]);
-    add_timing(h, "basin_sweeps", (float)it);
-    if (!conv) return CTWS_OK;
-    k_basin_c<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fopen, fpl, cr, w.key);
-    if (pl.nd_ws == 3)
-        k_basin_keys<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.fopen, w.key, w.flake, w.front0, w.bctl + 1);
-    else
-        k_basin_keys<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.fopen, w.key, w.flake, w.front0, w.bctl + 1);
-    k_basin_lake_reset<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0, h->stream>>>(
-        w.desc, w.stat, w.flake, w.key);
-    LAUNCHCHK();
-    HIPCHK(hipMemcpyAsync(h->h_counter + 1, w.bctl + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    add_timing(h, "basin_lake", (float)h->h_counter[1]);
-    if (h->h_counter[1]) {
-        // the lake voxels' (C, d): the frontier relaxation with the lake as its open set and every
-        // other voxel as the first changed set
-        std::swap(w.fopen, w.flake);
-        r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, fiters, rounds, fkms);
-        std::swap(w.fopen, w.flake);
-        if (r != CTWS_OK) return r;
-    }
-    if (pl.nd_ws == 3) k_basin_tile<3><<<tg, 512, 0, h->stream>>>(w.desc, w.stat, w.key, w.fopen, fpl, w.P);
-    else k_basin_tile<2><<<tg, 512, 0, h->stream>>>(w.desc, w.stat, w.key, w.fopen, fpl, w.P);
-    k_basin_hop<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.P, w.fopen, w.key);
-    LAUNCHCHK();
-    *done = true;
-    return CTWS_OK;
-}
-
 int64_t words_of(int64_t n) { return n / 64 + 1; }
 int64_t chunks_of(int64_t n) { return (words_of(n) + 255) / 256; }
 
@@ -893,6 +809,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int64_t maxN = 0, maxNI = 0;
     int maxIZ = 0, maxIY = 0, maxIX = 0;
     bool real_edt = pl.real_pitch;  // the batch's distances take vigra's real-valued path
+    bool real_double = pl.real_pitch;  // ... with a double temporary (else float)
     const uint64_t bvol = (uint64_t)(cfg->block_shape[0] * cfg->block_shape[1] * cfg->block_shape[2]);
     {
         bool any_mask = false;
@@ -1024,6 +941,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // dmax >= 2^24: float32 squared distances are no longer exact integers; vigra's float
         // arithmetic is then reproduced by the real-valued path (k_edt_real_*)
         if (dmax >= 16777216.0 && !pl.from_seeds) real_edt = true;
+        if (dmax > 3.4028234663852886e38 && !pl.from_seeds) real_double = true;  // > FLT_MAX: double, as vigra
     }
     // flood tile grids: the largest (wide kernel) bounds the per-tile arrays
     auto set_tiles = [&](bool packed) {
@@ -1166,10 +1084,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     } else {
     if (real_edt) {
         // vigra's real-valued path: double temporary (non-integer pitch) or float (dmax >= 2^24)
-        EdtRealParams er{{pl.pitchd[0], pl.pitchd[1], pl.pitchd[2]}, pl.dt_2d, pl.real_pitch ? 1 : 0};
+        EdtRealParams er{{pl.pitchd[0], pl.pitchd[1], pl.pitchd[2]}, pl.dt_2d, real_double ? 1 : 0};
         const int nthr = 64 * 256;
         const int maxL = std::max(maxZ, std::max(maxY, maxX));
-        const size_t esz = pl.real_pitch ? 8 : 4;
+        const size_t esz = real_double ? 8 : 4;
         if ((r = grow(h, h->edt_scratch, (size_t)nthr * maxL * (2 * esz + 20))) != CTWS_OK) return r;
         char* scr = (char*)h->edt_scratch.p;
         auto run_real = [&](auto tag) {
@@ -1180,7 +1098,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 k_edt_real_line<T><<<nthr / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb, er, a, tmp, scr, maxL);
             k_edt_real_final<T><<<vg, 256, 0, h->stream>>>(w.desc, w.stat, er, tmp, w.dt, w.smin, w.smax);
         };
-        if (pl.real_pitch) run_real(double());
+        if (real_double) run_real(double());
         else run_real(float());
         LAUNCHCHK();
         if (!pl.dt_2d && pl.nd_ws == 2) {
@@ -1257,13 +1175,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     // ---- seed map smoothing, hmap -----------------------------------------------------------
     HmapParams hp{(float)cfg->alpha, (float)(1.0 - cfg->alpha), pl.nd_ws == 2 ? 1 : 0};
     const float* seedmap = w.dt;
-    bool lm_done = false;  // the local maxima came out of the seed-map Gaussian's tiles
     if (pl.seeds_smooth) {
         bool any = false;
         for (int a = (pl.nd_ws == 3 ? 0 : 1); a < 3; ++a) any |= pl.sig_seeds[a] > 0.0;
         if (any) {
-            if ((r = run_gauss(h, pl, pl.sig_seeds, false, w.dt, w.sm, nb, maxZ, maxY, maxX, hp, 0,
-                               h->fuse_localmax ? w.cls : nullptr, &lm_done)) != CTWS_OK)
+            if ((r = run_gauss(h, pl, pl.sig_seeds, false, w.dt, w.sm, nb, maxZ, maxY, maxX, hp, 0)) != CTWS_OK)
                 return r;
             seedmap = w.sm;
         }
@@ -1278,7 +1194,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
     {
-        if (!lm_done) k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.smax);
+        k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.smax);
         LAUNCHCHK();
         // plateaus (equal-valued maxima candidates) and the seed CC: LDS tile union-find
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
@@ -1383,7 +1299,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     uint32_t* fst = h->trace ? w.fstat : nullptr;
     if (descent) {
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
-        // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles; k_basin_tile: the same)
+        // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
         const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
         const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
         {
@@ -1399,11 +1315,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         for (int i = 0; i < nb; ++i) any_mask |= desc[i].mask != nullptr;
         const bool plat_fill = h->plateau_fill && packed && any_mask;
         if (plat_fill) HIPCHK(hipMemsetAsync(w.plev, 0, sizeof(uint32_t) * (size_t)nb, h->stream));
-        // basin flood (k_basin.hip): the descent also records every open voxel's catchment root
-        const bool basin = h->basin && packed;
         k_descent_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
-                                                  w.front0, fst, basin ? (uint32_t*)w.A : nullptr,
-                                                  plat_fill ? w.plev : nullptr);
+                                                  w.front0, fst, plat_fill ? w.plev : nullptr);
         LAUNCHCHK();
         if (plat_fill) {
             HIPCHK(hipMemsetAsync(w.fplat, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
@@ -1411,13 +1324,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             LAUNCHCHK();
         }
         mark("flood_descent");
-        // the remaining voxels: on the catchment graph (k_basin.hip), else (or when its root pairs
-        // do not fit / converge) by the frontier relaxation (k_frontier, one voxel per lane)
-        bool basin_done = false;
-        if (basin && (r = run_basin(h, pl, nb, T, TF, max_tiles, TT, packed, wtg, dg, plat_fill, &basin_done, &fiters,
-                                    &rounds1, &fk1)) != CTWS_OK)
-            return r;
-        if (!basin_done && (r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
+        // the remaining voxels: the frontier relaxation (k_frontier, one voxel per lane)
+        if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
             return r;
         if (plat_fill) {
             // the plateau: entries, min-plus runs along x, y (, z), then the frontier from there
@@ -1450,37 +1358,16 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         // fixpoint check of every voxel (a guard: the descent argument and the frontier's
         // convergence make a violation impossible); on a violation the batch is flooded again
-        // from the seeds alone.  On by default (CTWS_VERIFY=0 turns it off).  After the basin
-        // flood the check always runs first with marks: the voxels whose label a tie between two
-        // argmin neighbours left too large (and everything below them) are repaired by the
-        // frontier relaxation from the marked voxels' neighbourhoods, then checked again.
-        auto verify = [&](uint64_t* marks) -> int {
+        // from the seeds alone.  On by default (CTWS_VERIFY=0 turns it off).
+        if (h->verify) {
             HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
-            if (marks) HIPCHK(hipMemsetAsync(marks, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
             if (pl.nd_ws == 3)
-                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter, marks);
+                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
             else
-                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter, marks);
+                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
             LAUNCHCHK();
             HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
-            return CTWS_OK;
-        };
-        bool checked = false;
-        if (basin_done) {
-            if ((r = verify(w.front0)) != CTWS_OK) return r;
-            checked = true;
-            add_timing(h, "basin_repair", h->h_counter[0] ? 1.f : 0.f);
-            if (h->h_counter[0]) {
-                if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters, &rounds1, &fk1)) != CTWS_OK)
-                    return r;
-                h->h_counter[0] = 0;
-                checked = h->verify != 0;
-                if (checked && (r = verify(nullptr)) != CTWS_OK) return r;
-            }
-        }
-        if (h->verify || checked) {
-            if (!checked && (r = verify(nullptr)) != CTWS_OK) return r;
             if (h->trace && h->h_counter[0]) {
                 fprintf(stderr, "[ctws] flood verify: violations at");
                 for (uint32_t k = 0; k < std::min(8u, h->h_counter[1]); ++k) fprintf(stderr, " %u", h->h_counter[2 + k]);
@@ -1579,9 +1466,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 // the regrow's fixpoint at the voxels it solved (the removed ones)
                 HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
                 if (pl.nd_ws == 3)
-                    k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter, nullptr);
+                    k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
                 else
-                    k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter, nullptr);
+                    k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
                 LAUNCHCHK();
                 HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
                 HIPCHK(hipStreamSynchronize(h->stream));
@@ -1820,7 +1707,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             blocks[redo[k]].status = rb[k].status;
             blocks[redo[k]].max_label = rb[k].max_label;
             blocks[redo[k]].n_ids = rb[k].n_ids;
+            if (k < h->last_bare.size()) bare[redo[k]] = h->last_bare[k];  // the re-run's result
         }
+        // the device workspace now holds the re-run's blocks only: no block of this call can be
+        // read back consistently (ctws_debug_read answers EINVAL)
+        h->last_desc.clear();
         add_timing(h, "p2_merge_reruns", (float)redo.size());
     }
     h->last_bare = std::move(bare);
@@ -2327,9 +2218,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_HOST_BATCH_VOXELS")) h->host_batch_voxels = std::max<int64_t>(1, std::atoll(t));
     if (const char* t = std::getenv("CTWS_HOST_RAMP")) h->host_ramp = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PLATEAU_FILL")) h->plateau_fill = std::atoi(t);
-    if (const char* t = std::getenv("CTWS_BASIN")) h->basin = std::atoi(t);
     if (const char* t = std::getenv("CTWS_OUTPUT_TILE")) h->output_tile = std::atoi(t);
-    if (const char* t = std::getenv("CTWS_FUSE_LOCALMAX")) h->fuse_localmax = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_MODE")) h->h2d_mode = std::atoi(t);
     if (const char* t = std::getenv("CTWS_H2D_WGS")) h->h2d_wgs = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_HOST_BATCH_BLOCKS")) h->host_batch_blocks = std::max(0, std::atoi(t));
@@ -2388,7 +2277,7 @@ void ctws_close(ctws_handle* h) {
                     h->edt_fh.p, h->edt_scratch.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
                     h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p,
-                    w.fplat, w.plev, w.flake, w.fseed, w.bctl, h->basin_edges.p};
+                    w.fplat, w.plev, w.fseed};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);

@@ -83,7 +83,7 @@ __global__ void k_gauss_row_r(const BlockDesc*, const BlockStat*, GaussParams, H
 constexpr int kGaussYxTY = 32;
 template <int R>
 __global__ void k_gauss_yx(const BlockDesc*, const BlockStat*, int, HmapParams, const double*, const double*,
-                           const float*, const float*, const uint32_t*, const uint32_t*, float*, uint8_t*, BlockStat*);
+                           const float*, const float*, const uint32_t*, const uint32_t*, float*);
 
 // k_cc.hip
 __global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, const uint32_t*);
@@ -154,27 +154,12 @@ __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64
 template <int ND>
 __global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
                                const uint64_t*, uint32_t*);
-__global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, uint32_t*, uint64_t*, uint8_t*,
-                               uint64_t*, uint64_t*, uint32_t*, uint32_t*, uint32_t*);
+__global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint8_t*,
+                               uint64_t*, uint64_t*, uint32_t*, uint32_t*);
 template <int ND, int CW, int CY, int CZ>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
                            const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int);
-// k_basin.hip: the descent flood's open voxels on the catchment graph
-template <int ND>
-__global__ void k_basin_edges(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint64_t*,
-                              const uint64_t*, uint32_t*, uint4*, uint32_t*, uint32_t);
-__global__ void k_basin_relax(const uint4*, const uint32_t*, uint32_t, uint32_t*, uint32_t*, int);
-__global__ void k_basin_c(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint64_t*,
-                          const uint64_t*, const uint32_t*, uint64_t*);
-template <int ND>
-__global__ void k_basin_keys(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint64_t*,
-                             uint64_t*, uint64_t*, uint32_t*);
-__global__ void k_basin_lake_reset(const BlockDesc*, const BlockStat*, const uint64_t*, uint64_t*);
-template <int ND>
-__global__ void k_basin_tile(const BlockDesc*, const BlockStat*, const uint64_t*, const uint64_t*, const uint64_t*,
-                             uint32_t*);
-__global__ void k_basin_hop(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, uint64_t*);
 // k_eval.hip (VI / Rand contingency table)
 __global__ void k_eval_add(const uint64_t*, const uint64_t*, int64_t, int, uint64_t*, unsigned long long*, int64_t,
                            uint64_t*, unsigned long long*, int64_t, uint64_t*, unsigned long long*, int64_t,
@@ -204,7 +189,7 @@ __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint6
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
 template <int ND>
 __global__ void k_flood_verify(const BlockDesc*, const BlockStat*, const float*, const uint64_t*, const uint64_t*,
-                               uint32_t*, uint64_t*);
+                               uint32_t*);
 constexpr int kWordWaves = 4;  // waves per workgroup of the word-tiled kernels
 __global__ void k_flood_reset(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
                               const uint64_t*, uint64_t*, uint8_t*);

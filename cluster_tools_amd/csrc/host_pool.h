@@ -23,6 +23,12 @@
 namespace ctws_host {
 
 // parallel_for over [0, n): the calling thread works too; returns when every index is done.
+//
+// Generations: a worker joins a parallel_for by copying (fn, n) under the lock and counting
+// itself active; parallel_for returns only when every index is done AND no worker is still
+// inside its claim loop.  So a worker can never carry a claim (next_ index) or a stale fn from
+// one generation into the next: next_ / done_ are reset for generation g + 1 only after every
+// worker of generation g has left work().
 class WorkerPool {
    public:
     explicit WorkerPool(int threads) {
@@ -52,19 +58,19 @@ class WorkerPool {
             ++gen_;
         }
         cv_.notify_all();
-        work();
+        work(&fn, n);
         std::unique_lock<std::mutex> l(m_);
-        cv_done_.wait(l, [&]() { return done_.load() == n_; });
-        fn_ = nullptr;
+        cv_done_.wait(l, [&]() { return done_.load() >= n_ && active_ == 0; });
+        fn_ = nullptr;  // (under the lock: a late worker sees no work and waits for the next gen)
     }
 
    private:
-    void work() {
+    void work(const std::function<void(int64_t)>* fn, int64_t n) {
         while (true) {
             const int64_t i = next_.fetch_add(1);
-            if (i >= n_) return;
-            (*fn_)(i);
-            if (done_.fetch_add(1) + 1 == n_) {
+            if (i >= n) return;
+            (*fn)(i);
+            if (done_.fetch_add(1) + 1 == n) {
                 std::lock_guard<std::mutex> g(m_);
                 cv_done_.notify_all();
             }
@@ -73,20 +79,31 @@ class WorkerPool {
     void loop() {
         uint64_t seen = 0;
         while (true) {
+            const std::function<void(int64_t)>* fn;
+            int64_t n;
             {
                 std::unique_lock<std::mutex> l(m_);
                 cv_.wait(l, [&]() { return stop_ || (gen_ != seen && fn_ != nullptr); });
                 if (stop_) return;
                 seen = gen_;
+                fn = fn_;
+                n = n_;
+                ++active_;
             }
-            work();
+            work(fn, n);
+            {
+                std::lock_guard<std::mutex> g(m_);
+                --active_;
+            }
+            cv_done_.notify_all();
         }
     }
     std::vector<std::thread> th_;
     std::mutex m_;
     std::condition_variable cv_, cv_done_;
-    const std::function<void(int64_t)>* fn_ = nullptr;
-    int64_t n_ = 0;
+    const std::function<void(int64_t)>* fn_ = nullptr;  // guarded by m_
+    int64_t n_ = 0;                                     // guarded by m_
+    int active_ = 0;                                    // workers inside work(), guarded by m_
     std::atomic<int64_t> next_{0}, done_{0};
     uint64_t gen_ = 0;
     bool stop_ = false;

@@ -729,9 +729,8 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
     }
     __syncthreads();
     // exit entry: kDescRes | label when the chain ends at a seed root of this tile; the block
-    // index of the root when it ends at a root without a seed (the root itself: kDescRes | 0),
-    // so that k_descent_init learns the catchment root of every open voxel (k_basin.hip); else
-    // the block index of the first voxel outside the tile (k_descent_init follows it)
+    // index of the root when it ends at a root without a seed (the root itself: kDescRes | 0);
+    // else the block index of the first voxel outside the tile (k_descent_init follows it)
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int c = threadIdx.x + k * NT;
@@ -767,16 +766,11 @@ template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, c
 // flood (INF key).  Bitmaps, one word per 64 voxels of a row (the 64 lanes of a wave cover
 // exactly one word): open = not final yet, chg = final (the first "changed" set, whose
 // neighbours form the first frontier).
-// With `cr` (the basin flood, k_basin.hip): an open voxel's par entry becomes the block index
-// of its catchment root (the root without a seed its descent ends at; the root keeps
-// kDescRes | 0), and cr[root] = INF.  Rewriting par in place while other waves hop through it
-// is safe: every value a hop can read (the old pointer or the root) lies on the same chain.
 __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                      const float* __restrict__ h, uint32_t* __restrict__ par,
+                                                      const float* __restrict__ h, const uint32_t* __restrict__ par,
                                                       uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
                                                       uint64_t* __restrict__ open, uint64_t* __restrict__ chg,
-                                                      uint32_t* __restrict__ nopen, uint32_t* __restrict__ cr,
-                                                      uint32_t* __restrict__ plev) {
+                                                      uint32_t* __restrict__ nopen, uint32_t* __restrict__ plev) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     uint32_t cnt_open = 0;  // statistics (CTWS_TRACE): voxels left to the relaxation
@@ -797,7 +791,7 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
     for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
         int64_t gi[U];
         bool valid[U];
-        uint32_t e[U], last[U];
+        uint32_t e[U];
         float hv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -808,12 +802,10 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
             gi[u] = B.base + (valid[u] ? row * B.X + x : 0);
             e[u] = gbl(par)[gi[u]];
             hv[u] = gbl(h)[gi[u]];
-            last[u] = (uint32_t)(gi[u] - B.base);  // the root when the chain has no hop
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (!valid[u]) e[u] = kDescRes;
-        const uint32_t e0[U] = {e[0], e[1], e[2], e[3]};
         for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
             bool more = false;
 #pragma unroll
@@ -821,10 +813,7 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
             if (!more) break;
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (!(e[u] & kDescRes)) {
-                    last[u] = e[u];
-                    e[u] = gbl(par)[B.base + e[u]];
-                }
+                if (!(e[u] & kDescRes)) e[u] = gbl(par)[B.base + e[u]];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -834,10 +823,6 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
                 key[gi[u]] = res ? (((uint64_t)ordf(hv[u]) << 32) | (uint64_t)lr) : kPackInf;
                 fixedv[gi[u]] = res ? 1 : 0;
                 if (want_lev && !res && !gbl(B.mask)[gi[u] - B.base]) lev = max(lev, ordf(hv[u]));
-                if (cr && !res) {
-                    if (e0[u] & kDescRes) cr[gi[u]] = 0xFFFFFFFFu;       // a root: no catchment pass yet
-                    else if (last[u] != e0[u]) par[gi[u]] = last[u];  // -> its root
-                }
             }
             const uint64_t op = __ballot(valid[u] && !res);
             const uint64_t fi = __ballot(valid[u] && res);
@@ -1260,8 +1245,7 @@ __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restr
 template <int ND>
 __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint64_t* __restrict__ key,
-                                                      const uint64_t* __restrict__ open, uint32_t* __restrict__ flag,
-                                                      uint64_t* __restrict__ mark) {
+                                                      const uint64_t* __restrict__ open, uint32_t* __restrict__ flag) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     constexpr int U = 4, R = U + 2;
@@ -1353,30 +1337,15 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
                 if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + zb + (int64_t)y * B.X + x);
             }
             bad |= b1;
-            // mark (the basin flood's repair, k_basin.hip): the violator's neighbours become
-            // "changed", so that the frontier relaxation re-evaluates the violator itself
-            if (mark && __ballot(b1)) {
-                const uint64_t bm = __ballot(b1);
-                if (lane == 0) {
-                    uint64_t* mw = mark + B.fbase + ((int64_t)z * B.Y + y) * wpr + xw;
-                    atomicOr((unsigned long long*)mw, (unsigned long long)((bm << 1) | (bm >> 1) | bm));
-                    if ((bm & 1ull) && xw > 0) atomicOr((unsigned long long*)(mw - 1), 1ull << 63);
-                    if ((bm >> 63) && xw + 1 < wpr) atomicOr((unsigned long long*)(mw + 1), 1ull);
-                    if (y > 0) atomicOr((unsigned long long*)(mw - wpr), (unsigned long long)bm);
-                    if (y + 1 < B.Y) atomicOr((unsigned long long*)(mw + wpr), (unsigned long long)bm);
-                    if (ND == 3 && z > 0) atomicOr((unsigned long long*)(mw - (int64_t)B.Y * wpr), (unsigned long long)bm);
-                    if (ND == 3 && z + 1 < B.Z) atomicOr((unsigned long long*)(mw + (int64_t)B.Y * wpr), (unsigned long long)bm);
-                }
-            }
         }
       }
     }
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 template __global__ void k_flood_verify<3>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
-                                           const uint64_t*, uint32_t*, uint64_t*);
+                                           const uint64_t*, uint32_t*);
 template __global__ void k_flood_verify<2>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
-                                           const uint64_t*, uint32_t*, uint64_t*);
+                                           const uint64_t*, uint32_t*);
 
 // seeds only (fallback after a failed verification)
 __global__ void __launch_bounds__(256) k_flood_reset(const BlockDesc* __restrict__ D, const BlockStat* S,

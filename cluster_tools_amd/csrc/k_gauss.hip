@@ -329,19 +329,12 @@ constexpr int kYxP = 129;  // LDS pitch: 128 + 1
 
 __host__ __device__ constexpr int gauss_yx_tx(int R) { return 128 - 2 * R; }
 
-//
-// lm_cls (2-D ws, the seed map): the local maxima come out of the same tile (k_localmax's
-// classes, watershed.py:187-192 -> vigra localMaxima, 8-neighbourhood): tiles then overlap by one
-// voxel on every side and each stores — and classifies — only its interior (kYxTY - 2) x (TX - 2)
-// outputs, whose 8 neighbours it holds in LDS; the separate k_localmax pass (4 B read per voxel)
-// goes away.  Sw: the same stats as S, for the plateau count.
 template <int R>
 __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ D, const BlockStat* S, int hmap_src,
                                                   HmapParams hp, const double* __restrict__ taps_y,
                                                   const double* __restrict__ taps_x, const float* __restrict__ in,
                                                   const float* __restrict__ dt, const uint32_t* smin,
-                                                  const uint32_t* smax, float* __restrict__ out,
-                                                  uint8_t* __restrict__ lm_cls, BlockStat* Sw) {
+                                                  const uint32_t* smax, float* __restrict__ out) {
     constexpr int TX = gauss_yx_tx(R);
     constexpr int NROW = kYxTY + 2 * R;
     constexpr int NL = NROW / 2;  // staged rows per thread
@@ -350,16 +343,14 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
     const BlockStat& st = S[blockIdx.y];
     if (!st.active) return;
     const int Y = B.Y, X = B.X;
-    const bool lm = lm_cls != nullptr;
-    const int SY = lm ? kYxTY - 2 : kYxTY, SX = lm ? TX - 2 : TX;  // tile stride
-    const int ntx = (X + SX - 1) / SX, nty = (Y + SY - 1) / SY;
+    const int ntx = (X + TX - 1) / TX, nty = (Y + kYxTY - 1) / kYxTY;
     // XCD-contiguous tile order
     const int n = gridDim.x, per = n >> 3;
     const int bid = blockIdx.x;
     const int t = bid < (per << 3) ? (bid & 7) * per + (bid >> 3) : bid;
     if (t >= B.Z * nty * ntx) return;
     const int z = t / (nty * ntx), rem = t - z * (nty * ntx);
-    const int y0 = (rem / ntx) * SY - (lm ? 1 : 0), x0 = (rem % ntx) * SX - (lm ? 1 : 0);
+    const int y0 = (rem / ntx) * kYxTY, x0 = (rem % ntx) * TX;
     const int tid = threadIdx.x;
     const int c = tid & 127, half = tid >> 7;
     auto refl = [](int p, int L) { return min(max(reflect_idx(p, L), 0), L - 1); };
@@ -450,54 +441,18 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
     }
     __syncthreads();
     // ---- coalesced stores of the valid part of the tile
-    if (!lm) {
-        const int ny = min(kYxTY, Y - y0), nx = min(TX, X - x0);
-        gwptr_t<float> o = gblw(out) + sbase + (int64_t)y0 * X + x0;
-        for (int v = tid; v < kYxTY * TX; v += 256) {
-            const int pp = v / TX, xx = v - pp * TX;
-            if (pp < ny && xx < nx) o[(int64_t)pp * X + xx] = win_s[pp * kYxP + xx];
-        }
-        return;
+    const int ny = min(kYxTY, Y - y0), nx = min(TX, X - x0);
+    gwptr_t<float> o = gblw(out) + sbase + (int64_t)y0 * X + x0;
+    for (int v = tid; v < kYxTY * TX; v += 256) {
+        const int pp = v / TX, xx = v - pp * TX;
+        if (pp < ny && xx < nx) o[(int64_t)pp * X + xx] = win_s[pp * kYxP + xx];
     }
-    // the interior: store, and classify as k_localmax does (gt: a strictly greater neighbour,
-    // eq: an equal one; in a slice with a positive dt value no zero voxel is a maximum)
-    const float NEG = -__builtin_huge_valf();
-    const bool pos = smax[B.sbase + z] > 0x80000000u;  // ordf(+0.0f)
-    uint32_t nplat = 0;
-    constexpr int LSY = kYxTY - 2, LSX = TX - 2;  // (= SY, SX: constants for the index split)
-    for (int v = tid; v < LSY * LSX; v += 256) {
-        const int pp = 1 + v / LSX, xx = 1 + v % LSX;
-        const int y = y0 + pp, x = x0 + xx;
-        if (y >= Y || x >= X) continue;
-        const int64_t gi = sbase + (int64_t)y * X + x;
-        const float cc = win_s[pp * kYxP + xx];
-        gblw(out)[gi] = cc;
-        bool gt = false, eq = false;
-#pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-                if (dy == 0 && dx == 0) continue;
-                const bool in_b = y + dy >= 0 && y + dy < Y && x + dx >= 0 && x + dx < X;
-                const float w = in_b ? win_s[(pp + dy) * kYxP + xx + dx] : NEG;
-                gt |= w > cc;
-                eq |= w == cc;
-            }
-        if (cc == 0.0f && pos) {
-            gt = true;
-            eq = false;
-        }
-        gblw(lm_cls)[gi] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
-        nplat += eq ? 1u : 0u;
-    }
-    nplat = wg_reduce_u32(nplat, OpAdd());
-    if (threadIdx.x == 0 && nplat) atomicAdd(&Sw[blockIdx.y].plateau, nplat);
 }
 
 #define CTWS_GAUSS_R(R)                                                                                          \
     template __global__ void k_gauss_yx<R>(const BlockDesc*, const BlockStat*, int, HmapParams, const double*,     \
                                            const double*, const float*, const float*, const uint32_t*,             \
-                                           const uint32_t*, float*, uint8_t*, BlockStat*);                         \
+                                           const uint32_t*, float*);                                               \
     template __global__ void k_gauss_col_r<32, R>(const BlockDesc*, const BlockStat*, GaussParams, HmapParams,      \
                                                   const double*, const float*, const float*, const uint32_t*,       \
                                                   const uint32_t*, float*);                                        \

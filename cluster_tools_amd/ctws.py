@@ -39,6 +39,9 @@ def lib():
                               % (LIB_PATH, _HERE))
             L = C.CDLL(LIB_PATH)
             L.ctws_abi_version.restype = C.c_int
+            if L.ctws_abi_version() != ABI_VERSION:
+                raise OSError("libctws.so ABI version %d, expected %d (include/ctws.h): rebuild it"
+                              % (L.ctws_abi_version(), ABI_VERSION))
             L.ctws_open.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
             L.ctws_close.argtypes = [C.c_void_p]
             L.ctws_close.restype = None
@@ -64,6 +67,9 @@ def lib():
             _lib = L
         return _lib
 
+
+# include/ctws.h CTWS_ABI_VERSION (2: the library's own RCCL communicator entry points removed)
+ABI_VERSION = 2
 
 EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
                     'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_unique_u64', 'ctws_unique_counts_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',

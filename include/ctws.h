@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define CTWS_ABI_VERSION 1
+#define CTWS_ABI_VERSION 2
 
 /* error codes */
 #define CTWS_OK            0

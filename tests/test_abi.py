@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for f in declared_functions():
         assert hasattr(lib, f), f
     assert set(declared_functions()) == set(ctws.EXPORTED_SYMBOLS)
-    assert lib.ctws_abi_version() == 1
+    assert lib.ctws_abi_version() == ctws.ABI_VERSION == 2
 
 
 def test_struct_layout_matches_header(tmp_path):

@@ -2,8 +2,7 @@
 
 The flood's fixpoint (K = f(min of the neighbours' keys), k_flood.hip) is unique, so every
 chunk brick (CTWS_FRONTIER_CHUNK2D / _3D), a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
-non-converged re-queue path runs), the masked-plateau fill switched off (CTWS_PLATEAU_FILL=0) and the
-catchment-graph flood instead of the frontier relaxation (CTWS_BASIN=1) must reproduce the oracle's flood model bit for bit on every
+non-converged re-queue path runs), and the masked-plateau fill switched off (CTWS_PLATEAU_FILL=0) must reproduce the oracle's flood model bit for bit on every
 parity case, as the default schedule does (test_gpu_parity.py::test_flood_matches_model_exactly).
 The knobs are read when a handle is opened.
 """
@@ -26,13 +25,8 @@ VARIANTS = {
     'one_sweep': {'CTWS_FRONTIER_REPS': '1'},
     # masked blocks' plateaus relaxed hop by hop instead of filled by run scans (k_plateau.hip)
     'no_plateau_fill': {'CTWS_PLATEAU_FILL': '0'},
-    # the open voxels on the catchment graph instead of by the frontier relaxation (k_basin.hip)
-    'basin': {'CTWS_BASIN': '1'},
-    'basin_no_plateau_fill': {'CTWS_BASIN': '1', 'CTWS_PLATEAU_FILL': '0'},
     # cropped blocks' uint64 output through the word-tiled k_output instead of k_output_crop
     'output_words': {'CTWS_OUTPUT_TILE': '0'},
-    # 2-D local maxima in the seed-map Gaussian's tiles (opt-in) instead of the separate k_localmax pass
-    'localmax_fused': {'CTWS_FUSE_LOCALMAX': '1'},
 }
 
 
