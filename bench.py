@@ -15,10 +15,16 @@ output through ctws_ws_blocks) is reported beside it as `host_resident`.
 `--config N` runs the other BASELINE configs on one GPU (config 2: 512^3 3-D; config 4: 1024^3
 with halo [8,32,32]; config 5: one z-slab share of the 2048^3 uint8 two-pass run).
 
-Multi-GPU (torchrun, one process per GPU): weak scaling — every rank processes its own
-volume of the config; after each step the per-block label counts are all-gathered over RCCL
-and exclusively scanned into compact global id offsets (the exchange of
+Multi-GPU, one process per GPU: `--gpus N` starts the N ranks itself (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT in each child's environment, before anything in the
+parent touches a GPU; the parent waits and fails when a rank fails), or runs as one rank of a
+torchrun launch when WORLD_SIZE is set.  Weak scaling (`value`): every rank processes its own
+z-slab volume of the config; after each step the per-block label counts are all-gathered over
+RCCL and exclusively scanned into compact global id offsets (the exchange of
 relabel/find_labeling.py:104-116).  value = inner voxels of all ranks / max-over-ranks time.
+`strong_config4` (every run): config 4's whole 1024^3 volume cut into N z-slabs of the block grid
+(BASELINE.json configs[3]: "blocks sharded over 8 MI355X, RCCL label-offset scan").
+Ranks that share a GPU (a rehearsal on a 1-GPU box) use a gloo group instead of RCCL.
 
 The CPU baseline (rank 0, N = 1) is the oracle (oracle/, the C++ restatement of the
 reference path) on a bounded sample of the same workload, driven like LocalTask: one
@@ -374,48 +380,84 @@ def progress(msg):
 _T0 = time.time()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=5)
-    ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--config', type=int, default=DEFAULT_CONFIG, choices=sorted(CONFIGS))
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe-inclusive) pass')
-    ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end n5 workflow run')
-    ap.add_argument('--e2e-z', type=int, default=64, help='z extent of the end-to-end sub-volume')
-    ap.add_argument('--cpu-cores', type=int, default=0, help='cap on the CPU baseline jobs (0: usable cores)')
-    ap.add_argument('--scaling', choices=('weak', 'strong'), default='weak',
-                    help='weak: every rank runs the config\'s single-GPU workload (default); strong: the '
-                         'config\'s whole volume (config 4: 1024^3, config 5: 2048^3) in z-slabs over the ranks')
-    ap.add_argument('--streams', type=int, default=3,
-                    help='library handles (one HIP stream each) per GPU, driven from host threads; '
-                         'the blocks are split between them so their launch-bound phases overlap')
-    args = ap.parse_args()
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
 
+
+def launch_ranks(n, argv):
+    """`--gpus N` without a launcher: start N ranks of this script (one process per GPU) and wait.
+
+    Runs before anything in this process touches a GPU (no exec from a GPU process).  Children
+    get the torchrun environment; rank 0 prints the JSON line.  A failing rank ends the others
+    (their exact PIDs) and the parent exits with its code."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), CTWS_BENCH_CHILD='1')
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print('[bench] rank %d exited with %d: stopping the other ranks' % (procs.index(p), code),
+                      file=sys.stderr, flush=True)
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def dist_env():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    cfg = CONFIGS[args.config]
-    two_pass = cfg.get('two_pass', False)
+    local_rank = int(os.environ.get('LOCAL_RANK', str(rank)))
+    return world, rank, local_rank
 
-    cpu, ref_block = None, None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, ref_block = cpu_baseline(args.config, args.cpu_cores)
 
+def launch_check():
+    """--launch-check: the process group of the ranks, no GPU (tests/test_bench_launch.py)."""
     import torch
     import torch.distributed as dist
+    world, rank, local_rank = dist_env()
+    if os.environ.get('CTWS_BENCH_FAIL_RANK') == str(rank):
+        sys.exit(3)  # test hook: a rank that dies before joining the group
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    t = torch.tensor([rank, local_rank, world], dtype=torch.int64)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    if rank == 0:
+        print(json.dumps({'launch_check': True, 'world_size': dist.get_world_size(),
+                          'ranks': [p.tolist() for p in parts]}), flush=True)
+    dist.destroy_process_group()
+
+
+def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req, host_pass=False,
+                 keep_block=None):
+    """Stage one workload in HBM, run `warmup` + timed `steps` steps, and measure it.
+
+    A step = the `_ws_block` (and `_ws_pass2`) of every block of the rank's share, then the RCCL
+    offset scan.  Returns the timing, the per-stage HIP-event times of one extra single-stream
+    step, the algorithmic bytes, and (host_pass, rank 0) the PCIe-inclusive rate."""
+    import torch
     from cluster_tools_amd import ctws
     from cluster_tools_amd.synthetic import boundary_map_torch, ellipsoid_mask_torch
     from cluster_tools_amd.watershed import sharded
-
-    torch.cuda.set_device(local_rank)
-    dev = torch.device('cuda', local_rank)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
-
-    shape = tuple(cfg['shape'])
-    geo = volume_geometry(cfg, rank, world, args.scaling)
+    from cluster_tools_amd.watershed.watershed import pass2_levels
+    import torch.distributed as dist
+    cfg = CONFIGS[cfg_id]
+    two_pass = cfg.get('two_pass', False)
+    geo = volume_geometry(cfg, rank, world, scaling)
     full = geo['full']
     origin = (geo['g0'], 0, 0)
     gen = dict(seed=cfg['seed'], device=dev, dtype=cfg.get('dtype', 'float32'), pitch=cfg.get('pitch', (24, 24, 24)),
@@ -427,7 +469,7 @@ def main():
         z1 = min(geo['gshape'][0], z0 + zs)
         vol[z0:z1] = boundary_map_torch((z1 - z0,) + tuple(geo['gshape'][1:]),
                                         **dict(gen, origin=(origin[0] + z0, 0, 0)))
-        progress('synthetic input z %d..%d' % (z0, z1))
+    progress('config %d (%s): synthetic input of rank %d generated, %s' % (cfg_id, scaling, rank, geo['gshape']))
     mvol = ellipsoid_mask_torch(geo['gshape'], origin, full, device=dev) if cfg.get('mask') else None
     blist = geo['blocks']
     # two-pass: the pass-1 labels of the region (own slab + z halos from the neighbour ranks)
@@ -457,19 +499,24 @@ def main():
     del vol
     if two_pass:
         colour = {b['block_id']: block_colour(cfg, geo, b) for b in blist}
-        passes = [[blocks[i] for i in sorted(blocks) if colour[i] == c] for c in (0, 1)]
-        for b in passes[1]:
+        p1 = [blocks[i] for i in sorted(blocks) if colour[i] == 0]
+        p2 = [blocks[i] for i in sorted(blocks) if colour[i] == 1]
+        for b in p2:
             b['crop_relabel'] = False
             b['initial_seeds'] = torch.empty(tuple(b['input'].shape[-3:]), dtype=torch.int64, device=dev)
             pass2_outer += int(b['input'].numel())
+        # pass 2 in the workflow's schedule (watershed.make_batches): dependency levels of the
+        # sequential loop, each level reading ds_out after the levels before it wrote
+        lv = pass2_levels([(b['osl'], b['isl']) for b in p2])
+        groups = [(0, p1)] + [(1, [b for b, l in zip(p2, lv) if l == k]) for k in range(max(lv) + 1 if lv else 0)]
     else:
-        passes = [list(blocks.values())]
+        groups = [(0, list(blocks.values()))]
+    groups = [(pid, g) for pid, g in groups if g]
     torch.cuda.synchronize()
 
-    nstreams = max(1, min(args.streams, min(len(p) for p in passes)))
-    handles = [ctws.Handle(local_rank) for _ in range(nstreams)]
+    nstreams = max(1, min(nstreams_req, max(len(g) for _, g in groups)))
+    handles = [ctws.Handle(dev.index) for _ in range(nstreams)]
     pool = ThreadPoolExecutor(nstreams) if nstreams > 1 else None
-    nblocks = len(blocks)
     stage_ms = {}
     offsets = {}
 
@@ -477,27 +524,31 @@ def main():
         ns = nstreams if ns is None else ns
         into = stage_ms if into is None else into
         res = []
-        for pid, pblocks in enumerate(passes):
+        exchanged = False
+        for pid, gblocks in groups:
             if pid == 1:
-                # the neighbour slabs' pass-1 labels in the z halos (RCCL point-to-point)
-                sharded.exchange_z_halos(out_vol, geo['lo'], geo['hi'])
-                for b in pblocks:  # initial_seeds = ds_out[input_bb] (two_pass_watershed.py:228)
+                if not exchanged:
+                    # the neighbour slabs' pass-1 labels in the z halos (point-to-point)
+                    sharded.exchange_z_halos(out_vol, geo['lo'], geo['hi'])
+                    exchanged = True
+                for b in gblocks:  # initial_seeds = ds_out[input_bb] (two_pass_watershed.py:228)
                     b['initial_seeds'].copy_(out_vol[b['osl']])
-            # contiguous shares of the pass's blocks, one per handle (stream)
-            parts = [pblocks[len(pblocks) * i // ns:len(pblocks) * (i + 1) // ns] for i in range(ns)]
+            nsg = max(1, min(ns, len(gblocks)))
+            # contiguous shares of the group's blocks, one per handle (stream)
+            parts = [gblocks[len(gblocks) * i // nsg:len(gblocks) * (i + 1) // nsg] for i in range(nsg)]
 
             def run(i):
                 return handles[i].ws_blocks_device(cfg['task'], cfg['block_shape'], parts[i], pass_id=pid)
 
-            rs = list(pool.map(run, range(ns))) if ns > 1 else [run(0)]
+            rs = list(pool.map(run, range(nsg))) if nsg > 1 else [run(0)]
             r = [x for part in rs for x in part]
             if record:
                 # stage times summed over the handles (overlapping streams: an upper bound)
-                for hh in handles[:ns]:
+                for hh in handles[:nsg]:
                     for k, v in hh.timings().items():
                         into[k] = into.get(k, 0.0) + v
             if two_pass:
-                for b, (st, _, _) in zip(pblocks, r):
+                for b, (st, _, _) in zip(gblocks, r):
                     if st in (0, 2):
                         out_vol[b['isl']] = b['output']
             res += r
@@ -508,26 +559,23 @@ def main():
             offsets['scan'], offsets['n_ids'] = sharded.compact_offsets(allc)
         return res
 
-    progress('inputs staged: %d blocks, %d outer voxels' % (len(blocks), outer_vox))
-    for k in range(args.warmup):
+    for k in range(warmup):
         step(False)
-        progress('warmup step %d' % k)
+        progress('config %d warmup step %d' % (cfg_id, k))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
+    for k in range(steps):
         step(True)
-        progress('step %d' % k)
+        progress('config %d step %d' % (cfg_id, k))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    stage_ms = {k: v / args.steps for k, v in stage_ms.items()}
+    dt_rank = time.perf_counter() - t0
+    dt = sharded.all_reduce_max(dt_rank, device=dev)
+    ms_ranks = [round(t / steps * 1e3, 3) for t in sharded.all_gather_float(dt_rank, device=dev)]
+    stage_ms = {k: v / steps for k, v in stage_ms.items()}
     # roofline durations: one more, untimed step with every block on ONE stream, so that no
     # other stream's kernels share the chip while a launch runs (with concurrent streams the
     # HIP-event duration of a launch includes the time it shares)
@@ -537,21 +585,12 @@ def main():
         torch.cuda.synchronize()
     else:
         stage_1 = stage_ms
+    inner_all = sharded.all_reduce_sum_int(inner_vox, device=dev)
 
-    inner_all = inner_vox
-    if world > 1:
-        t = torch.tensor([inner_vox], dtype=torch.int64, device=dev)
-        dist.all_reduce(t)
-        inner_all = int(t.item())
-    total_vox = inner_all * args.steps
-    value = total_vox / dt / 1e9
-    ms_per_step = dt / args.steps * 1e3
-
-    # ---- host-resident pass (PCIe-inclusive): numpy in, numpy uint64 out --------------------
     host = None
-    if rank == 0 and not args.no_host and not two_pass:
+    if host_pass and rank == 0 and not two_pass:
         hb = []
-        for b in passes[0]:
+        for b in groups[0][1]:
             hb.append(dict(input=b['input'].cpu().numpy(), inner_begin=b['inner_begin'],
                            inner_shape=list(b['output'].shape), crop_relabel=b['crop_relabel'],
                            block_id=b['block_id'],
@@ -559,14 +598,14 @@ def main():
                            out=np.empty(tuple(b['output'].shape), dtype=np.uint64)))
         handles[0].ws_blocks(cfg['task'], cfg['block_shape'], hb)  # warm the staging buffers
         ths = []
-        for _ in range(max(1, min(3, args.steps))):
+        for _ in range(max(1, min(3, steps))):
             t0 = time.perf_counter()
             handles[0].ws_blocks(cfg['task'], cfg['block_shape'], hb)
             ths.append(time.perf_counter() - t0)
         th = min(ths)
         phases = {k: round(v, 2) for k, v in handles[0].timings().items() if k.startswith('host_')}
         same = all(np.array_equal(h_['out'], b['output'].cpu().numpy().view(np.uint64))
-                   for h_, b in zip(hb, passes[0]))
+                   for h_, b in zip(hb, groups[0][1]))
         h2d = int(sum(x['input'].nbytes + (x['mask'].nbytes if x['mask'] is not None else 0) for x in hb))
         host = {'value': round(inner_vox / th / 1e9, 4), 'unit': 'Gvoxel/s', 'ms_per_step': round(th * 1e3, 3),
                 'runs_ms': [round(t * 1e3, 1) for t in ths],
@@ -575,23 +614,137 @@ def main():
                 'h2d_bytes': h2d, 'd2h_bytes': int(inner_vox * 4), 'host_output_bytes': int(inner_vox * 8),
                 'phases_ms': phases, 'pcie': pcie_rates(dev), 'matches_device_path': bool(same)}
         del hb
+    kept = None
+    if keep_block is not None and keep_block in blocks:
+        kept = blocks[keep_block]['output'].cpu().numpy().view(np.uint64)
+    for hh in handles:
+        hh.close()
+    if pool:
+        pool.shutdown()
+    out = dict(cfg_id=cfg_id, geo=geo, full=full, dt=dt, ms_ranks=ms_ranks, steps=steps,
+               inner_vox=inner_vox, outer_vox=outer_vox, pass2_outer=pass2_outer, inner_all=inner_all,
+               nblocks=len(blocks), npass=2 if two_pass else 1, ngroups=len(groups), nstreams=nstreams,
+               stage_ms=stage_ms, stage_1=stage_1, n_ids=offsets.get('n_ids'), host=host, kept=kept)
+    del blocks, groups, out_vol, mvol
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def roofline_of(cfg, m):
+    """Per-stage GB/s, the dominant stage's roofline and the pipeline roofline of a measurement."""
+    def per_stage(sm):
+        return {k: sum(sm.get(p, 0.0) for p in STAGE_PARTS.get(k, (k,))) for k in stage_bytes(cfg)}
+    sbytes = stage_bytes(cfg)
+    stages = per_stage(m['stage_1'])
+    stage_gbs = {}
+    for k, ms in stages.items():
+        b, unit = sbytes[k]
+        nbytes = b * (m['outer_vox'] if unit == 'outer' else m['inner_vox'])
+        stage_gbs[k] = round(nbytes / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
+    # roofline of the dominant stage by time (algorithmic bytes / its single-stream HIP-event time)
+    dom = max(stages, key=lambda k: stages[k])
+    dom_ms = stages[dom]
+    b_unit, unit = sbytes[dom]
+    dom_bytes = b_unit * (m['outer_vox'] if unit == 'outer' else m['inner_vox'])
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    ms_per_step = m['dt'] / m['steps'] * 1e3
+    alg_total = alg_bytes(cfg, m['outer_vox'], m['inner_vox'], m['pass2_outer'])
+    pipe = alg_total / (ms_per_step * 1e-3) / 1e9
+    return dict(dom=dom, dom_ms=dom_ms, dom_bytes=dom_bytes, b_unit=b_unit, unit=unit, achieved=achieved,
+                stage_gbs=stage_gbs, alg_total=alg_total, pipe=pipe, ms_per_step=ms_per_step)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--config', type=int, default=DEFAULT_CONFIG, choices=sorted(CONFIGS))
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe-inclusive) pass')
+    ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end n5 workflow run')
+    ap.add_argument('--no-strong', action='store_true', help='skip the strong-scaling config 4 run')
+    ap.add_argument('--strong-steps', type=int, default=3)
+    ap.add_argument('--e2e-z', type=int, default=64, help='z extent of the end-to-end sub-volume')
+    ap.add_argument('--cpu-cores', type=int, default=0, help='cap on the CPU baseline jobs (0: usable cores)')
+    ap.add_argument('--scaling', choices=('weak', 'strong'), default='weak',
+                    help='weak: every rank runs the config\'s single-GPU workload (default); strong: the '
+                         'config\'s whole volume (config 4: 1024^3, config 5: 2048^3) in z-slabs over the ranks')
+    ap.add_argument('--streams', type=int, default=3,
+                    help='library handles (one HIP stream each) per GPU, driven from host threads; '
+                         'the blocks are split between them so their launch-bound phases overlap')
+    ap.add_argument('--launch-check', action='store_true',
+                    help='start the ranks and their process group only (no GPU): a launcher test')
+    args = ap.parse_args()
+
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        # no launcher around us: start the ranks ourselves (nothing here has touched a GPU)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local_rank = dist_env()
+    if args.launch_check:
+        launch_check()
+        return
+    if world != args.gpus:
+        progress('WORLD_SIZE %d overrides --gpus %d' % (world, args.gpus))
+    cfg = CONFIGS[args.config]
+    two_pass = cfg.get('two_pass', False)
+
+    cpu, ref_block = None, None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, ref_block = cpu_baseline(args.config, args.cpu_cores)
+
+    import torch
+    import torch.distributed as dist
+
+    ndev = torch.cuda.device_count()  # (does not initialise the GPU)
+    dev_index = local_rank % max(1, ndev)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device('cuda', dev_index)
+    backend = None
+    if world > 1:
+        # RCCL needs one device per rank; ranks sharing a GPU (a rehearsal) use gloo
+        backend = os.environ.get('CTWS_DIST_BACKEND') or ('nccl' if ndev >= world else 'gloo')
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
+    devices = sorted(set(int(x) for x in (sharded_gather_devices(dev_index, dev) if world > 1 else [dev_index])))
+
+    m = run_workload(args.config, args.scaling, rank, world, dev, args.steps, args.warmup, args.streams,
+                     host_pass=not args.no_host, keep_block=ref_block[0] if ref_block else None)
+    rf = roofline_of(cfg, m)
+    value = m['inner_all'] * args.steps / m['dt'] / 1e9
+
+    # ---- strong scaling of config 4: the 1024^3 volume in z-slabs over the ranks -------------
+    strong = None
+    if not args.no_strong and not (args.config == 4 and args.scaling == 'strong'):
+        s = run_workload(4, 'strong', rank, world, dev, args.strong_steps, 1, args.streams)
+        srf = roofline_of(CONFIGS[4], s)
+        strong = {'value': round(s['inner_all'] * s['steps'] / s['dt'] / 1e9, 4), 'unit': 'Gvoxel/s',
+                  'ms_per_step': round(s['dt'] / s['steps'] * 1e3, 3), 'ms_per_step_ranks': s['ms_ranks'],
+                  'steps': s['steps'], 'n_gpus': world, 'scaling': 'strong',
+                  'volume': list(s['full']), 'block_shape': list(CONFIGS[4]['block_shape']),
+                  'halo': list(CONFIGS[4]['halo']), 'blocks_this_rank': s['nblocks'],
+                  'inner_voxels_all_gpus': s['inner_all'], 'global_ids': s['n_ids'],
+                  'pipeline_roofline_frac_per_gpu': round(srf['pipe'] / HBM_PEAK_GBS, 4),
+                  'flood_ms_1stream_rank0': round(sum(s['stage_1'].get(p, 0.0) for p in STAGE_PARTS['flood']), 3),
+                  'offset_scan': 'per step: all-gather of the per-block distinct-id counts (%s) + exclusive scan'
+                                 % (backend or 'single process')}
 
     # ---- end to end: n5 gzip in -> WatershedWorkflow (GPU jobs) + relabel -> n5 out --------
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e and not two_pass:
         progress('end-to-end workflow run')
-        for hh in handles:
-            hh.close()
-        handles = []
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         e2e = end_to_end(args.config, dev, z_extent=args.e2e_z)
 
     # ---- VI of the GPU output vs the oracle on the CPU baseline's first block ---------------
     vi = None
-    if ref_block is not None and ref_block[1] is not None and ref_block[0] in blocks:
+    if ref_block is not None and ref_block[1] is not None and m['kept'] is not None:
         from cluster_tools_amd.metrics import vi_scores, rand_scores
-        gpu_out = blocks[ref_block[0]]['output'].cpu().numpy().view(np.uint64)
+        gpu_out = m['kept']
         ref = ref_block[1]
         vs, vm = vi_scores(gpu_out, ref)
         are, _ = rand_scores(gpu_out, ref)
@@ -600,74 +753,62 @@ def main():
               'bit_exact': bool(np.array_equal(gpu_out, ref)),
               'bar': 'VI <= 0.01, ARand <= 1e-3 (BASELINE.json north_star)'}
 
-    def per_stage(sm):
-        return {k: sum(sm.get(p, 0.0) for p in STAGE_PARTS.get(k, (k,))) for k in stage_bytes(cfg)}
-
-    sbytes = stage_bytes(cfg)
-    stages = per_stage(stage_1)
-    stage_gbs = {}
-    for k, ms in stages.items():
-        b, unit = sbytes[k]
-        nbytes = b * (outer_vox if unit == 'outer' else inner_vox)
-        stage_gbs[k] = round(nbytes / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
-    # roofline of the dominant stage by time (algorithmic bytes / its single-stream HIP-event time)
-    dom = max(stages, key=lambda k: stages[k])
-    dom_ms = stages[dom]
-    b_unit, unit = sbytes[dom]
-    dom_bytes = b_unit * (outer_vox if unit == 'outer' else inner_vox)
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    alg_total = alg_bytes(cfg, outer_vox, inner_vox, pass2_outer)
-    pipe = alg_total / (ms_per_step * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(HERE, 'profiles', 'pmc_traffic_c%d.json' % args.config)
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get(dom)
+            traffic = json.load(f).get(rf['dom'])
 
     if rank == 0:
         line = {
             'metric': 'Gvoxel/s DT-watershed (node, 1/2/4/8 GPU) + % HBM roofline; VI vs ref',
             'value': round(value, 4), 'unit': 'Gvoxel/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 3), 'higher_is_better': True,
+            'warmup': args.warmup, 'ms_per_step': round(rf['ms_per_step'], 3), 'higher_is_better': True,
             'scaling': args.scaling, 'vs_baseline': None, 'dtype': cfg.get('dtype', 'float32').replace('float', 'f'),
             'data': 'synthetic',
-            'config': {'workload': cfg['workload'], 'volume': list(shape), 'full_volume': list(full),
+            'config': {'workload': cfg['workload'], 'volume': list(cfg['shape']), 'full_volume': list(m['full']),
                        'block_shape': list(cfg['block_shape']),
-                       'halo': list(cfg['halo']), 'blocks_per_gpu': nblocks, 'passes': len(passes),
-                       'inner_voxels_per_gpu': inner_vox, 'outer_voxels_per_gpu': outer_vox,
-                       'streams_per_gpu': nstreams,
+                       'halo': list(cfg['halo']), 'blocks_per_gpu': m['nblocks'], 'passes': m['npass'],
+                       'inner_voxels_per_gpu': m['inner_vox'], 'outer_voxels_per_gpu': m['outer_vox'],
+                       'streams_per_gpu': m['nstreams'],
                        'parallelism': 'z-slabs of the block grid, one process per GPU, %d GPU(s), %s scaling'
                                       % (world, args.scaling),
-                       'inner_voxels_all_gpus': inner_all,
-                       'pass2_order': ('relaxed: every pass-2 block reads ds_out[input_bb] before any pass-2 '
-                                       'write (the reference with n_jobs >= n_blocks); the workflow serialises '
-                                       'overlapping halo corners (watershed.make_batches)') if two_pass else None},
-            'roofline': {'bound': 'hbm', 'kernel': '%s (%s)' % (dom, STAGE_KERNELS[dom]),
-                         'ms_per_step': round(dom_ms, 3), 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                         'alg_bytes': dom_bytes, 'alg_bytes_per_voxel': b_unit, 'voxels': unit,
+                       'inner_voxels_all_gpus': m['inner_all'],
+                       'devices': len(devices), 'dist_backend': backend,
+                       'pass2_order': ('dependency levels of the sequential loop (watershed.pass2_levels, as '
+                                       'the workflow): %d launch groups' % (m['ngroups'] - 1)) if two_pass else None},
+            'ms_per_step_ranks': m['ms_ranks'],
+            'roofline': {'bound': 'hbm', 'kernel': '%s (%s)' % (rf['dom'], STAGE_KERNELS[rf['dom']]),
+                         'ms_per_step': round(rf['dom_ms'], 3), 'achieved': round(rf['achieved'], 1),
+                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': round(rf['achieved'] / HBM_PEAK_GBS, 4),
+                         'traffic': traffic, 'alg_bytes': rf['dom_bytes'], 'alg_bytes_per_voxel': rf['b_unit'],
+                         'voxels': rf['unit'],
                          'timing': 'HIP events on the library stream, one untimed step with all blocks on 1 stream',
                          'traffic_unit': 'HBM bytes per step of the stage (profiles/pmc_traffic_c%d.json)'
                                          % args.config},
-            'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(alg_total / inner_vox, 1),
-                                  'achieved': round(pipe, 1), 'unit': 'GB/s',
-                                  'frac': round(pipe / HBM_PEAK_GBS, 4)},
-            'host_resident': host,
+            'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(rf['alg_total'] / m['inner_vox'], 1),
+                                  'achieved': round(rf['pipe'], 1), 'unit': 'GB/s',
+                                  'frac': round(rf['pipe'] / HBM_PEAK_GBS, 4)},
+            'strong_config4': strong,
+            'host_resident': m['host'],
             'end_to_end': e2e,
             'vi_vs_oracle': vi,
-            'stage_ms': {k: round(v, 3) for k, v in stage_ms.items()},
-            'stage_ms_1stream': {k: round(v, 3) for k, v in stage_1.items()},
-            'stage_gbs': stage_gbs,
-            'global_ids': offsets.get('n_ids'),
+            'stage_ms': {k: round(v, 3) for k, v in m['stage_ms'].items()},
+            'stage_ms_1stream': {k: round(v, 3) for k, v in m['stage_1'].items()},
+            'stage_gbs': rf['stage_gbs'],
+            'global_ids': m['n_ids'],
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
-    for hh in handles:
-        hh.close()
-    if pool:
-        pool.shutdown()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def sharded_gather_devices(dev_index, dev):
+    """The device index of every rank (to report how many distinct GPUs the ranks used)."""
+    from cluster_tools_amd.watershed import sharded
+    return sharded.all_gather_float(dev_index, device=dev)
 
 
 if __name__ == '__main__':

@@ -20,7 +20,8 @@ without communication.  There are exactly two exchanges:
 
 Single-process use needs no process group: the functions fall back to local computation.
 With a process group (any world size, including 1) the exchanges go through it -- RCCL
-(backend "nccl") on MI355X, gloo on CPU.
+(backend "nccl") on MI355X, gloo on CPU.  A gloo group also serves GPU tensors (ranks that
+share a device, e.g. a 2-rank rehearsal on one GPU): they are staged through host memory.
 """
 import numpy as np
 
@@ -28,6 +29,47 @@ import numpy as np
 def _dist():
     import torch.distributed as dist
     return dist if (dist.is_available() and dist.is_initialized()) else None
+
+
+def comm_device(device=None):
+    """The device the group's collectives take tensors on: `device` for RCCL, the host for gloo."""
+    dist = _dist()
+    if dist is not None and dist.get_backend() == 'gloo':
+        return None
+    return device
+
+
+def all_reduce_max(value, device=None):
+    """Max of a float over the ranks (the bench's max-over-ranks step time)."""
+    import torch
+    dist = _dist()
+    if dist is None:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=comm_device(device))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_gather_float(value, device=None):
+    """Every rank's value, in rank order."""
+    import torch
+    dist = _dist()
+    if dist is None:
+        return [float(value)]
+    t = torch.tensor([float(value)], dtype=torch.float64, device=comm_device(device))
+    parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [float(p.item()) for p in parts]
+
+
+def all_reduce_sum_int(value, device=None):
+    import torch
+    dist = _dist()
+    if dist is None:
+        return int(value)
+    t = torch.tensor([int(value)], dtype=torch.int64, device=comm_device(device))
+    dist.all_reduce(t)
+    return int(t.item())
 
 
 def shard_range(n_items, rank, world):
@@ -46,6 +88,7 @@ def gather_counts(local_counts, device=None):
     blocks).  Returns one int64 numpy array in rank order, i.e. global block order."""
     import torch
     dist = _dist()
+    device = comm_device(device)
     local = torch.as_tensor(np.asarray(local_counts, dtype=np.int64), device=device)
     if dist is None:
         return local.cpu().numpy()
@@ -94,14 +137,22 @@ def exchange_z_halos(vol, lo, hi):
         return vol
     rank, world = dist.get_rank(), dist.get_world_size()
     Z = vol.shape[0] - lo - hi
+    host = comm_device(vol.device) is None and vol.device.type != 'cpu'  # gloo: through the host
+
+    def out(t):
+        return t.cpu() if host else t.contiguous()
+
+    def buf(n):
+        shape = (n,) + tuple(vol.shape[1:])
+        return vol.new_empty(shape, device='cpu') if host else vol.new_empty(shape)
     ops, recv_lo, recv_hi = [], None, None
     if rank > 0 and lo:
-        ops.append(dist.P2POp(dist.isend, vol[lo:2 * lo].contiguous(), rank - 1))
-        recv_lo = vol.new_empty((lo,) + tuple(vol.shape[1:]))
+        ops.append(dist.P2POp(dist.isend, out(vol[lo:2 * lo]), rank - 1))
+        recv_lo = buf(lo)
         ops.append(dist.P2POp(dist.irecv, recv_lo, rank - 1))
     if rank + 1 < world and hi:
-        ops.append(dist.P2POp(dist.isend, vol[lo + Z - hi:lo + Z].contiguous(), rank + 1))
-        recv_hi = vol.new_empty((hi,) + tuple(vol.shape[1:]))
+        ops.append(dist.P2POp(dist.isend, out(vol[lo + Z - hi:lo + Z]), rank + 1))
+        recv_hi = buf(hi)
         ops.append(dist.P2POp(dist.irecv, recv_hi, rank + 1))
     if ops:
         for r in dist.batch_isend_irecv(ops):

@@ -145,42 +145,54 @@ def _overlaps(a, b):
     return all(sa.start < sb.stop and sb.start < sa.stop for sa, sb in zip(a, b))
 
 
+def pass2_levels(bbs):
+    """Dependency levels of pass-2 blocks in list order: a sequential-equivalent schedule.
+
+    `bbs` = [(input_bb, output_bb)] in block-list order.  In the reference's sequential loop
+    (two_pass_watershed.py:296-299) block y reads ds_out[input_bb] after every earlier block
+    wrote and before every later one writes; same-colour checkerboard blocks interact only where
+    a diagonal neighbour's inner block lies in the other's halo.  level(y) = 1 + max level of
+    the earlier blocks that overlap y (either way round), 0 without one.  Blocks of one level
+    never overlap; running the levels in order, each level's blocks reading before any of them
+    writes, gives every block exactly the ds_out the sequential loop gives it."""
+    levels = []
+    for j, (in_j, out_j) in enumerate(bbs):
+        lv = 0
+        for i in range(j):
+            in_i, out_i = bbs[i]
+            if levels[i] + 1 > lv and (_overlaps(in_j, out_i) or _overlaps(in_i, out_j)):
+                lv = levels[i] + 1
+        levels.append(lv)
+    return levels
+
+
 def make_batches(blocking, block_list, config, pass_id, batch_blocks):
     """Split the job's block list (in order) into GPU batches.
 
     Pass 0 reads only ds_in, so any split works.  Pass 1 (`_ws_pass2`) reads ds_out[input_bb]:
-    in the reference's sequential loop (two_pass_watershed.py:296-299) a block sees the writes
-    of the blocks before it, and in the checkerboard a block's halo corners can overlap the
-    inner block of a diagonal neighbour of the same colour.  A batch reads all its blocks
-    before any of them is written, so a block starts a new batch when its input bb overlaps
-    the output bb of a block already in the current batch.
+    the batches follow pass2_levels (every batch holds blocks of one level, levels in order),
+    the schedule that reproduces the reference's sequential loop.
     """
-    batches, cur, cur_out = [], [], []
-    for bid in block_list:
-        if pass_id == 1:
-            input_bb, _, _ = _get_bbs(blocking, bid, config)
-            if any(_overlaps(input_bb, ob) for ob in cur_out):
-                batches.append(cur)
-                cur, cur_out = [], []
-        if len(cur) >= batch_blocks:
-            batches.append(cur)
-            cur, cur_out = [], []
-        cur.append(bid)
-        if pass_id == 1:
-            cur_out.append(_get_bbs(blocking, bid, config)[2])
-    if cur:
-        batches.append(cur)
-    return batches
+    if pass_id == 1:
+        levels = pass2_levels([_get_bbs(blocking, bid, config)[0::2] for bid in block_list])
+        batches = []
+        for lv in range(max(levels) + 1 if levels else 0):
+            ids = [bid for bid, l in zip(block_list, levels) if l == lv]
+            batches += [ids[k:k + batch_blocks] for k in range(0, len(ids), batch_blocks)]
+        return batches
+    return [list(block_list[k:k + batch_blocks]) for k in range(0, len(block_list), batch_blocks)]
 
 
 def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, batch_blocks=None):
     """Run `_ws_block` (pass 0) or `_ws_pass2` (pass 1) for `block_list` on the GPU.
 
-    Blocks are processed in batches with the same observable behaviour as the reference's
-    sequential loop: outputs are written and "processed block" is logged in block-list order;
-    a block the kernels cannot finish (status CTWS_BLOCK_FAILED, e.g. the reference's own
-    takeDict failure) raises after the blocks before it are written, as the reference job
-    would raise at that block.
+    Blocks are processed in batches with the same results as the reference's sequential loop:
+    pass 0 in block-list order; pass 1 by the dependency levels of pass2_levels, which give
+    every block the ds_out it reads in the sequential loop.  Outputs are written and "processed
+    block" is logged batch by batch; a block the kernels cannot finish (status
+    CTWS_BLOCK_FAILED, e.g. the reference's own takeDict failure) raises after the batches
+    before it are written, as the reference job raises at that block (pass 1: blocks of earlier
+    levels may lie after it in the list).
     """
     from cluster_tools_amd import ctws
     block_shape = list(config['block_shape'])
