@@ -162,6 +162,8 @@ struct ctws_handle {
     int frontier_dir = 1;    // CTWS_FRONTIER_DIR: local sweeps queue only the neighbours a change may lower
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
+    bool cur_plat_fill = false;  // run_batch: the masked plateau of the current flood is held back
+    int tile_first = 0;  // CTWS_TILE_FIRST=1: one tile-flood round on the open tiles before the frontier
     std::vector<BlockDesc> last_desc;
     // pass 2 (2-D): per block of the next run_batch, the slice offsets of its previous run (empty:
     // none); a block with a wrapped-id merge runs again until its offsets are self-consistent
@@ -590,10 +592,10 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
         hipEventRecord(h->fev[0], h->stream);
         if (packed && nd == 3)
             k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.cls, cur, nxt, lcur, lnxt,
-                                                        w.counter);
+                                                        w.counter, nullptr);
         else if (packed)
             k_flood_packed<2><<<g, 128, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.cls, cur, nxt, lcur, lnxt,
-                                                        w.counter);
+                                                        w.counter, nullptr);
         else if (nd == 3)
             k_flood<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         else
@@ -638,6 +640,35 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
                  uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
     Workspace& w = h->ws;
     const int64_t nch = (TF >> kChunkShift) + 1;
+    // (not while a masked plateau is out of the open set: the tile flood relaxes every voxel that
+    // is not fixed, the plateau fill expects its voxels untouched)
+    if (h->tile_first && packed && !h->cur_plat_fill) {
+        // one round of the tile flood (k_flood_packed) on every tile holding an open voxel: each
+        // tile relaxes to its local fixpoint with line sweeps in registers (a front crosses a
+        // tile in one sweep), its changed voxels become the frontier's first changed set
+        int TZ, TY, TX;
+        flood_tile_dims(pl.nd_ws, true, &TZ, &TY, &TX);
+        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+        HIPCHK(hipMemsetAsync(w.act1, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
+        HIPCHK(hipMemsetAsync(w.lines0, 0, sizeof(uint32_t) * kLineWords * (size_t)TT, h->stream));
+        HIPCHK(hipMemsetAsync(w.lines1, 0, sizeof(uint32_t) * kLineWords * (size_t)TT, h->stream));
+        HIPCHK(hipMemsetAsync(w.counter, 0, kCounterBytes, h->stream));
+        k_frontier_tiles<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0,
+                           h->stream>>>(w.desc, w.stat, w.fopen, w.act0, TZ, TY, TX);
+        HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+        const dim3 g((unsigned)max_tiles, nb);
+        if (pl.nd_ws == 3)
+            k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.cls, w.act0, w.act1, w.lines0,
+                                                        w.lines1, w.counter, w.front0);
+        else
+            k_flood_packed<2><<<g, 128, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.cls, w.act0, w.act1, w.lines0,
+                                                        w.lines1, w.counter, w.front0);
+        LAUNCHCHK();
+        if (h->trace) {
+            HIPCHK(hipStreamSynchronize(h->stream));
+            std::fprintf(stderr, "[ctws] tile round before the frontier done\n");
+        }
+    }
     uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
     uint32_t* gen[2] = {w.fchunk0, w.fchunk1};  // iteration it writes gen[it & 1], reads gen[(it + 1) & 1]
     uint32_t* wl[2] = {w.wl0, w.wl1};
@@ -1314,6 +1345,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         bool any_mask = false;
         for (int i = 0; i < nb; ++i) any_mask |= desc[i].mask != nullptr;
         const bool plat_fill = h->plateau_fill && packed && any_mask;
+        h->cur_plat_fill = plat_fill;
         if (plat_fill) HIPCHK(hipMemsetAsync(w.plev, 0, sizeof(uint32_t) * (size_t)nb, h->stream));
         k_descent_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
                                                   w.front0, fst, plat_fill ? w.plev : nullptr);
@@ -1343,6 +1375,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
                 return r;
         }
+        h->cur_plat_fill = false;
         mark("flood_relax");
         if (fst) {
             std::vector<uint32_t> hs(2 * (size_t)nb);
@@ -2212,6 +2245,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_TILE_FIRST")) h->tile_first = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))
         h->frontier_max_iters = std::max(0, std::min(kFrontierMaxItersCap, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_GAUSS_YX")) h->gauss_yx = std::atoi(t);

@@ -147,7 +147,7 @@ __global__ void k_flood(const BlockDesc*, const BlockStat*, const float*, uint64
 
 template <int ND>
 __global__ void k_flood_packed(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint8_t*,
-                               const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
+                               const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint64_t*);
 constexpr int kLineWords = 24;
 constexpr int kStatSlots = 64;  // flood statistics: counter[4 + slot * 4 + k]  // per tile: 8 words of line bits for each of x, y, z
 __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);

@@ -250,7 +250,8 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
                                                                         uint32_t* __restrict__ act_next,
                                                                         uint32_t* __restrict__ lines_cur,
                                                                         uint32_t* __restrict__ lines_next,
-                                                                        uint32_t* __restrict__ counter) {
+                                                                        uint32_t* __restrict__ counter,
+                                                                        uint64_t* __restrict__ chg) {
     using T = PTile<ND>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, NT = T::THREADS;
     constexpr int HZ = T::HZ, HY = T::HY, HX = T::HX;
@@ -455,9 +456,26 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
         __syncthreads();
     }
 
-    // write back changed voxels; collect the lines of the face neighbours whose halo changed
+    // write back changed voxels; collect the lines of the face neighbours whose halo changed.
+    // chg (the frontier's changed bitmap, one bit per voxel, rows of 64-bit words): the changed
+    // voxels, one atomic per tile row segment (a wave covers 64 / TX rows of TX voxels)
+    static_assert(64 % TX == 0 && TN % NT == 0, "");
     for (int c = tid; c < TN; c += NT) {
-        if (!(sf[c] & 2)) continue;
+        const bool changed = (sf[c] & 2) != 0;
+        if (chg) {
+            const uint64_t bits = __ballot(changed);
+            const int lane = tid & 63;
+            if (lane % TX == 0) {
+                const uint64_t seg = (bits >> lane) & ((TX == 64) ? ~0ull : ((1ull << TX) - 1ull));
+                if (seg) {
+                    const int ly = (c / TX) % TY, lz = c / (TX * TY);
+                    const int64_t row = (int64_t)(z0 + lz) * B.Y + (y0 + ly);
+                    atomicOr((unsigned long long*)&chg[B.fbase + row * ((B.X + 63) >> 6) + (x0 >> 6)],
+                             (unsigned long long)(seg << (x0 & 63)));
+                }
+            }
+        }
+        if (!changed) continue;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
         key[gb + gz * YX + (int64_t)gy * B.X + gx] = sk[((lz + ZOFF) * HY + (ly + 1)) * HX + (lx + 1)];
@@ -498,10 +516,10 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
 
 template __global__ void k_flood_packed<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
                                            const uint8_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
-                                           uint32_t*);
+                                           uint32_t*, uint64_t*);
 template __global__ void k_flood_packed<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
                                            const uint8_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
-                                           uint32_t*);
+                                           uint32_t*, uint64_t*);
 
 
 // packed keys -> labels (keeps the seed bit of `lab`)
