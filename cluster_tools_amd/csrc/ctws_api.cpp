@@ -163,6 +163,9 @@ struct ctws_handle {
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
     bool cur_plat_fill = false;  // run_batch: the masked plateau of the current flood is held back
+    int frontier_lds = 1;  // CTWS_FRONTIER_LDS: iteration 0 by k_frontier_lds for the flood (1), also the regrow (2), never (0)
+    int frontier_lds_grid = 768;  // CTWS_FRONTIER_LDS_GRID: workgroups (one wave, ~53 KB of LDS each: 3 per CU)
+    int frontier_lds_reps = 64;   // CTWS_FRONTIER_LDS_REPS: local sweeps of a chunk in iteration 0
     int tile_first = 0;  // CTWS_TILE_FIRST=1: one tile-flood round on the open tiles before the frontier
     std::vector<BlockDesc> last_desc;
     // pass 2 (2-D): per block of the next run_batch, the slice offsets of its previous run (empty:
@@ -637,7 +640,7 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 // it has not converged after frontier_max_iters iterations (very long equal-height paths) the
 // tile flood finishes from the current keys.
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
-                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
+                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out, bool regrow = false) {
     Workspace& w = h->ws;
     const int64_t nch = (TF >> kChunkShift) + 1;
     // (not while a masked plateau is out of the open set: the tile flood relaxes every voxel that
@@ -714,8 +717,15 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             h->frontier_reps, h->frontier_dir);                                                                     \
         break;
-            switch (fkind) {
-                CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
+            if (it == 0 && h->frontier_lds >= (regrow ? 2 : 1) && fkind == 0) {
+                // iteration 0: the chunk resident in LDS (one wave per workgroup)
+                k_frontier_lds<2, 64, 1><<<(unsigned)h->frontier_lds_grid, 64, 0, h->stream>>>(
+                    w.desc, w.stat, w.hm, w.key, w.fopen, fb[0], fb[1], gen[1], gen[0], 0, wl[0], w.wlcnt,
+                    wl[1], w.wlcnt + 1, w.qgen, fst ? fst + nb : nullptr, h->frontier_lds_reps);
+            } else {
+                switch (fkind) {
+                    CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
+                }
             }
 #undef CTWS_FRONTIER
             if (h->trace) hipEventRecord(tev[k + 1], h->stream);
@@ -1492,7 +1502,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                                                            w.cls, w.fopen, w.front0);
                 LAUNCHCHK();
             }
-            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2)) !=
+            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2, true)) !=
                 CTWS_OK)
                 return r;
             if (h->verify) {
@@ -2246,6 +2256,9 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_TILE_FIRST")) h->tile_first = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FRONTIER_LDS")) h->frontier_lds = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FRONTIER_LDS_GRID")) h->frontier_lds_grid = std::max(8, std::atoi(t));
+    if (const char* t = std::getenv("CTWS_FRONTIER_LDS_REPS")) h->frontier_lds_reps = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))
         h->frontier_max_iters = std::max(0, std::min(kFrontierMaxItersCap, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_GAUSS_YX")) h->gauss_yx = std::atoi(t);

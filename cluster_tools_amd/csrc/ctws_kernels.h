@@ -184,6 +184,10 @@ hipError_t fs_segmented_sort(void* tmp, size_t& bytes, const uint32_t* in, uint3
 // per-chunk arrays (generations, queued marks) are indexed at fbase >> kChunkShift: a block's
 // frontier words hold at least 2^kChunkShift words per chunk (every brick is 64 words)
 constexpr int kChunkShift = 6;
+template <int ND, int CY, int CZ>
+__global__ void k_frontier_lds(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
+                               const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
+                               const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 template <int CW, int CY, int CZ>
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);
