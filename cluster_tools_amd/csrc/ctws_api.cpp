@@ -158,15 +158,13 @@ struct ctws_handle {
     int fchunk3_env = 0;  // CTWS_FRONTIER_CHUNK3D given: used for every 3-D batch
     int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
     int cur_max[3] = {0, 0, 0};  // largest outer block extents (Z, Y, X) of the current batch
-    int frontier_grid = 2048;  // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4)
+    // CTWS_FRONTIER_GRID: workgroups of k_frontier (chunks in flight / 4).  1024 rather than 2048:
+    // half the chunks in flight keep more of each chunk's lines in L2 between its local sweeps
+    // (r04: config 3 relaxation 20.3 -> 18.5 ms per step; 512: 23.0 ms, too few waves)
+    int frontier_grid = 1024;
     int frontier_dir = 1;    // CTWS_FRONTIER_DIR: local sweeps queue only the neighbours a change may lower
     int frontier_reps = 32;  // CTWS_FRONTIER_REPS: local sweeps per chunk and launch (r02 sweep: 4 -> 32 cut k_frontier 19%)
     int frontier_max_iters = kFrontierMaxIters;  // CTWS_FRONTIER_ITERS: then the tile flood finishes
-    bool cur_plat_fill = false;  // run_batch: the masked plateau of the current flood is held back
-    int frontier_lds = 1;  // CTWS_FRONTIER_LDS: iteration 0 by k_frontier_lds for the flood (1), also the regrow (2), never (0)
-    int frontier_lds_grid = 768;  // CTWS_FRONTIER_LDS_GRID: workgroups (one wave, ~53 KB of LDS each: 3 per CU)
-    int frontier_lds_reps = 64;   // CTWS_FRONTIER_LDS_REPS: local sweeps of a chunk in iteration 0
-    int tile_first = 0;  // CTWS_TILE_FIRST=1: one tile-flood round on the open tiles before the frontier
     std::vector<BlockDesc> last_desc;
     // pass 2 (2-D): per block of the next run_batch, the slice offsets of its previous run (empty:
     // none); a block with a wrapped-id merge runs again until its offsets are self-consistent
@@ -595,10 +593,10 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
         hipEventRecord(h->fev[0], h->stream);
         if (packed && nd == 3)
             k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.cls, cur, nxt, lcur, lnxt,
-                                                        w.counter, nullptr);
+                                                        w.counter);
         else if (packed)
             k_flood_packed<2><<<g, 128, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.cls, cur, nxt, lcur, lnxt,
-                                                        w.counter, nullptr);
+                                                        w.counter);
         else if (nd == 3)
             k_flood<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, hm, w.key, w.lab, cur, nxt, w.counter);
         else
@@ -640,38 +638,9 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 // it has not converged after frontier_max_iters iterations (very long equal-height paths) the
 // tile flood finishes from the current keys.
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
-                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out, bool regrow = false) {
+                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
     Workspace& w = h->ws;
     const int64_t nch = (TF >> kChunkShift) + 1;
-    // (not while a masked plateau is out of the open set: the tile flood relaxes every voxel that
-    // is not fixed, the plateau fill expects its voxels untouched)
-    if (h->tile_first && packed && !h->cur_plat_fill) {
-        // one round of the tile flood (k_flood_packed) on every tile holding an open voxel: each
-        // tile relaxes to its local fixpoint with line sweeps in registers (a front crosses a
-        // tile in one sweep), its changed voxels become the frontier's first changed set
-        int TZ, TY, TX;
-        flood_tile_dims(pl.nd_ws, true, &TZ, &TY, &TX);
-        HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-        HIPCHK(hipMemsetAsync(w.act1, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
-        HIPCHK(hipMemsetAsync(w.lines0, 0, sizeof(uint32_t) * kLineWords * (size_t)TT, h->stream));
-        HIPCHK(hipMemsetAsync(w.lines1, 0, sizeof(uint32_t) * kLineWords * (size_t)TT, h->stream));
-        HIPCHK(hipMemsetAsync(w.counter, 0, kCounterBytes, h->stream));
-        k_frontier_tiles<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0,
-                           h->stream>>>(w.desc, w.stat, w.fopen, w.act0, TZ, TY, TX);
-        HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-        const dim3 g((unsigned)max_tiles, nb);
-        if (pl.nd_ws == 3)
-            k_flood_packed<3><<<g, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.cls, w.act0, w.act1, w.lines0,
-                                                        w.lines1, w.counter, w.front0);
-        else
-            k_flood_packed<2><<<g, 128, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.cls, w.act0, w.act1, w.lines0,
-                                                        w.lines1, w.counter, w.front0);
-        LAUNCHCHK();
-        if (h->trace) {
-            HIPCHK(hipStreamSynchronize(h->stream));
-            std::fprintf(stderr, "[ctws] tile round before the frontier done\n");
-        }
-    }
     uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
     uint32_t* gen[2] = {w.fchunk0, w.fchunk1};  // iteration it writes gen[it & 1], reads gen[(it + 1) & 1]
     uint32_t* wl[2] = {w.wl0, w.wl1};
@@ -717,15 +686,8 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             h->frontier_reps, h->frontier_dir);                                                                     \
         break;
-            if (it == 0 && h->frontier_lds >= (regrow ? 2 : 1) && fkind == 0) {
-                // iteration 0: the chunk resident in LDS (one wave per workgroup)
-                k_frontier_lds<2, 64, 1><<<(unsigned)h->frontier_lds_grid, 64, 0, h->stream>>>(
-                    w.desc, w.stat, w.hm, w.key, w.fopen, fb[0], fb[1], gen[1], gen[0], 0, wl[0], w.wlcnt,
-                    wl[1], w.wlcnt + 1, w.qgen, fst ? fst + nb : nullptr, h->frontier_lds_reps);
-            } else {
-                switch (fkind) {
-                    CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
-                }
+            switch (fkind) {
+                CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
             }
 #undef CTWS_FRONTIER
             if (h->trace) hipEventRecord(tev[k + 1], h->stream);
@@ -1355,7 +1317,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         bool any_mask = false;
         for (int i = 0; i < nb; ++i) any_mask |= desc[i].mask != nullptr;
         const bool plat_fill = h->plateau_fill && packed && any_mask;
-        h->cur_plat_fill = plat_fill;
         if (plat_fill) HIPCHK(hipMemsetAsync(w.plev, 0, sizeof(uint32_t) * (size_t)nb, h->stream));
         k_descent_init<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
                                                   w.front0, fst, plat_fill ? w.plev : nullptr);
@@ -1385,7 +1346,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &fiters, &rounds1, &fk1)) != CTWS_OK)
                 return r;
         }
-        h->cur_plat_fill = false;
         mark("flood_relax");
         if (fst) {
             std::vector<uint32_t> hs(2 * (size_t)nb);
@@ -1502,7 +1462,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                                                            w.cls, w.fopen, w.front0);
                 LAUNCHCHK();
             }
-            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2, true)) !=
+            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2)) !=
                 CTWS_OK)
                 return r;
             if (h->verify) {
@@ -2255,10 +2215,6 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
-    if (const char* t = std::getenv("CTWS_TILE_FIRST")) h->tile_first = std::atoi(t);
-    if (const char* t = std::getenv("CTWS_FRONTIER_LDS")) h->frontier_lds = std::atoi(t);
-    if (const char* t = std::getenv("CTWS_FRONTIER_LDS_GRID")) h->frontier_lds_grid = std::max(8, std::atoi(t));
-    if (const char* t = std::getenv("CTWS_FRONTIER_LDS_REPS")) h->frontier_lds_reps = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))
         h->frontier_max_iters = std::max(0, std::min(kFrontierMaxItersCap, std::atoi(t)));
     if (const char* t = std::getenv("CTWS_GAUSS_YX")) h->gauss_yx = std::atoi(t);

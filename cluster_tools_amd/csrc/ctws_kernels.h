@@ -147,7 +147,7 @@ __global__ void k_flood(const BlockDesc*, const BlockStat*, const float*, uint64
 
 template <int ND>
 __global__ void k_flood_packed(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint8_t*,
-                               const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint64_t*);
+                               const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 constexpr int kLineWords = 24;
 constexpr int kStatSlots = 64;  // flood statistics: counter[4 + slot * 4 + k]  // per tile: 8 words of line bits for each of x, y, z
 __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
@@ -184,10 +184,6 @@ hipError_t fs_segmented_sort(void* tmp, size_t& bytes, const uint32_t* in, uint3
 // per-chunk arrays (generations, queued marks) are indexed at fbase >> kChunkShift: a block's
 // frontier words hold at least 2^kChunkShift words per chunk (every brick is 64 words)
 constexpr int kChunkShift = 6;
-template <int ND, int CY, int CZ>
-__global__ void k_frontier_lds(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
-                               const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
-                               const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int);
 template <int CW, int CY, int CZ>
 __global__ void k_frontier_list0(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, uint32_t*);
 __global__ void k_frontier_tiles(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*, int, int, int);

@@ -250,8 +250,7 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
                                                                         uint32_t* __restrict__ act_next,
                                                                         uint32_t* __restrict__ lines_cur,
                                                                         uint32_t* __restrict__ lines_next,
-                                                                        uint32_t* __restrict__ counter,
-                                                                        uint64_t* __restrict__ chg) {
+                                                                        uint32_t* __restrict__ counter) {
     using T = PTile<ND>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, NT = T::THREADS;
     constexpr int HZ = T::HZ, HY = T::HY, HX = T::HX;
@@ -456,26 +455,9 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
         __syncthreads();
     }
 
-    // write back changed voxels; collect the lines of the face neighbours whose halo changed.
-    // chg (the frontier's changed bitmap, one bit per voxel, rows of 64-bit words): the changed
-    // voxels, one atomic per tile row segment (a wave covers 64 / TX rows of TX voxels)
-    static_assert(64 % TX == 0 && TN % NT == 0, "");
+    // write back changed voxels; collect the lines of the face neighbours whose halo changed
     for (int c = tid; c < TN; c += NT) {
-        const bool changed = (sf[c] & 2) != 0;
-        if (chg) {
-            const uint64_t bits = __ballot(changed);
-            const int lane = tid & 63;
-            if (lane % TX == 0) {
-                const uint64_t seg = (bits >> lane) & ((TX == 64) ? ~0ull : ((1ull << TX) - 1ull));
-                if (seg) {
-                    const int ly = (c / TX) % TY, lz = c / (TX * TY);
-                    const int64_t row = (int64_t)(z0 + lz) * B.Y + (y0 + ly);
-                    atomicOr((unsigned long long*)&chg[B.fbase + row * ((B.X + 63) >> 6) + (x0 >> 6)],
-                             (unsigned long long)(seg << (x0 & 63)));
-                }
-            }
-        }
-        if (!changed) continue;
+        if (!(sf[c] & 2)) continue;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
         key[gb + gz * YX + (int64_t)gy * B.X + gx] = sk[((lz + ZOFF) * HY + (ly + 1)) * HX + (lx + 1)];
@@ -516,10 +498,10 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
 
 template __global__ void k_flood_packed<3>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
                                            const uint8_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
-                                           uint32_t*, uint64_t*);
+                                           uint32_t*);
 template __global__ void k_flood_packed<2>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
                                            const uint8_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t*,
-                                           uint32_t*, uint64_t*);
+                                           uint32_t*);
 
 
 // packed keys -> labels (keeps the seed bit of `lab`)
@@ -1197,264 +1179,6 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
     }
 }
-// Iteration 0 of the frontier relaxation with the chunk resident in LDS (k_frontier_lds).
-//
-// Iteration 0 starts from the descent: every chunk holding an open voxel is listed and its
-// front must cross the chunk's open regions (a CPU replay of config 3 slices: 18 local Jacobi
-// sweeps per 64 x 64 chunk on average, 31 at most).  k_frontier pays a round trip to global
-// memory for every sweep (neighbour keys and heights gathered per visit); here one wave stages
-// the chunk's keys with a one-voxel halo and its heights in LDS with all loads in flight at
-// once, runs the same sweeps (frontier bits -> entry list -> relax -> changed bits -> the
-// in-chunk neighbours of the changes) on LDS until the chunk converges or `reps` sweeps are
-// done, and writes back the changed keys.  Halo keys are a snapshot, as k_frontier's stale
-// reads: a neighbour chunk's later change on the shared face queues this chunk again through
-// the changed bitmaps and generations (identical bookkeeping to k_frontier's, which runs the
-// later iterations).  One-word-wide bricks (CW = 1): lane = x for the row loads, lane = word
-// (row) for the bitmaps.  One wave per workgroup, ~53 KB of LDS: 3 chunks per CU.
-template <int ND, int CY, int CZ>
-struct LdsBrick {
-    static constexpr int ZH = ND == 3 ? 1 : 0;
-    static constexpr int HX = 66, HY = CY + 2, HZ = CZ + 2 * ZH;
-    static constexpr int NR = HY * HZ;  // halo rows
-    static constexpr int NK = NR * HX;
-};
-
-template <int ND, int CY, int CZ>
-__global__ void __launch_bounds__(64) k_frontier_lds(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                     const float* __restrict__ h, uint64_t* __restrict__ key,
-                                                     const uint64_t* __restrict__ open, const uint64_t* __restrict__ cprev,
-                                                     uint64_t* __restrict__ cnext, const uint32_t* __restrict__ gprev,
-                                                     uint32_t* __restrict__ gnext, int it, const uint32_t* __restrict__ list,
-                                                     const uint32_t* __restrict__ cnt, uint32_t* __restrict__ list_next,
-                                                     uint32_t* __restrict__ cnt_next, uint32_t* __restrict__ qgen,
-                                                     uint32_t* __restrict__ nvisit, int reps) {
-    static_assert(ND == 3 || CZ == 1, "2-D ws: slices are independent, chunks are one slice deep");
-    static_assert(CY * CZ == 64, "a brick is 64 one-word rows");
-    using LB = LdsBrick<ND, CY, CZ>;
-    constexpr int HX = LB::HX, HY = LB::HY, ZH = LB::ZH, NR = LB::NR;
-    __shared__ uint64_t K[LB::NK];
-    __shared__ uint32_t Hh[64 * 64];  // ordered heights, [word][bit]
-    __shared__ uint64_t schg[64];
-    __shared__ uint64_t sfw[64];
-    __shared__ int spre[64];
-    const int lane = threadIdx.x;
-    const int ly = lane % CY, lz = lane / CY;  // the lane's word (row) of the brick
-    const uint32_t n_entries = *cnt;
-    const uint32_t prev_gen = (uint32_t)it;
-    const uint32_t wg = (uint32_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
-    for (uint32_t e0 = wg; e0 < n_entries; e0 += gridDim.x) {
-        const uint32_t ent = list[e0];
-        const int bi = (int)(ent >> kWlChunkBits);
-        const int ch0 = (int)(ent & ((1u << kWlChunkBits) - 1u));
-        const BlockDesc& B = D[bi];
-        const FChunk<1, CY, CZ> G(B);
-        const int wpr = G.wpr;
-        const int ws = B.Y * wpr;
-        const int cplane = G.ncx * G.ncy;
-        const uint64_t* cp = cprev + B.fbase;
-        const uint64_t* op = open + B.fbase;
-        uint64_t* cn = cnext + B.fbase;
-        const gptr_t<uint64_t> kb = gbl(key + B.base);
-        const gptr_t<float> hb = gbl(h + B.base);
-        const uint32_t* gp = gprev + (B.fbase >> kChunkShift);
-        uint32_t* gn = gnext + (B.fbase >> kChunkShift);
-        uint32_t* qg = qgen + (B.fbase >> kChunkShift);
-        const int cx = (int)(ch0 % G.ncx), cy = (int)((ch0 / G.ncx) % G.ncy), cz = (int)(ch0 / cplane);
-        const int xw = cx, yy = cy * CY + ly, zz = cz * CZ + lz;
-        const bool wok = yy < B.Y && zz < B.Z;
-        const int wc = wok ? (zz * B.Y + yy) * wpr + xw : 0;
-        // ---- the first frontier (as k_frontier): open voxels next to a change of iteration it - 1
-        constexpr int NW = ND == 3 ? 7 : 5;
-        int wi[NW], ci[NW];
-        bool ok[NW];
-        wi[0] = wc;
-        ci[0] = ch0;
-        ok[0] = wok;
-        wi[1] = wc - 1;
-        ci[1] = ch0 - 1;
-        ok[1] = wok && xw > 0;
-        wi[2] = wc + 1;
-        ci[2] = ch0 + 1;
-        ok[2] = wok && xw + 1 < wpr;
-        wi[3] = wc - wpr;
-        ci[3] = ly == 0 ? ch0 - G.ncx : ch0;
-        ok[3] = wok && yy > 0;
-        wi[4] = wc + wpr;
-        ci[4] = ly == CY - 1 ? ch0 + G.ncx : ch0;
-        ok[4] = wok && yy + 1 < B.Y;
-        if (ND == 3) {
-            wi[5] = wc - ws;
-            ci[5] = lz == 0 ? ch0 - cplane : ch0;
-            ok[5] = wok && zz > 0;
-            wi[6] = wc + ws;
-            ci[6] = lz == CZ - 1 ? ch0 + cplane : ch0;
-            ok[6] = wok && zz + 1 < B.Z;
-        }
-        uint32_t gv[NW];
-        uint64_t cv[NW];
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            gv[k] = gbl(gp)[ok[k] ? ci[k] : ch0];
-            cv[k] = gbl(cp)[ok[k] ? wi[k] : wc];
-        }
-        const uint64_t opw = wok ? gbl(op)[wc] : 0ull;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-            const bool own = ci[k] == ch0;
-            const bool valid = own ? gv[k] == prev_gen : (gv[k] & ~kGenConv) == prev_gen;
-            cv[k] = (ok[k] && valid) ? cv[k] : 0ull;
-        }
-        uint64_t f = (cv[0] << 1) | (cv[0] >> 1) | (cv[1] >> 63) | (cv[2] << 63) | cv[3] | cv[4];
-        if (ND == 3) f |= cv[5] | cv[6];
-        f &= opw;
-        if (__ballot(f != 0ull) == 0ull) continue;  // nothing to relax in this chunk
-        // ---- stage keys (halo rows: lane = x + 1, lanes 0 / 1 also the x - 1 / x + 64 ends) and
-        // heights (lane = x), every load in flight at once
-        const int x0 = xw * 64;
-        const int zb = cz * CZ - ZH, yb = cy * CY - 1;
-        {
-            uint64_t v[NR], e[NR];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const int z = zb + r / HY, y = yb + r % HY;
-                const bool rok = z >= 0 && z < B.Z && y >= 0 && y < B.Y;
-                const int x = x0 + lane;
-                const int xe = lane == 0 ? x0 - 1 : x0 + 64;
-                const int64_t rowb = ((int64_t)(rok ? z : 0) * B.Y + (rok ? y : 0)) * B.X;
-                v[r] = (rok && x < B.X) ? kb[rowb + x] : kPackInf;
-                e[r] = (rok && lane < 2 && xe >= 0 && xe < B.X) ? kb[rowb + xe] : kPackInf;
-            }
-            float hv[64];
-#pragma unroll
-            for (int j = 0; j < 64; ++j) {
-                const int z = cz * CZ + j / CY, y = cy * CY + j % CY;
-                const int x = x0 + lane;
-                hv[j] = (z < B.Z && y < B.Y && x < B.X) ? hb[((int64_t)z * B.Y + y) * B.X + x] : 0.0f;
-            }
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                K[r * HX + lane + 1] = v[r];
-                if (lane == 0) K[r * HX] = e[r];
-                if (lane == 1) K[r * HX + 65] = e[r];
-            }
-#pragma unroll
-            for (int j = 0; j < 64; ++j) Hh[j * 64 + lane] = ordf(hv[j]);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint64_t acc = 0ull;
-        bool conv = true;
-        uint32_t vis = 0;
-        for (int rep = 0;; ++rep) {
-            const int cnt_bits = __popcll(f);
-            int incl = cnt_bits;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t = __shfl_up(incl, o);
-                if (lane >= o) incl += t;
-            }
-            const int total = __shfl(incl, 63);
-            if (total == 0) break;
-            vis += (uint32_t)total;
-            schg[lane] = 0ull;
-            sfw[lane] = f;
-            spre[lane] = incl - cnt_bits;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int t0 = 0; t0 < total; t0 += 64) {
-                const int e = t0 + lane;
-                if (e < total) {
-                    int j = 0;
-#pragma unroll
-                    for (int step = 32; step > 0; step >>= 1)
-                        if (spre[j + step] <= e) j += step;
-                    const int b = kth_set_bit(sfw[j], e - spre[j]);
-                    const int jy = j % CY, jz = j / CY;
-                    const int c = ((jz + ZH) * HY + (jy + 1)) * HX + b + 1;
-                    uint64_t m = min(min(K[c - 1], K[c + 1]), min(K[c - HX], K[c + HX]));
-                    if (ND == 3) m = min(m, min(K[c - HX * HY], K[c + HX * HY]));
-                    if (m != kPackInf) {
-                        const uint64_t k = f_packed(Hh[j * 64 + b], m);
-                        if (k != K[c]) {
-                            K[c] = k;
-                            atomicOr((unsigned long long*)&schg[j], 1ull << b);
-                        }
-                    }
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint64_t c = schg[lane];
-            acc |= c;
-            if (__ballot(c != 0ull) == 0ull) break;
-            if (rep + 1 >= reps) {
-                conv = false;
-                break;
-            }
-            // the in-chunk neighbours of this sweep's changes (rows: lanes; x: bit shifts)
-            f = (c << 1) | (c >> 1);
-            const uint64_t cym = shfl_u64(c, ly > 0 ? lane - 1 : lane);
-            const uint64_t cyp = shfl_u64(c, ly < CY - 1 ? lane + 1 : lane);
-            if (ly > 0) f |= cym;
-            if (ly < CY - 1 && yy + 1 < B.Y) f |= cyp;
-            if (ND == 3 && CZ > 1) {
-                const uint64_t czm = shfl_u64(c, lz > 0 ? lane - CY : lane);
-                const uint64_t czp = shfl_u64(c, lz < CZ - 1 ? lane + CY : lane);
-                if (lz > 0) f |= czm;
-                if (lz < CZ - 1 && zz + 1 < B.Z) f |= czp;
-            }
-            f &= opw;
-        }
-        if (nvisit && lane == 0 && vis) atomicAdd(&nvisit[bi], vis);
-        if (__ballot(acc != 0ull) == 0ull) continue;
-        // write back the changed keys, one brick row per step (lane = x)
-        for (int j = 0; j < 64; ++j) {
-            const uint64_t a = shfl_u64(acc, j);
-            if (!a) continue;
-            const int jy = j % CY, jz = j / CY;
-            if ((a >> lane) & 1ull) {
-                const int z = cz * CZ + jz, y = cy * CY + jy;
-                key[B.base + ((int64_t)z * B.Y + y) * B.X + x0 + lane] = K[((jz + ZH) * HY + (jy + 1)) * HX + lane + 1];
-            }
-        }
-        // publish the changed words and queue the chunks holding a neighbour of a change (faces),
-        // and itself unless it converged (k_frontier's epilogue)
-        if (wok) cn[wc] = acc;
-        if (lane == 0) gn[ch0] = ((uint32_t)it + 1u) | (conv ? kGenConv : 0u);
-        const bool fxm = __ballot(acc & 1ull) != 0ull;
-        const bool fxp = __ballot(acc >> 63) != 0ull;
-        const bool fym = __ballot(ly == 0 && acc != 0ull) != 0ull;
-        const bool fyp = __ballot(ly == CY - 1 && acc != 0ull) != 0ull;
-        const bool fzm = ND == 3 && __ballot(lz == 0 && acc != 0ull) != 0ull;
-        const bool fzp = ND == 3 && __ballot(lz == CZ - 1 && acc != 0ull) != 0ull;
-        int cand = -1;
-        if (lane == 0 && !conv) cand = ch0;
-        else if (lane == 1 && fxm && cx > 0) cand = ch0 - 1;
-        else if (lane == 2 && fxp && cx + 1 < G.ncx) cand = ch0 + 1;
-        else if (lane == 3 && fym && cy > 0) cand = ch0 - G.ncx;
-        else if (lane == 4 && fyp && cy + 1 < G.ncy) cand = ch0 + G.ncx;
-        else if (lane == 5 && fzm && cz > 0) cand = ch0 - cplane;
-        else if (lane == 6 && fzp && cz + 1 < G.ncz) cand = ch0 + cplane;
-        bool push = false;
-        if (cand >= 0) push = atomicMax(&qg[cand], (uint32_t)it + 1u) < (uint32_t)it + 1u;
-        const uint64_t pm = __ballot(push);
-        uint32_t base = 0;
-        if (lane == 0 && pm) base = atomicAdd(cnt_next, (uint32_t)__popcll(pm));
-        base = (uint32_t)__shfl((int)base, 0);
-        if (push)
-            list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
-        // (the next chunk's staging overwrites K / Hh: every lane is past its reads here)
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-template __global__ void k_frontier_lds<2, 64, 1>(const BlockDesc*, const BlockStat*, const float*, uint64_t*,
-                                                 const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,
-                                                 uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*,
-                                                 uint32_t*, uint32_t*, uint32_t*, int);
-
 // chunk bricks: 2-D ws (CZ = 1) and 3-D; CTWS_FRONTIER_CHUNK selects one (frontier_chunk_dims)
 #define CTWS_FRONTIER_INST(ND, CW, CY, CZ)                                                                           \
     template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \

@@ -25,10 +25,6 @@ VARIANTS = {
     'one_sweep': {'CTWS_FRONTIER_REPS': '1'},
     # masked blocks' plateaus relaxed hop by hop instead of filled by run scans (k_plateau.hip)
     'no_plateau_fill': {'CTWS_PLATEAU_FILL': '0'},
-    # iteration 0 by the gathering k_frontier instead of the LDS-resident k_frontier_lds (2-D)
-    'frontier_lds_off': {'CTWS_FRONTIER_LDS': '0'},
-    # k_frontier_lds for the regrow too, with a 3-sweep limit (non-converged chunks re-queued)
-    'frontier_lds_all_3reps': {'CTWS_FRONTIER_LDS': '2', 'CTWS_FRONTIER_LDS_REPS': '3'},
     # cropped blocks' uint64 output through the word-tiled k_output instead of k_output_crop
     'output_words': {'CTWS_OUTPUT_TILE': '0'},
 }
