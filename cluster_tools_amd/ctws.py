@@ -181,7 +181,7 @@ class Handle:
                 c.initial_seeds = s.ctypes.data
             out = b.get('out')
             if out is None:
-                out = np.zeros(ishape, dtype=np.uint64)
+                out = np.empty(ishape, dtype=np.uint64)  # (every voxel of a written block is set)
             assert out.dtype == np.uint64 and out.flags.c_contiguous and out.shape == ishape
             keep.append(out)
             c.output = out.ctypes.data

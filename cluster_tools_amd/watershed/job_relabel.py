@@ -1,0 +1,156 @@
+"""RelabelWorkflow fused into the watershed jobs: the per-block id-count exchange over a process
+group of the jobs (BASELINE north star: "the per-block max-label exclusive scan
+that assigns global ID offsets").
+
+The reference numbers the watershed ids with three more tasks and two file round trips:
+FindUniques (per-job np.unique, relabel/find_uniques.py:115-159), FindLabeling (np.unique of
+the concatenation, new ids consecutive from 1, 0 kept as 0 if present; find_labeling.py:84-126)
+and Write (every block through the table, attrs['maxId']; write/write.py:153-278).  Watershed
+ids of block b lie in [b * V, (b + 1) * V] (V = prod(block_shape), watershed.py:305-307), so
+the sorted global uniques are the blocks' sorted uniques in block-id order, and the new id of
+the k-th nonzero unique of block b is offsets[b] + 1 + k with offsets the exclusive scan of the
+blocks' nonzero-unique counts (thresholded_components/merge_offsets.py:106-122 does the same
+scan with files).  The one overlap the id ranges allow -- block b - 1's id b * V (a local label
+equal to V) and block b's bare offset b * V -- is detected from the blocks' first / last
+nonzero uniques and counted once, as np.unique would.
+
+Here the local jobs of one watershed task (all started at once by LocalTask) form one process
+group (rank = job id; RCCL when every job owns a GPU, gloo when jobs share one), all-gather one
+row per block (block id, nonzero count, first, last, has zero), scan, and write their blocks
+with the final ids -- the relabelled volume, the (N, 2) assignment table and maxId equal the
+three-task RelabelWorkflow's exactly (tests/test_job_relabel.py, tests/test_workflow_gpu.py).
+The table rows go through files (rank 0 writes the dataset), the scan through the group.
+"""
+import os
+from datetime import timedelta
+
+import numpy as np
+
+
+def block_row(block_id, uniques):
+    """(block id, nonzero count, first nonzero, last nonzero, has 0) of one block's sorted uniques."""
+    u = np.asarray(uniques, dtype=np.uint64)
+    nz = u[u != 0]
+    first = int(nz[0]) if len(nz) else -1
+    last = int(nz[-1]) if len(nz) else -1
+    return [int(block_id), len(nz), first, last, int(len(nz) != len(u))]
+
+
+def scan(rows):
+    """Offsets of every block from the rows of all blocks (any order).
+
+    Returns {block_id: (offset, dup)} and the number of new nonzero ids: block b's k-th nonzero
+    unique gets offset + 1 + k - dup, where dup = 1 when its first unique is the previous
+    block's last one (that id keeps the previous block's new id)."""
+    rows = sorted((tuple(int(v) for v in r) for r in rows), key=lambda r: r[0])
+    out, total, prev_last, prev_id = {}, 0, None, None
+    for bid, cnt, first, last, _ in rows:
+        dup = 1 if (cnt and prev_last is not None and prev_id == bid - 1 and first == prev_last) else 0
+        out[bid] = (total, dup)
+        total += cnt - dup
+        if cnt:
+            prev_last, prev_id = last, bid
+        else:
+            prev_last, prev_id = None, bid
+    return out, total
+
+
+def block_table(uniques, offset, dup):
+    """(keys, values) of one block: its nonzero uniques -> offset + 1 + k - dup."""
+    u = np.asarray(uniques, dtype=np.uint64)
+    nz = u[u != 0]
+    vals = np.arange(offset + 1 - dup, offset + 1 - dup + len(nz), dtype=np.uint64)
+    return nz, vals
+
+
+def rows_file(tmp_folder, job_id):
+    return os.path.join(tmp_folder, 'watershed_relabel_rows_job_%i.npy' % job_id)
+
+
+def _gather_rows(rows, device):
+    """All ranks' rows (k x 5 int64 each, k may differ per rank), concatenated."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    local = torch.as_tensor(np.asarray(rows, dtype=np.int64).reshape(-1, 5), device=device)
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(max(sizes), 1)
+    padded = torch.zeros((m, 5), dtype=torch.int64, device=device)
+    padded[:local.shape[0]] = local
+    parts = [torch.zeros_like(padded) for _ in range(world)]
+    dist.all_gather(parts, padded)
+    return np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)])
+
+
+def init_group(job_id, n_jobs, port, backend, device=None, timeout_s=900):
+    import torch.distributed as dist
+    if backend == 'nccl':
+        import torch
+        torch.cuda.set_device(device)
+        dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=job_id, world_size=n_jobs,
+                                timeout=timedelta(seconds=timeout_s), device_id=torch.device('cuda', device))
+    else:
+        dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=job_id, world_size=n_jobs,
+                                timeout=timedelta(seconds=timeout_s))
+
+
+def relabel_in_job(job_id, results, ds_out, tmp_folder, assignment_path, assignment_key, mapper,
+                   failed=False, log=print, device=None):
+    """The exchange, then the job's blocks written with their final ids.
+
+    results: [(block_id, output_bb, labels or None (skipped: nothing written), uniques)] of this
+    job.  mapper(labels, keys, values) maps a block in place (ctws lookup on the GPU).  A job
+    whose blocks failed still joins (failed=True) so that every job raises instead of waiting."""
+    import torch.distributed as dist
+    from cluster_tools_amd.utils import volume_utils as vu
+    comm_dev = device if dist.get_backend() == 'nccl' else None
+    rows = [block_row(bid, u) for bid, _, lab, u in results if lab is not None]
+    skipped = any(lab is None for _, _, lab, _ in results)
+    status = _gather_rows([[-1, int(failed), 0, 0, int(skipped)]] + rows, comm_dev)
+    flags, rows_all = status[status[:, 0] < 0], status[status[:, 0] >= 0]
+    if flags[:, 1].any():
+        raise RuntimeError("a watershed job of the group failed: no relabelling")
+    offs, n_new = scan(rows_all)
+    has_zero = bool(flags[:, 4].any() or rows_all[:, 4].any())
+    log("global ids: %i (offset scan over %i blocks)" % (n_new, len(rows_all)))
+    keys_all, vals_all = [], []
+    for bid, bb, lab, u in results:
+        if lab is None:
+            continue
+        off, dup = offs[bid]
+        keys, vals = block_table(u, off, dup)
+        if len(keys):
+            mapper(lab, keys, vals)
+        ds_out[bb] = lab
+        keys_all.append(keys)
+        vals_all.append(vals)
+        log("processed block %i" % bid)  # (the reference's line: after the block's final write)
+    rows = np.stack([np.concatenate(keys_all) if keys_all else np.zeros(0, np.uint64),
+                     np.concatenate(vals_all) if vals_all else np.zeros(0, np.uint64)], axis=1)
+    np.save(rows_file(tmp_folder, job_id), rows)
+    dist.barrier()
+    if job_id == 0:
+        # the assignment table as FindLabeling writes it, and Write's maxId
+        parts = [np.load(rows_file(tmp_folder, j)) for j in range(dist.get_world_size())]
+        table = np.concatenate(parts) if parts else np.zeros((0, 2), np.uint64)
+        if len(table):
+            _, first = np.unique(table[:, 0], return_index=True)
+            table = table[first]
+        if has_zero:
+            table = np.concatenate([np.zeros((1, 2), np.uint64), table])
+        table = table.astype(np.uint64)
+        with vu.file_reader(assignment_path) as f:
+            if assignment_key in f:
+                import shutil
+                shutil.rmtree(os.path.join(assignment_path, assignment_key), ignore_errors=True)
+            ds = f.create_dataset(assignment_key, shape=table.shape, dtype='uint64', compression='gzip',
+                                  chunks=(max(1, min(1000000, len(table))), 2))
+            ds[:] = table
+        ds_out.attrs['maxId'] = int(table[:, 1].max()) if len(table) else 0
+        for j in range(dist.get_world_size()):
+            os.remove(rows_file(tmp_folder, j))
+    dist.barrier()
+    return n_new

@@ -2,8 +2,12 @@
 
 Watershed{Local,Slurm,LSF} (or TwoPassWatershed* with two_pass=True), then RelabelWorkflow
 (FindUniques -> FindLabeling -> Write in place, assignment table at
-output_path/'relabel_watershed').  The optional post-watershed agglomeration of the reference
-(agglomeration=True, nifty RAG + clustering) is out of scope for this build and raises.
+output_path/'relabel_watershed').  One-pass runs with target 'local' fold the relabel into the
+watershed jobs (relabel_in_job, default on): the jobs exchange their per-block id counts over a
+process group and write the final ids, the table and maxId themselves (job_relabel.py); the
+output, table and maxId are those of the three-task RelabelWorkflow.  The optional
+post-watershed agglomeration of the reference (agglomeration=True, nifty RAG + clustering) is out
+of scope for this build and raises.
 """
 import os
 
@@ -23,6 +27,8 @@ class WatershedWorkflow(WorkflowBase):
     mask_key = luigi.Parameter(default='')
     two_pass = luigi.BoolParameter(default=False)
     agglomeration = luigi.BoolParameter(default=False)
+    # not in the reference: the relabel inside the local watershed jobs (see above)
+    relabel_in_job = luigi.BoolParameter(default=True)
 
     def requires(self):
         if self.agglomeration:
@@ -32,6 +38,12 @@ class WatershedWorkflow(WorkflowBase):
             ws_task = getattr(two_pass_tasks, self._get_task_name('TwoPassWatershed'))
         else:
             ws_task = getattr(watershed_tasks, self._get_task_name('Watershed'))
+        if self.relabel_in_job and not self.two_pass and self.target == 'local':
+            return ws_task(tmp_folder=self.tmp_folder, max_jobs=self.max_jobs, config_dir=self.config_dir,
+                           input_path=self.input_path, input_key=self.input_key,
+                           output_path=self.output_path, output_key=self.output_key,
+                           mask_path=self.mask_path, mask_key=self.mask_key,
+                           assignment_path=self.output_path, assignment_key='relabel_watershed')
         # the watershed jobs keep the uniques of the blocks they write; FindUniques reads those
         # instead of the label volume
         uniques_path = os.path.join(self.tmp_folder, 'watershed_block_uniques')

@@ -25,13 +25,17 @@ def main():
     cfg = bench.CONFIGS[3]
     z = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     jobs = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    in_job = (sys.argv[3] != '0') if len(sys.argv) > 3 else True   # relabel_in_job
     shape = (z,) + tuple(cfg['shape'][1:])
-    d = os.path.join(HERE, 'gpurun_out', 'e2e')
+    import shutil
+    import tempfile
+    d = tempfile.mkdtemp(prefix='ctws_e2e_probe_')   # (data stays off gpurun_out)
     os.makedirs(os.path.join(d, 'configs'), exist_ok=True)
     x = boundary_map_torch(shape, seed=1, device=torch.device('cuda', 0), pitch=cfg['pitch']).cpu().numpy()
     inp = os.path.join(d, 'data.n5')
     with vu.file_reader(inp) as f:
-        ds = f.create_dataset('boundaries', shape=shape, dtype=x.dtype, chunks=(32, 256, 256))
+        ds = f.create_dataset('boundaries', shape=shape, dtype=x.dtype,
+                              chunks=tuple(b // 2 for b in cfg['block_shape']))
         ds.n_threads = 16
         ds[...] = x
     with open(os.path.join(d, 'configs', 'global.config'), 'w') as f:
@@ -45,9 +49,11 @@ def main():
             'from cluster_tools_amd import luigi_compat as luigi\n'
             'from cluster_tools_amd.watershed import WatershedWorkflow\n'
             'wf = WatershedWorkflow(input_path=%r, input_key="boundaries", output_path=%r, output_key="ws", '
-            'config_dir=%r, tmp_folder=%r, target="local", max_jobs=%d)\n'
+            'config_dir=%r, tmp_folder=%r, target="local", max_jobs=%d, relabel_in_job=%r)\n'
             'sys.exit(0 if luigi.build([wf], local_scheduler=True) else 1)\n'
-            % (HERE, inp, os.path.join(d, 'ws.n5'), os.path.join(d, 'configs'), os.path.join(d, 'tmp'), jobs))
+            % (HERE, inp, os.path.join(d, 'ws.n5'), os.path.join(d, 'configs'), os.path.join(d, 'tmp'), jobs, in_job))
+    del x
+    print('volume %s, %d jobs, relabel_in_job %s' % (shape, jobs, in_job), flush=True)
     t0 = datetime.now()
     tt = time.perf_counter()
     rc = subprocess.call([sys.executable, '-c', code])
@@ -62,6 +68,7 @@ def main():
         if log.endswith('_0.log'):
             for t, l in zip(ts, lines):
                 print('      %6.2f %s' % ((t - t0).total_seconds(), l.split(': ', 1)[1].strip()[:90]))
+    shutil.rmtree(d, ignore_errors=True)
 
 
 if __name__ == '__main__':

@@ -99,7 +99,10 @@ def _check_result(res, with_mask, ref=None):
 
 @pytest.mark.parametrize('name', sorted(CONFIGS))
 @pytest.mark.parametrize('with_mask', [False, True])
-def test_watershed_workflow(tmp_path, name, with_mask):
+@pytest.mark.parametrize('relabel_in_job', [True, False])
+def test_watershed_workflow(tmp_path, name, with_mask, relabel_in_job):
+    """relabel_in_job: the relabel folded into the watershed jobs (their process group's offset
+    scan, job_relabel.py) must give the three-task RelabelWorkflow's volume, table and maxId."""
     from cluster_tools_amd.watershed import WatershedWorkflow
     from cluster_tools_amd.watershed.watershed import WatershedLocal
     cfg_dir, inp, x, c = _setup(tmp_path, name, with_mask)
@@ -117,7 +120,7 @@ def test_watershed_workflow(tmp_path, name, with_mask):
     # 2. the whole workflow (watershed + relabel)
     wf = WatershedWorkflow(input_path=inp, input_key='boundaries', output_path=out, output_key='ws',
                            config_dir=cfg_dir, tmp_folder=str(tmp_path / 'tmp'), target='local', max_jobs=2,
-                           **mask_kw)
+                           relabel_in_job=relabel_in_job, **mask_kw)
     _build(wf, tmp_path / 'tmp')
     with vu.file_reader(out, 'r') as f:
         res = f['ws'][:]
@@ -132,6 +135,8 @@ def test_watershed_workflow(tmp_path, name, with_mask):
     start = 0 if uniq[0] == 0 else 1
     np.testing.assert_array_equal(table[:, 0], uniq)
     np.testing.assert_array_equal(table[:, 1], np.arange(start, start + len(uniq), dtype='uint64'))
+    if relabel_in_job:
+        return
     # the watershed jobs' per-block uniques that FindUniques read instead of the volume: one
     # file per written block (mask-skipped blocks have none and are read), each np.unique of
     # the block's raw labels
