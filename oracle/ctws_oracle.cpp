@@ -441,6 +441,10 @@ struct PQCompare {
 // the GPU must reproduce bit for bit, and VI(model, vigra) is the tie-break gap.
 // ---------------------------------------------------------------------------------------
 int g_flood_model = 0;
+// tie orders for the tie-order experiment (scripts/tie_order_experiment.py): the GPU's
+// order is 1.  2: (C, label), no hop distance; 3: (C, d, -label); 4: (C, d, push count) = FIFO
+// inside an equal-(C, d) front; 5: (C, push count) = FIFO on a plateau
+int g_tie_order = 1;
 
 inline uint32_t ordf(float f) {
     uint32_t u;
@@ -452,11 +456,17 @@ struct ModelEntry {
     uint64_t key;
     uint32_t label;
     int64_t node;
+    uint64_t seq;  // push count (tie orders 4, 5)
 };
 struct ModelCompare {
     bool operator()(const ModelEntry& a, const ModelEntry& b) const {
         if (a.key != b.key) return a.key > b.key;
-        return a.label > b.label;
+        switch (g_tie_order) {
+            case 3: return a.label < b.label;
+            case 4:
+            case 5: return a.seq > b.seq;
+            default: return a.label > b.label;
+        }
     }
 };
 
@@ -464,10 +474,12 @@ uint32_t watersheds_model(const float* h, const Dims& d, uint32_t* labels) {
     auto nb = direct_nbrs(d.nd);
     std::priority_queue<ModelEntry, std::vector<ModelEntry>, ModelCompare> pq;
     uint32_t maxRegionLabel = 0;
+    uint64_t seq = 0;
+    const bool use_d = g_tie_order != 2 && g_tie_order != 5;
     for (int64_t i = 0; i < d.size; ++i)
         if (labels[i]) {
             maxRegionLabel = std::max(maxRegionLabel, labels[i]);
-            pq.push({(uint64_t)ordf(h[i]) << 32, labels[i], i});
+            pq.push({(uint64_t)ordf(h[i]) << 32, labels[i], i, seq++});
         }
     int64_t c[3];
     while (!pq.empty()) {
@@ -484,8 +496,8 @@ uint32_t watersheds_model(const float* h, const Dims& d, uint32_t* labels) {
                 const uint32_t cc = (uint32_t)(e.key >> 32);
                 // d saturates at 4095 (12-bit field of the GPU's packed key)
                 const uint64_t k = hb > cc ? ((uint64_t)hb << 32)
-                                           : ((e.key & 0xFFFFFFFFull) >= 4095ull ? e.key : e.key + 1ull);
-                pq.push({k, e.label, j});
+                                           : (!use_d || (e.key & 0xFFFFFFFFull) >= 4095ull ? e.key : e.key + 1ull);
+                pq.push({k, e.label, j, seq++});
             }
         }
     }
@@ -860,6 +872,7 @@ const char* orc_last_error() { return g_err.c_str(); }
 
 // 0: vigra's heap order (the reference); 1: the GPU flood's (C, d, label) order (model)
 void orc_set_flood_model(int on) { g_flood_model = on; }
+void orc_set_tie_order(int order) { g_tie_order = order; }
 
 // stage-level entry points (for cross-checks against scipy / scikit-image)
 int orc_distance_transform(const uint8_t* fg, int nd, const int64_t* shape, const double* pitch,
