@@ -3,15 +3,20 @@
     python scripts/roofline_from_trace.py <run_kernel_trace.csv> <bench line .json> <runs>
 
 The trace must come from `bench.py --streams 1 --no-host --no-cpu-baseline` (one library
-stream, no host-resident pass), `runs` = warmup + steps of that command.  The flood stage of a
-batch is every dispatch from its k_descent_tile up to and including the first k_flood_verify
-after it (the second verify of a batch belongs to the size-filter regrow).  Prints the summed
+stream, no host-resident pass), `runs` = warmup + steps of that command.  Dispatches are
+assigned to stages by scripts/stage_map.py (the rule pmc_traffic.py uses for the bytes): the
+flood of a batch is every dispatch from its k_descent_tile up to the size filter's first kernel
+(the regrow's frontier launches and check belong to the size filter).  Prints the summed
 kernel time per step, the achieved GB/s of the stage's algorithmic bytes (12 B per outer voxel,
 SURVEY.md §8(d)) and the bench line's own HIP-event figure beside it.
 """
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from stage_map import classify, short as kshort  # noqa: E402
 
 
 def main():
@@ -22,19 +27,20 @@ def main():
             rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']))
     rows.sort()
     line = json.loads([l for l in open(bench).read().splitlines() if l.startswith('{')][-1])
-    flood_ns, per_kernel, in_flood, batches = 0, {}, False, 0
-    for s, e, name in rows:
-        if 'ctws::' not in name or 'k_copy_to_host' in name:
-            continue  # library kernels of the stage only (no torch, no host-path copies)
-        short = name.split('(')[0].replace('void ', '').replace('ctws::', '')
+    flood_ns, per_kernel, batches = 0, {}, 0
+    rows = [r for r in rows if 'k_copy_to_host' not in r[2]]  # (host-path copies: not the stage)
+    stage_ms = {}
+    for (s, e, name), st in zip(rows, classify([r[2] for r in rows])):
+        if st is None:
+            continue  # library kernels of the stage only (no torch)
+        stage_ms[st] = stage_ms.get(st, 0) + (e - s)
+        if st != 'flood':
+            continue
+        short = kshort(name)
         if short.startswith('k_descent_tile'):
-            in_flood = True
             batches += 1
-        if in_flood:
-            flood_ns += e - s
-            per_kernel[short] = per_kernel.get(short, 0) + (e - s)
-            if short.startswith('k_flood_verify'):
-                in_flood = False
+        flood_ns += e - s
+        per_kernel[short] = per_kernel.get(short, 0) + (e - s)
     ms = flood_ns / 1e6 / runs
     alg = line['roofline']['alg_bytes']
     achieved = alg / (ms * 1e-3) / 1e9
@@ -43,7 +49,8 @@ def main():
            'achieved_GBs': round(achieved, 1), 'frac': round(achieved / line['roofline']['peak'], 4),
            'bench_hip_event_ms': line['roofline']['ms_per_step'], 'bench_frac': line['roofline']['frac'],
            'agreement': round(ms / line['roofline']['ms_per_step'], 3),
-           'per_kernel_ms_per_step': {k: round(v / 1e6 / runs, 3) for k, v in sorted(per_kernel.items())}}
+           'per_kernel_ms_per_step': {k: round(v / 1e6 / runs, 3) for k, v in sorted(per_kernel.items())},
+           'stage_ms_per_step': {k: round(v / 1e6 / runs, 3) for k, v in sorted(stage_ms.items())}}
     print(json.dumps(out, indent=1))
 
 
