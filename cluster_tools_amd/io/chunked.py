@@ -18,6 +18,7 @@ import json
 import os
 import threading
 import zlib
+from collections import OrderedDict
 from concurrent import futures
 from itertools import product
 
@@ -112,6 +113,12 @@ class Dataset:
         self.path = path
         self.fmt = fmt
         self.n_threads = 1
+        # decompressed-chunk cache for reads (bytes; 0 = off): blocks read with halos share their
+        # border chunks, a job reading neighbouring blocks then inflates each chunk once
+        self.cache_bytes = 0
+        self._cache = OrderedDict()
+        self._cache_used = 0
+        self._cache_lock = threading.Lock()
         if fmt == 'n5':
             with open(os.path.join(path, 'attributes.json')) as f:
                 meta = json.load(f)
@@ -159,6 +166,24 @@ class Dataset:
 
     def read_chunk(self, cid):
         """Chunk data (valid region, C order) or None if the chunk does not exist."""
+        if self.cache_bytes:
+            with self._cache_lock:
+                hit = self._cache.get(cid)
+                if hit is not None:
+                    self._cache.move_to_end(cid)
+                    return hit
+        arr = self._read_chunk(cid)
+        if self.cache_bytes and arr is not None and arr.nbytes <= self.cache_bytes:
+            with self._cache_lock:
+                if cid not in self._cache:
+                    self._cache[cid] = arr
+                    self._cache_used += arr.nbytes
+                    while self._cache_used > self.cache_bytes:
+                        _, old = self._cache.popitem(last=False)
+                        self._cache_used -= old.nbytes
+        return arr
+
+    def _read_chunk(self, cid):
         p = self._chunk_path(cid)
         if not os.path.exists(p):
             return None
@@ -245,7 +270,7 @@ class Dataset:
             if full:
                 chunk = np.ascontiguousarray(value[tuple(src)], dtype=self.dtype)
             else:
-                old = self.read_chunk(cid)
+                old = self._read_chunk(cid)
                 chunk = np.full(tuple(e - b for b, e in zip(beg, end)), self._fill, dtype=self.dtype) \
                     if old is None else old.copy()
                 chunk[tuple(dst)] = value[tuple(src)]

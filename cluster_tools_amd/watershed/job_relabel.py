@@ -63,6 +63,24 @@ def block_table(uniques, offset, dup):
     return nz, vals
 
 
+def write_blocks(ds_out, written, log, n_threads=None):
+    """ds_out[bb] = labels for every (block_id, bb, labels): the chunks of all blocks through one
+    pool (a block's chunks alone are too few to keep the job's threads busy); "processed block"
+    after each block's last chunk, in block order."""
+    from concurrent import futures
+    n_threads = n_threads or max(4, getattr(ds_out, 'n_threads', 1))
+    single = getattr(ds_out, 'n_threads', 1)
+    ds_out.n_threads = 1
+    try:
+        with futures.ThreadPoolExecutor(n_threads) as pool:
+            futs = [(bid, pool.submit(ds_out.__setitem__, bb, lab)) for bid, bb, lab in written]
+            for bid, f in futs:
+                f.result()
+                log("processed block %i" % bid)  # (the reference's line: after the block's write)
+    finally:
+        ds_out.n_threads = single
+
+
 def rows_file(tmp_folder, job_id):
     return os.path.join(tmp_folder, 'watershed_relabel_rows_job_%i.npy' % job_id)
 
@@ -116,7 +134,8 @@ def relabel_in_job(job_id, results, ds_out, tmp_folder, assignment_path, assignm
     offs, n_new = scan(rows_all)
     has_zero = bool(flags[:, 4].any() or rows_all[:, 4].any())
     log("global ids: %i (offset scan over %i blocks)" % (n_new, len(rows_all)))
-    keys_all, vals_all = [], []
+    # map every block (GPU lookup), then write them all through one pool of chunk writers
+    written, tables = [], {}
     for bid, bb, lab, u in results:
         if lab is None:
             continue
@@ -124,33 +143,45 @@ def relabel_in_job(job_id, results, ds_out, tmp_folder, assignment_path, assignm
         keys, vals = block_table(u, off, dup)
         if len(keys):
             mapper(lab, keys, vals)
-        ds_out[bb] = lab
-        keys_all.append(keys)
-        vals_all.append(vals)
-        log("processed block %i" % bid)  # (the reference's line: after the block's final write)
-    rows = np.stack([np.concatenate(keys_all) if keys_all else np.zeros(0, np.uint64),
-                     np.concatenate(vals_all) if vals_all else np.zeros(0, np.uint64)], axis=1)
-    np.save(rows_file(tmp_folder, job_id), rows)
+        # (a duplicated first id keeps the previous block's row in the table)
+        tables[bid] = (keys[dup:], vals[dup:])
+        written.append((bid, bb, lab))
+    write_blocks(ds_out, written, log)
+    # this job's table rows in block order, with each block's row count
+    bids = sorted(tables)
+    np.save(rows_file(tmp_folder, job_id), np.stack([
+        np.concatenate([tables[b][0] for b in bids]) if bids else np.zeros(0, np.uint64),
+        np.concatenate([tables[b][1] for b in bids]) if bids else np.zeros(0, np.uint64)], axis=1))
+    np.save(rows_file(tmp_folder, job_id) + '.blocks.npy',
+            np.array([[b, len(tables[b][0])] for b in bids], np.int64).reshape(-1, 2))
     dist.barrier()
     if job_id == 0:
-        # the assignment table as FindLabeling writes it, and Write's maxId
-        parts = [np.load(rows_file(tmp_folder, j)) for j in range(dist.get_world_size())]
-        table = np.concatenate(parts) if parts else np.zeros((0, 2), np.uint64)
-        if len(table):
-            _, first = np.unique(table[:, 0], return_index=True)
-            table = table[first]
+        # the assignment table as FindLabeling writes it (rows sorted by old id = block order),
+        # assembled from the jobs' per-block row runs without a sort, and Write's maxId
+        runs = []
+        for j in range(dist.get_world_size()):
+            rows = np.load(rows_file(tmp_folder, j))
+            blocks = np.load(rows_file(tmp_folder, j) + '.blocks.npy')
+            start = 0
+            for b, n in blocks:
+                runs.append((int(b), rows[start:start + n]))
+                start += n
+        runs.sort(key=lambda r: r[0])
+        table = np.concatenate([r for _, r in runs]) if runs else np.zeros((0, 2), np.uint64)
         if has_zero:
             table = np.concatenate([np.zeros((1, 2), np.uint64), table])
-        table = table.astype(np.uint64)
+        table = np.ascontiguousarray(table, dtype=np.uint64)
         with vu.file_reader(assignment_path) as f:
             if assignment_key in f:
                 import shutil
                 shutil.rmtree(os.path.join(assignment_path, assignment_key), ignore_errors=True)
             ds = f.create_dataset(assignment_key, shape=table.shape, dtype='uint64', compression='gzip',
                                   chunks=(max(1, min(1000000, len(table))), 2))
+            ds.n_threads = 8
             ds[:] = table
         ds_out.attrs['maxId'] = int(table[:, 1].max()) if len(table) else 0
         for j in range(dist.get_world_size()):
             os.remove(rows_file(tmp_folder, j))
+            os.remove(rows_file(tmp_folder, j) + '.blocks.npy')
     dist.barrier()
     return n_new

@@ -63,10 +63,14 @@ class WatershedBase(luigi.Task):
         shape, ws_config = ws_task_setup(self, block_shape)
         blocks = self.blocks_to_process(shape, block_shape, roi_begin, roi_end, block_list_path)
         n_jobs = min(len(blocks), self.max_jobs)
+        consecutive = False
         if self.assignment_key != '' and isinstance(self, LocalTask):
             ws_config['relabel'] = relabel_job_config(self, n_jobs)
             self.allow_retry = False  # the group numbers all blocks at once: no partial re-runs
-        self.run_jobs(n_jobs, blocks, ws_config)
+            # a job takes consecutive blocks (neighbours: their halo chunks are inflated once,
+            # ds_in's chunk cache); which job runs a block does not change its result
+            consecutive = True
+        self.run_jobs(n_jobs, blocks, ws_config, consecutive_blocks=consecutive)
 
 
 def ws_task_setup(task, block_shape):
@@ -233,6 +237,9 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
     batches = make_batches(blocking, block_list, config, pass_id, batch_blocks)
     n_io = max(1, int(config.get('threads_per_job', 1)))
     ds_in.n_threads = ds_out.n_threads = max(n_io, 4)
+    if hasattr(ds_in, 'cache_bytes'):
+        # inflate each input chunk once for the job's blocks with halos (n5 / zarr reader)
+        ds_in.cache_bytes = int(float(config.get('read_cache_gb', 2.0)) * (1 << 30))
 
     def read_batch(ids):
         return [_read_block(blocking, bid, ds_in, ds_out, mask, config, pass_id) for bid in ids]
@@ -312,19 +319,26 @@ def _run_blocks_relabel(job_id, blocking, ds_in, ds_out, mask, config, rel):
     import torch.distributed as dist
     from cluster_tools_amd import ctws
     from cluster_tools_amd.watershed import job_relabel
+    # the group first: all jobs start together, so the rendezvous is immediate; a job that dies
+    # later breaks its peers' pending collective (gloo / RCCL report the lost peer) instead of
+    # leaving them waiting out the timeout
+    job_relabel.init_group(job_id, rel['n_jobs'], rel['port'], rel['backend'], device=_device())
     keep, failed = [], None
     try:
-        run_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, pass_id=0, keep=keep)
-    except Exception as e:  # still join the group: every job then raises instead of waiting
-        import traceback
-        traceback.print_exc()
-        failed = e
-    job_relabel.init_group(job_id, rel['n_jobs'], rel['port'], rel['backend'], device=_device())
-    try:
-        with ctws.Handle(_device()) as h:
-            job_relabel.relabel_in_job(job_id, keep, ds_out, rel['tmp_folder'], rel['assignment_path'],
-                                       rel['assignment_key'], lambda lab, k, v: h.lookup_u64(lab, k, v),
-                                       failed=failed is not None, log=fu.log, device=_device())
+        try:
+            run_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, pass_id=0, keep=keep)
+        except Exception as e:  # still take part in the exchange: every job then raises
+            import traceback
+            traceback.print_exc()
+            failed = e
+        if failed is None:
+            with ctws.Handle(_device()) as h:
+                job_relabel.relabel_in_job(job_id, keep, ds_out, rel['tmp_folder'], rel['assignment_path'],
+                                           rel['assignment_key'], lambda lab, k, v: h.lookup_u64(lab, k, v),
+                                           log=fu.log, device=_device())
+        else:
+            job_relabel.relabel_in_job(job_id, [], ds_out, rel['tmp_folder'], rel['assignment_path'],
+                                       rel['assignment_key'], None, failed=True, log=fu.log, device=_device())
     finally:
         dist.destroy_process_group()
     if failed is not None:

@@ -151,9 +151,12 @@ def test_no_retry_without_budget_renames_log(tmp_path):
     assert os.path.exists(str(tmp_path / 'tmp' / 'failing_task_failed.log'))
 
 
-def test_watershed_task_writes_job_configs_and_fails_loudly_without_gpu(tmp_path):
+@pytest.mark.parametrize('relabel_in_job', [True, False])
+def test_watershed_task_writes_job_configs_and_fails_loudly_without_gpu(tmp_path, relabel_in_job):
     """Without a GPU the job processes die before 'processed job': the task raises, the
-    workflow returns False and the task log is renamed (no silent CPU fallback)."""
+    workflow returns False and the task log is renamed (no silent CPU fallback).  With the
+    relabel in the jobs (job_relabel.py) the jobs take consecutive blocks and fail together
+    through their process group instead of waiting for each other."""
     import torch
     if torch.cuda.is_available():
         pytest.skip('GPU present')
@@ -164,11 +167,14 @@ def test_watershed_task_writes_job_configs_and_fails_loudly_without_gpu(tmp_path
     with vu.file_reader(inp) as f:
         f.create_dataset('raw', data=boundary_map((32, 64, 64), seed=2), chunks=(16, 32, 32))
     wf = WatershedWorkflow(input_path=inp, input_key='raw', output_path=str(tmp_path / 'ws.n5'), output_key='ws',
-                           config_dir=cfg, tmp_folder=str(tmp_path / 'tmp'), target='local', max_jobs=2)
+                           config_dir=cfg, tmp_folder=str(tmp_path / 'tmp'), target='local', max_jobs=2,
+                           relabel_in_job=relabel_in_job)
     assert not luigi.build([wf], local_scheduler=True)
     tmp = tmp_path / 'tmp'
     job0 = json.load(open(str(tmp / 'watershed_job_0.config')))
-    assert job0['block_list'] == [0, 2, 4, 6] and job0['threshold'] == .5 and job0['block_shape'] == [16, 32, 32]
+    blocks0 = [0, 1, 2, 3] if relabel_in_job else [0, 2, 4, 6]
+    assert job0['block_list'] == blocks0 and job0['threshold'] == .5 and job0['block_shape'] == [16, 32, 32]
+    assert ('relabel' in job0) == relabel_in_job
     assert os.path.exists(str(tmp / 'watershed_failed.log'))
     assert os.path.exists(str(tmp / 'watershed.py'))
     assert open(str(tmp / 'watershed.py')).readline().strip() == '#! ' + sys.executable
