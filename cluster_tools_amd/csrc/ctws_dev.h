@@ -329,12 +329,18 @@ constexpr uint32_t kLabelBits = 20;
 constexpr uint64_t kLabelMask = (1ull << kLabelBits) - 1ull;
 constexpr uint64_t kDOne = 1ull << kLabelBits;
 constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
+// The tie order inside an equal-C plateau: d = min(hops since the plateau level was entered,
+// kDMax).  kDMax = 1 ("entered at the voxel's own height, or flooded over") measured closest to
+// vigra's binary-heap order on tie-dominated inputs (scripts/tie_order_experiment.py,
+// profiles/r04/tie_order_experiment.json: WatershedFromSeeds on uint8 VI 0.54 -> 0.15, clamped
+// raw map 1.78 -> 0.52; every BASELINE config block 0 either way).  INF stays INF (d = 0xFFF).
+constexpr uint32_t kDMax = 1;
 
 // K(q) = f_q(min over the neighbours): a neighbour key `best` pushed into voxel q of height hb
 __device__ __forceinline__ uint64_t f_packed(uint32_t hb, uint64_t best) {
     const uint32_t c = (uint32_t)(best >> 32);
     if (hb > c) return ((uint64_t)hb << 32) | (best & kLabelMask);
-    return ((best & kDMask) == kDMask) ? best : best + kDOne;
+    return ((best & kDMask) >= ((uint64_t)kDMax << kLabelBits)) ? best : best + kDOne;
 }
 
 // seed test: from the seed CC parents (pass 1: `cc` = PF after k_root_label) or, when cc is

@@ -48,7 +48,7 @@ __device__ __forceinline__ void take_min(uint64_t nk, uint32_t nl, uint64_t& bk,
 __device__ __forceinline__ uint64_t f_key(uint32_t hb, uint64_t bk) {
     const uint32_t c = (uint32_t)(bk >> 32);
     if (hb > c) return (uint64_t)hb << 32;
-    return bk + 1ull;  // (C, d + 1); d never reaches 2^32
+    return (uint32_t)bk >= kDMax ? bk : bk + 1ull;  // (C, min(d + 1, kDMax)), as f_packed
 }
 
 template <int ND>

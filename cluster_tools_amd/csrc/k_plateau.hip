@@ -27,11 +27,11 @@
 
 namespace ctws {
 
-// n more hops inside the plateau: d + n, saturating as f_packed does; INF stays INF
+// n more hops inside the plateau: d + n, saturating at kDMax as f_packed does; INF stays INF
 __device__ __forceinline__ uint64_t key_hops(uint64_t k, uint32_t n) {
     if (k == kPackInf) return k;
     const uint32_t d = (uint32_t)((k & kDMask) >> kLabelBits);
-    const uint32_t d2 = min(d + n, 4095u);
+    const uint32_t d2 = min(d + n, kDMax);
     return (k & ~kDMask) | ((uint64_t)d2 << kLabelBits);
 }
 

@@ -442,9 +442,9 @@ struct PQCompare {
 // ---------------------------------------------------------------------------------------
 int g_flood_model = 0;
 // tie orders for the tie-order experiment (scripts/tie_order_experiment.py): the GPU's
-// order is 1.  2: (C, label), no hop distance; 3: (C, d, -label); 4: (C, d, push count) = FIFO
-// inside an equal-(C, d) front; 5: (C, push count) = FIFO on a plateau
-int g_tie_order = 1;
+// order is 6 (kDMax = 1 in cluster_tools_amd/csrc/ctws_dev.h; order 1 was rounds 1-3's).  2: (C, label), no hop distance; 3: (C, d, -label); 4: (C, d, push count) = FIFO
+// inside an equal-(C, d) front; 5: (C, push count) = FIFO on a plateau; 6: (C, min(d, 1), label)
+int g_tie_order = 6;
 
 inline uint32_t ordf(float f) {
     uint32_t u;
@@ -495,8 +495,9 @@ uint32_t watersheds_model(const float* h, const Dims& d, uint32_t* labels) {
                 const uint32_t hb = ordf(h[j]);
                 const uint32_t cc = (uint32_t)(e.key >> 32);
                 // d saturates at 4095 (12-bit field of the GPU's packed key)
+                const uint64_t dcap = g_tie_order == 6 ? 1ull : 4095ull;
                 const uint64_t k = hb > cc ? ((uint64_t)hb << 32)
-                                           : (!use_d || (e.key & 0xFFFFFFFFull) >= 4095ull ? e.key : e.key + 1ull);
+                                           : (!use_d || (e.key & 0xFFFFFFFFull) >= dcap ? e.key : e.key + 1ull);
                 pq.push({k, e.label, j, seq++});
             }
         }

@@ -7,11 +7,13 @@ vigra's watershedsNew pops a std::priority_queue keyed by priority alone, so equ
 (oracle/ctws_oracle.cpp:watersheds_new).  The GPU's flood computes the unique fixpoint of one
 total order (k_flood.hip: C, then the hop distance d inside an equal-C plateau, then the label);
 oracle watersheds_model restates it.  Orders compared (oracle g_tie_order):
-  1 (C, d, label)  -- the GPU's
+  1 (C, d, label)  -- the GPU's in rounds 1-3 (d saturating at 4095)
   2 (C, label)     -- no hop distance
   3 (C, d, -label)
   4 (C, d, push count): FIFO inside an equal-(C, d) front
   5 (C, push count):    FIFO on a plateau
+  6 (C, min(d, 1), label): the hop distance reduced to "entered at its own height or not" --
+                           the GPU's since round 4 (the closest to the heap overall)
 Only orders of the form (C, d?, label-ish) are fixpoints a parallel relaxation can reach; 4 and 5
 are sequential references for how close an insertion-ordered queue gets.
 Output: VI(order, heap) per case, JSON on stdout."""
@@ -46,12 +48,12 @@ def main():
         heap = run()
         ign = [0] if block.get('mask') is not None else None
         row = {}
-        for order in (1, 2, 3, 4, 5):
+        for order in (1, 2, 3, 4, 5, 6):
             L.orc_set_tie_order(order)
             with O.flood_model():
                 m = run()
             row[order] = round(float(sum(vi_scores(m, heap, ign))), 4)
-        L.orc_set_tie_order(1)
+        L.orc_set_tie_order(6)
         out['%s:%s' % (kind, name)] = row
         print(name, row, file=sys.stderr, flush=True)
     print(json.dumps(out, indent=1))
