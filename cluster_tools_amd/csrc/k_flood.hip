@@ -588,15 +588,15 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
     const float* hb = h + B.base;
     constexpr int NT = kDescThreads, PER = TN / NT;  // voxels per thread: c = threadIdx.x + k * NT
     static_assert(TN % NT == 0 && PER <= 32, "");
-    // seed entries of the thread's voxels (cc parent or lab), then the halo heights: every load
-    // unconditional (clamped index, global address space) so that all of them are in flight
-    // together; out-of-block values are selected away afterwards
-    // cc (the seed forest): members only, their bits in sbits; the tile's bitmap rows (a 32-bit
-    // half word per TX <= 32 voxels of a row) go to LDS with the halo, the entries are loaded
-    // unconditionally (a non-member's entry is stale and selected away by its bit)
+    // seed entries of the thread's voxels, then the halo heights: loads unconditional (clamped
+    // index, global address space) so that all of them are in flight together; out-of-block
+    // values are selected away afterwards.
+    // lab (pass 2, fallbacks): every voxel's entry (kFixedBit = seed).  cc (the seed forest,
+    // pass 1): members only, their bits in sbits; the tile's bitmap rows (a 32-bit half word per
+    // TX <= 32 voxels of a row) go to LDS with the halo heights, and only the members' entries
+    // (~1 % of the voxels) are loaded after that, a second round trip instead of 4 B per voxel
     constexpr int WPR32 = (TX + 31) / 32, NW32 = TZ * TY * WPR32;
     __shared__ uint32_t sbm[NW32];
-    const uint32_t* sdsrc = cc ? cc : lab;
     uint32_t inm = 0, seedm = 0;
     uint32_t sv[PER];
 #pragma unroll
@@ -605,7 +605,7 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = min(z0 + lz, B.Z - 1), gy = min(y0 + ly, B.Y - 1), gx = min(x0 + lx, B.X - 1);
         inm |= ((z0 + lz < B.Z && y0 + ly < B.Y && x0 + lx < B.X) ? 1u : 0u) << k;
-        sv[k] = gbl(sdsrc)[B.base + gz * YX + (int64_t)gy * B.X + gx];
+        sv[k] = cc ? kNoParent : gbl(lab)[B.base + gz * YX + (int64_t)gy * B.X + gx];
     }
     static_assert(NW32 <= NT, "");
     uint32_t bwv = ~0u;
@@ -639,14 +639,19 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
     }
     if (cc && (int)threadIdx.x < NW32) sbm[threadIdx.x] = bwv;
     __syncthreads();
+    if (cc) {
+        // the members' seed-forest entries
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int c = threadIdx.x + k * NT;
+            const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY), r = c / TX;
+            const int gx = x0 + lx;
+            if (((inm >> k) & 1u) && ((sbm[r * WPR32 + (lx >> 5)] >> (gx & 31)) & 1u))
+                sv[k] = gbl(cc)[B.base + (z0 + lz) * YX + (int64_t)(y0 + ly) * B.X + gx];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-        if (cc) {
-            const int c = threadIdx.x + k * NT;
-            const int lx = c % TX, r = c / TX;
-            const int gx = x0 + lx;
-            if (!((sbm[r * WPR32 + (lx >> 5)] >> (gx & 31)) & 1u)) sv[k] = kNoParent;
-        }
         const bool sd = cc ? sv[k] != kNoParent : (sv[k] & kFixedBit) != 0u;
         seedm |= (((inm >> k) & 1u) && sd ? 1u : 0u) << k;
     }
