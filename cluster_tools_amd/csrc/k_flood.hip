@@ -383,9 +383,9 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
             const uint32_t bh = (uint32_t)(b >> 32), bl = (uint32_t)b;
             const bool above = hb[p] > bh;
             const uint32_t nh = max(hb[p], bh);
-            uint32_t inc;
-            const bool ovf = __builtin_add_overflow(bl, 1u << kLabelBits, &inc);
-            const uint32_t nl = above ? (bl & (uint32_t)kLabelMask) : (ovf ? bl : inc);
+            // d + 1 saturating at kDMax, as f_packed
+            const bool sat = (bl >> kLabelBits) >= kDMax;
+            const uint32_t nl = above ? (bl & (uint32_t)kLabelMask) : (sat ? bl : bl + (1u << kLabelBits));
             uint64_t nk = ((uint64_t)nh << 32) | nl;
             nk = (upd & (1u << p)) ? nk : v[p];
             chg |= (nk != v[p]) ? (1u << p) : 0u;
@@ -956,11 +956,15 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                                   uint32_t* __restrict__ nvisit, int reps, int dirf) {
     static_assert(ND == 3 || CZ == 1, "2-D ws: slices are independent, chunks are one slice deep");
     __shared__ uint64_t schg[kFrontierWaves][64];
-    // dirf: the local sweeps queue only the neighbours a change can lower.  f_q(K) > K for every
-    // key (h > C gives (h, 0) > (C, d); else d + 1), so a neighbour q whose key is <= the new key
-    // of p (read in the same visit: a stale read is >= the current key, keys only decrease)
-    // cannot take a lower key through p.  sdir[d]: changed voxels whose neighbour in direction d
-    // (-z, +z, -y, +y, -x, +x) may improve
+    // dirf: the local sweeps queue only the neighbours a change of p can affect, by the (C, d)
+    // part of the keys (the label ignored).  (C, d) never increases during the relaxation (from
+    // INF: C = max(h, min C), d from the lexicographic minimum), while a key's label may change
+    // either way.  f_q(K) >= K in (C, d), so a neighbour q whose (C, d) is below p's new (C, d)
+    // can neither take a lower key through p nor have had p as its argmin (that needs (C, d)_q
+    // >= (C, d)_p); q's read may be stale, and a stale (C, d) is only larger.  Equal (C, d) is
+    // queued: with d capped (kDMax) a plateau's voxels share (C, 1), and a label change of p
+    // must reach the voxels that took their label from p.  sdir[d]: changed voxels whose
+    // neighbour in direction d (-z, +z, -y, +y, -x, +x) must be re-evaluated
     constexpr int NDIR = ND == 3 ? 6 : 4;
     __shared__ uint64_t sdir[kFrontierWaves][6][64];
     __shared__ uint64_t sfw[kFrontierWaves][64];
@@ -1106,7 +1110,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                 // its bit is shifted out of the chunk or masked by open)
 #pragma unroll
                                 for (int d = 0; d < 6; ++d)
-                                    if ((ND == 3 || d >= 2) && nb[d] > k)
+                                    if ((ND == 3 || d >= 2) && (nb[d] >> kLabelBits) >= (k >> kLabelBits))
                                         atomicOr((unsigned long long*)&sdir[wv][ND == 3 ? d : d - 2][j], 1ull << b);
                             }
                         }
