@@ -329,12 +329,15 @@ constexpr uint32_t kLabelBits = 20;
 constexpr uint64_t kLabelMask = (1ull << kLabelBits) - 1ull;
 constexpr uint64_t kDOne = 1ull << kLabelBits;
 constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
-// The tie order inside an equal-C plateau: d = min(hops since the plateau level was entered,
-// kDMax).  kDMax = 1 ("entered at the voxel's own height, or flooded over") measured closest to
-// vigra's binary-heap order on tie-dominated inputs (scripts/tie_order_experiment.py,
-// profiles/r04/tie_order_experiment.json: WatershedFromSeeds on uint8 VI 0.54 -> 0.15, clamped
-// raw map 1.78 -> 0.52; every BASELINE config block 0 either way).  INF stays INF (d = 0xFFF).
-constexpr uint32_t kDMax = 1;
+// The tie order inside an equal-C plateau: d = hops since the plateau level was entered,
+// saturating at kDMax (the 12-bit field; INF has d = 0xFFF and stays INF).  d must grow along
+// every parent edge: then (C, d) strictly increases from a voxel's argmin neighbour to the voxel,
+// the fixpoint is unique, and any relaxation schedule reaches the sequential model's result.
+// Orders with d capped at 1 or without d measured closer to vigra's heap order on tie-dominated
+// inputs (scripts/tie_order_experiment.py) but lose that: equal keys along a plateau path let a
+// cycle of voxels keep a stale label, and the GPU converged to such a fixpoint (round 4,
+// config-1 2-D test config: VI 0.029 against the model's 0) -- not adopted.
+constexpr uint32_t kDMax = 4095;
 
 // K(q) = f_q(min over the neighbours): a neighbour key `best` pushed into voxel q of height hb
 __device__ __forceinline__ uint64_t f_packed(uint32_t hb, uint64_t best) {

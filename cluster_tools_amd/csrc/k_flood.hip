@@ -961,10 +961,11 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     // INF: C = max(h, min C), d from the lexicographic minimum), while a key's label may change
     // either way.  f_q(K) >= K in (C, d), so a neighbour q whose (C, d) is below p's new (C, d)
     // can neither take a lower key through p nor have had p as its argmin (that needs (C, d)_q
-    // >= (C, d)_p); q's read may be stale, and a stale (C, d) is only larger.  Equal (C, d) is
-    // queued: with d capped (kDMax) a plateau's voxels share (C, 1), and a label change of p
-    // must reach the voxels that took their label from p.  sdir[d]: changed voxels whose
-    // neighbour in direction d (-z, +z, -y, +y, -x, +x) must be re-evaluated
+    // > (C, d)_p); q's read may be stale, and a stale (C, d) is only larger.  (Comparing whole
+    // keys would not do: a label change can raise p's key, and the voxels that took their label
+    // from p must see it.)  Equal (C, d) is queued too (only d's saturation at kDMax makes it
+    // possible).  sdir[d]: changed voxels whose neighbour in direction d (-z, +z, -y, +y, -x,
+    // +x) must be re-evaluated
     constexpr int NDIR = ND == 3 ? 6 : 4;
     __shared__ uint64_t sdir[kFrontierWaves][6][64];
     __shared__ uint64_t sfw[kFrontierWaves][64];

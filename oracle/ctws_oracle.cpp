@@ -442,9 +442,10 @@ struct PQCompare {
 // ---------------------------------------------------------------------------------------
 int g_flood_model = 0;
 // tie orders for the tie-order experiment (scripts/tie_order_experiment.py): the GPU's
-// order is 6 (kDMax = 1 in cluster_tools_amd/csrc/ctws_dev.h; order 1 was rounds 1-3's).  2: (C, label), no hop distance; 3: (C, d, -label); 4: (C, d, push count) = FIFO
+// order is 1 (kDMax = 4095 in cluster_tools_amd/csrc/ctws_dev.h).  Orders 2 and 6 have no
+// unique fixpoint (equal keys along plateau paths), so no parallel relaxation can promise them.  2: (C, label), no hop distance; 3: (C, d, -label); 4: (C, d, push count) = FIFO
 // inside an equal-(C, d) front; 5: (C, push count) = FIFO on a plateau; 6: (C, min(d, 1), label)
-int g_tie_order = 6;
+int g_tie_order = 1;
 
 inline uint32_t ordf(float f) {
     uint32_t u;

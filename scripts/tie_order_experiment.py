@@ -7,13 +7,15 @@ vigra's watershedsNew pops a std::priority_queue keyed by priority alone, so equ
 (oracle/ctws_oracle.cpp:watersheds_new).  The GPU's flood computes the unique fixpoint of one
 total order (k_flood.hip: C, then the hop distance d inside an equal-C plateau, then the label);
 oracle watersheds_model restates it.  Orders compared (oracle g_tie_order):
-  1 (C, d, label)  -- the GPU's in rounds 1-3 (d saturating at 4095)
+  1 (C, d, label)  -- the GPU's (d saturating at 4095)
   2 (C, label)     -- no hop distance
   3 (C, d, -label)
   4 (C, d, push count): FIFO inside an equal-(C, d) front
   5 (C, push count):    FIFO on a plateau
-  6 (C, min(d, 1), label): the hop distance reduced to "entered at its own height or not" --
-                           the GPU's since round 4 (the closest to the heap overall)
+  6 (C, min(d, 1), label): the hop distance reduced to "entered at its own height or not"
+Orders 2 and 6 are closest to the heap on the tie-dominated inputs, but (C, d) no longer strictly
+increases along parent edges: the fixpoint is not unique (a cycle of equal-key plateau voxels
+can keep a stale label) and the GPU's relaxation reached another one (round 4) -- not adopted.
 Only orders of the form (C, d?, label-ish) are fixpoints a parallel relaxation can reach; 4 and 5
 are sequential references for how close an insertion-ordered queue gets.
 Output: VI(order, heap) per case, JSON on stdout."""
@@ -53,7 +55,7 @@ def main():
             with O.flood_model():
                 m = run()
             row[order] = round(float(sum(vi_scores(m, heap, ign))), 4)
-        L.orc_set_tie_order(6)
+        L.orc_set_tie_order(1)
         out['%s:%s' % (kind, name)] = row
         print(name, row, file=sys.stderr, flush=True)
     print(json.dumps(out, indent=1))
