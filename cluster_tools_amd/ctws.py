@@ -372,4 +372,35 @@ class Handle:
                     'ctws_lookup_u64')
         return int(miss.value)
 
+    def unique_u64_device(self, labels):
+        """np.unique of a uint64 (or int64) torch tensor on this GPU: the sorted uniques as a
+        numpy uint64 array (the labels stay in HBM; only the uniques cross PCIe)."""
+        import torch
+        assert labels.is_cuda and labels.is_contiguous() and labels.element_size() == 8
+        torch.cuda.current_stream(labels.device).synchronize()
+        n = C.c_int64(0)
+        cap = 1024
+        while True:
+            out = torch.empty(cap, dtype=torch.int64, device=labels.device)
+            ret = lib().ctws_unique_u64(self._h, labels.data_ptr(), labels.numel(), 1, out.data_ptr(), cap,
+                                        C.byref(n))
+            if ret == -1 and n.value > cap:
+                cap = n.value
+                continue
+            self._check(ret, 'ctws_unique_u64')
+            return out[:n.value].cpu().numpy().view(np.uint64)
+
+    def lookup_u64_device(self, labels, keys, values):
+        """lookup_u64 on a uint64 / int64 torch tensor on this GPU (in place) with a numpy
+        table; returns the number of labels absent from it."""
+        import torch
+        assert labels.is_cuda and labels.is_contiguous() and labels.element_size() == 8
+        kd = torch.from_numpy(np.ascontiguousarray(keys, dtype=np.uint64).view(np.int64)).to(labels.device)
+        vd = torch.from_numpy(np.ascontiguousarray(values, dtype=np.uint64).view(np.int64)).to(labels.device)
+        torch.cuda.current_stream(labels.device).synchronize()
+        miss = C.c_int64(0)
+        self._check(lib().ctws_lookup_u64(self._h, labels.data_ptr(), labels.numel(), 1, kd.data_ptr(), vd.data_ptr(),
+                                          kd.numel(), C.byref(miss)), 'ctws_lookup_u64')
+        return int(miss.value)
+
     # ---- multi-GPU label-count exchange (RCCL) ------------------------------------------

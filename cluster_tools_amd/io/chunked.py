@@ -12,17 +12,19 @@ module implements the two on-disk formats directly:
 * zarr v2: ``.zarray`` / ``.zattrs`` / ``.zgroup`` JSON; chunk files ``<ds>/i.j.k`` holding the
   full (padded) chunk in C order, gzip- or zlib-compressed or raw.
 
-Chunk (de)compression runs on a thread pool of ``n_threads`` (zlib releases the GIL).
+Chunk (de)compression (libdeflate through ctypes, zlib as the fallback: deflate.py) runs on a
+thread pool of ``n_threads`` (both release the GIL).
 """
 import json
 import os
 import threading
-import zlib
 from collections import OrderedDict
 from concurrent import futures
 from itertools import product
 
 import numpy as np
+
+from cluster_tools_amd.io import deflate
 
 _N5_DTYPES = {'uint8': 'uint8', 'uint16': 'uint16', 'uint32': 'uint32', 'uint64': 'uint64',
               'int8': 'int8', 'int16': 'int16', 'int32': 'int32', 'int64': 'int64',
@@ -51,19 +53,22 @@ def _normalize_index(index, shape):
     return tuple(out), squeeze
 
 
-def _compress(data, compression, level=5):
-    if compression == 'gzip':
-        c = zlib.compressobj(level, zlib.DEFLATED, 31)
-        return c.compress(data) + c.flush()
-    if compression == 'zlib':
-        return zlib.compress(data, level)
-    return data
-
-
-def _decompress(data, compression):
+def _compress(arr, compression, level=5):
+    """The chunk file payload of the C-contiguous array `arr` (bytes)."""
     if compression in ('gzip', 'zlib'):
-        return zlib.decompress(data, 47)  # auto-detect gzip / zlib header
-    return data
+        return deflate.deflate(arr, compression, level)
+    return arr.tobytes()
+
+
+def _decompress(data, compression, nbytes):
+    """The decompressed payload as a uint8 array of `nbytes` (gzip / zlib header detected)."""
+    if compression in ('gzip', 'zlib'):
+        out = deflate.inflate(data, nbytes)
+    else:
+        out = np.frombuffer(data, np.uint8)
+    if out.size != nbytes:
+        raise ValueError("chunk holds %i bytes, expected %i" % (out.size, nbytes))
+    return out
 
 
 def _dump_json(path, obj):
@@ -127,6 +132,8 @@ class Dataset:
             self.dtype = np.dtype(meta['dataType'])
             comp = meta.get('compression', {'type': 'raw'})
             self.compression = comp.get('type', 'raw') if isinstance(comp, dict) else 'raw'
+            if self.compression == 'gzip' and comp.get('useZlib'):
+                self.compression = 'zlib'  # n5 "gzip" with the zlib wrapper
             self._fill = 0
         else:
             with open(os.path.join(path, '.zarray')) as f:
@@ -194,11 +201,15 @@ class Dataset:
             mode, nd = np.frombuffer(raw[:4], dtype='>u2')
             assert mode == 0, "varlength n5 chunks are not supported"
             cshape = tuple(np.frombuffer(raw[4:4 + 4 * nd], dtype='>u4')[::-1].astype(int))
-            data = _decompress(raw[4 + 4 * nd:], self.compression)
-            arr = np.frombuffer(data, dtype=self.dtype.newbyteorder('>')).reshape(cshape)
-            return arr.astype(self.dtype)
-        data = _decompress(raw, self.compression)
-        arr = np.frombuffer(data, dtype=self.dtype).reshape(self.chunks)
+            data = _decompress(raw[4 + 4 * nd:], self.compression,
+                               int(np.prod(cshape)) * self.dtype.itemsize)
+            arr = data.view(self.dtype.newbyteorder('>')).reshape(cshape)
+            if not arr.flags.writeable:
+                return arr.astype(self.dtype)
+            # big-endian -> native in place (the inflated buffer is ours)
+            return arr.byteswap(inplace=True).view(self.dtype)
+        data = _decompress(raw, self.compression, int(np.prod(self.chunks)) * self.dtype.itemsize)
+        arr = data.view(self.dtype).reshape(self.chunks)
         return arr[tuple(slice(0, e - b) for b, e in zip(beg, end))]
 
     def write_chunk(self, cid, arr):
@@ -210,13 +221,12 @@ class Dataset:
         if self.fmt == 'n5':
             header = np.array([0, len(valid)], dtype='>u2').tobytes() + \
                 np.array(valid[::-1], dtype='>u4').tobytes()
-            payload = _compress(np.ascontiguousarray(arr, dtype=self.dtype.newbyteorder('>')).tobytes(),
-                                self.compression)
+            payload = _compress(np.ascontiguousarray(arr, dtype=self.dtype.newbyteorder('>')), self.compression)
             data = header + payload
         else:
             full = np.full(self.chunks, self._fill, dtype=self.dtype)
             full[tuple(slice(0, v) for v in valid)] = arr
-            data = _compress(full.tobytes(), self.compression)
+            data = _compress(full, self.compression)
         tmp = p + '.tmp%d' % os.getpid()
         with open(tmp, 'wb') as f:
             f.write(data)

@@ -64,9 +64,10 @@ def block_table(uniques, offset, dup):
 
 
 def write_blocks(ds_out, written, log, n_threads=None):
-    """ds_out[bb] = labels for every (block_id, bb, labels): the chunks of all blocks through one
-    pool (a block's chunks alone are too few to keep the job's threads busy); "processed block"
-    after each block's last chunk, in block order."""
+    """ds_out[bb] = labels for every (block_id, bb, labels) of the iterable `written`: the chunks
+    of all blocks through one pool (a block's chunks alone are too few to keep the job's threads
+    busy), each block submitted as soon as the iterable yields it; "processed block" after each
+    block's last chunk, in block order."""
     from concurrent import futures
     n_threads = n_threads or max(4, getattr(ds_out, 'n_threads', 1))
     single = getattr(ds_out, 'n_threads', 1)
@@ -120,8 +121,10 @@ def relabel_in_job(job_id, results, ds_out, tmp_folder, assignment_path, assignm
     """The exchange, then the job's blocks written with their final ids.
 
     results: [(block_id, output_bb, labels or None (skipped: nothing written), uniques)] of this
-    job.  mapper(labels, keys, values) maps a block in place (ctws lookup on the GPU).  A job
-    whose blocks failed still joins (failed=True) so that every job raises instead of waiting."""
+    job; labels may be a numpy array or a tensor resident on the GPU.  mapper(labels, keys,
+    values) returns the block with its final ids as a numpy uint64 array (ctws lookup on the GPU;
+    an empty table leaves the labels as they are).  A job whose blocks failed still joins
+    (failed=True) so that every job raises instead of waiting."""
     import torch.distributed as dist
     from cluster_tools_amd.utils import volume_utils as vu
     comm_dev = device if dist.get_backend() == 'nccl' else None
@@ -134,19 +137,20 @@ def relabel_in_job(job_id, results, ds_out, tmp_folder, assignment_path, assignm
     offs, n_new = scan(rows_all)
     has_zero = bool(flags[:, 4].any() or rows_all[:, 4].any())
     log("global ids: %i (offset scan over %i blocks)" % (n_new, len(rows_all)))
-    # map every block (GPU lookup), then write them all through one pool of chunk writers
-    written, tables = [], {}
-    for bid, bb, lab, u in results:
-        if lab is None:
-            continue
-        off, dup = offs[bid]
-        keys, vals = block_table(u, off, dup)
-        if len(keys):
-            mapper(lab, keys, vals)
-        # (a duplicated first id keeps the previous block's row in the table)
-        tables[bid] = (keys[dup:], vals[dup:])
-        written.append((bid, bb, lab))
-    write_blocks(ds_out, written, log)
+    # map the blocks one by one (GPU lookup) while the chunk writers compress the ones before
+    tables = {}
+
+    def mapped():
+        for bid, bb, lab, u in results:
+            if lab is None:
+                continue
+            off, dup = offs[bid]
+            keys, vals = block_table(u, off, dup)
+            # (a duplicated first id keeps the previous block's row in the table)
+            tables[bid] = (keys[dup:], vals[dup:])
+            yield bid, bb, mapper(lab, keys, vals)
+
+    write_blocks(ds_out, mapped(), log)
     # this job's table rows in block order, with each block's row count
     bids = sorted(tables)
     np.save(rows_file(tmp_folder, job_id), np.stack([

@@ -224,6 +224,9 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
 
     keep (a list; pass 0): nothing is written -- each block's (block_id, output_bb, labels or None
     for a skipped block, uniques) is appended instead, for the in-job relabel (job_relabel.py).
+    The labels then stay in HBM (torch tensors) when the job's outputs fit in half the free
+    device memory (config 'keep_on_device', default on): the relabel maps them there and each
+    block crosses PCIe once, with its final ids.
     """
     from cluster_tools_amd import ctws
     block_shape = list(config['block_shape'])
@@ -263,6 +266,7 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
             fu.log_block_success(b['block_id'])
 
     with ctws.Handle(_device()) as h, futures.ThreadPoolExecutor(2) as io:
+        on_device = keep is not None and _keep_on_device(blocking, block_list, config)
         nxt = io.submit(read_batch, batches[0]) if batches else None
         pending_write = None
         for bi in range(len(batches)):
@@ -273,11 +277,17 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
             for b in blocks:
                 fu.log("start processing block %i" % b['block_id'])
             todo = [b for b in blocks if not b.get('skip')]
-            res = h.ws_blocks(lib_config, block_shape, todo, pass_id=pass_id) if todo else []
+            if not todo:
+                res = []
+            elif on_device:
+                res = _ws_blocks_resident(h, lib_config, block_shape, todo)
+            else:
+                res = h.ws_blocks(lib_config, block_shape, todo, pass_id=pass_id)
             error = h.last_error()
             by_id = {b['block_id']: r for b, r in zip(todo, res)}
             results = [by_id.get(b['block_id']) for b in blocks]
-            uniques = [h.unique_u64(r['output']) if (uniques_path or keep is not None) and r is not None
+            uniq = h.unique_u64_device if on_device else h.unique_u64
+            uniques = [uniq(r['output']) if (uniques_path or keep is not None) and r is not None
                        and r['status'] in (0, 2) else None for r in results]
             if pending_write is not None:
                 pending_write.result()
@@ -289,6 +299,36 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
                 nxt = io.submit(read_batch, batches[bi + 1]) if bi + 1 < len(batches) else None
         if pending_write is not None:
             pending_write.result()
+
+
+def _keep_on_device(blocking, block_list, config):
+    """Whether the job's uint64 outputs fit in half the free memory of its GPU."""
+    if not config.get('keep_on_device', True):
+        return False
+    import torch
+    need = 0
+    for bid in block_list:
+        _, inner_bb, _ = _get_bbs(blocking, bid, config)
+        need += 8 * int(np.prod([s.stop - s.start for s in inner_bb]))
+    free, _ = torch.cuda.mem_get_info(_device())
+    return need <= free // 2
+
+
+def _ws_blocks_resident(h, lib_config, block_shape, todo):
+    """Pass-0 blocks through ctws_ws_blocks_device: the inputs uploaded, the outputs left in HBM
+    as int64 tensors (uint64 bits) -> [{'output': tensor, 'status', 'max_label', 'n_ids'}]."""
+    import torch
+    dev = torch.device('cuda', _device())
+    dblocks = []
+    for b in todo:
+        db = {'block_id': b['block_id'], 'inner_begin': b['inner_begin'], 'crop_relabel': b['crop_relabel'],
+              'input': torch.from_numpy(np.ascontiguousarray(b['input'])).to(dev),
+              'output': torch.empty(tuple(b['inner_shape']), dtype=torch.int64, device=dev)}
+        if b.get('mask') is not None:
+            db['mask'] = torch.from_numpy(np.ascontiguousarray(b['mask'], dtype=np.uint8)).to(dev)
+        dblocks.append(db)
+    st = h.ws_blocks_device(lib_config, block_shape, dblocks, pass_id=0)
+    return [{'output': db['output'], 'status': s, 'max_label': m, 'n_ids': n} for db, (s, m, n) in zip(dblocks, st)]
 
 
 def run_job(job_id, config_path, pass_id=None):
@@ -333,9 +373,16 @@ def _run_blocks_relabel(job_id, blocking, ds_in, ds_out, mask, config, rel):
             failed = e
         if failed is None:
             with ctws.Handle(_device()) as h:
+                def mapper(lab, keys, vals):
+                    if hasattr(lab, 'data_ptr'):   # resident in HBM: map there, then download
+                        if len(keys):
+                            h.lookup_u64_device(lab, keys, vals)
+                        return lab.cpu().numpy().view(np.uint64)
+                    if len(keys):
+                        h.lookup_u64(lab, keys, vals)
+                    return lab
                 job_relabel.relabel_in_job(job_id, keep, ds_out, rel['tmp_folder'], rel['assignment_path'],
-                                           rel['assignment_key'], lambda lab, k, v: h.lookup_u64(lab, k, v),
-                                           log=fu.log, device=_device())
+                                           rel['assignment_key'], mapper, log=fu.log, device=_device())
         else:
             job_relabel.relabel_in_job(job_id, [], ds_out, rel['tmp_folder'], rel['assignment_path'],
                                        rel['assignment_key'], None, failed=True, log=fu.log, device=_device())

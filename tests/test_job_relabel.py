@@ -75,7 +75,9 @@ def _worker(rank, world, port, root):
 
         def mapper(lab, keys, vals):
             nz = lab != 0
-            lab[nz] = vals[np.searchsorted(keys, lab[nz])]
+            if len(keys):
+                lab[nz] = vals[np.searchsorted(keys, lab[nz])]
+            return lab
 
         with vu.file_reader(os.path.join(root, 'ws.n5')) as f:
             ds = f['ws']

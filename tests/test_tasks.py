@@ -95,6 +95,38 @@ def test_n5_layout_is_standard(tmp_path):
     assert np.array_equal(data, np.arange(60))
 
 
+@pytest.mark.parametrize('codec', ['libdeflate', 'zlib'])
+@pytest.mark.parametrize('ext,comp', [('n5', 'gzip'), ('n5', 'zlib'), ('zr', 'gzip'), ('zr', 'zlib'), ('n5', 'raw')])
+def test_chunk_codecs_interoperate(tmp_path, monkeypatch, codec, ext, comp):
+    """Chunks written with either codec (libdeflate, or zlib when it is absent) read back with
+    the other and with Python's zlib / gzip; float chunks come back native-endian."""
+    import zlib
+    from cluster_tools_amd.io import deflate
+    if codec == 'libdeflate' and not deflate.available():
+        pytest.skip('libdeflate.so.0 not installed')
+    if codec == 'zlib':
+        monkeypatch.setattr(deflate, '_lib', False)
+    path = str(tmp_path / ('d.' + ext))
+    rng = np.random.RandomState(1)
+    x = rng.rand(19, 33, 21).astype('float32')
+    lab = (np.arange(19 * 33 * 21, dtype='uint64') // 50 + (1 << 40)).reshape(19, 33, 21)
+    with vu.file_reader(path) as f:
+        f.create_dataset('x', shape=x.shape, chunks=(8, 16, 16), dtype='float32', compression=comp)[:] = x
+        f.create_dataset('l', shape=x.shape, chunks=(8, 16, 16), dtype='uint64', compression=comp)[:] = lab
+    monkeypatch.setattr(deflate, '_lib', None if codec == 'zlib' else False)
+    with vu.file_reader(path, 'r') as f:
+        rx = f['x'][:]
+        assert rx.dtype == np.float32 and rx.dtype.isnative and np.array_equal(rx, x)
+        assert np.array_equal(f['l'][:], lab)
+    if comp != 'raw':
+        # every chunk file is a plain gzip / zlib stream
+        name = os.path.join(path, 'l', '0', '0', '0') if ext == 'n5' else os.path.join(path, 'l', '0.0.0')
+        raw = open(name, 'rb').read()
+        payload = raw[16:] if ext == 'n5' else raw
+        assert (payload[:2] == b'\x1f\x8b') == (comp == 'gzip')
+        zlib.decompress(payload, 47)
+
+
 def test_tail(tmp_path):
     p = tmp_path / 'out.txt'
     p.write_text('abcd\n1234\n5678\nwxyz\n')
