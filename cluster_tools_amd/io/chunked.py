@@ -244,23 +244,34 @@ class Dataset:
         return [fn(i) for i in items]
 
     def __getitem__(self, index):
-        bb, squeeze = _normalize_index(index, self.shape)
-        out = np.full(tuple(s.stop - s.start for s in bb), self._fill, dtype=self.dtype)
+        return self.read_many([index])[0]
+
+    def read_many(self, indices):
+        """[self[i] for i in indices], with the chunks of all of them read and inflated by one
+        pool (each chunk once, copied into every array that overlaps it): a batch of blocks
+        keeps n_threads busy where a block with few chunks of its own would not."""
+        bbs = [_normalize_index(i, self.shape) for i in indices]
+        # every voxel is written below: from its chunk, or the fill value where none is stored
+        outs = [np.empty(tuple(s.stop - s.start for s in bb), dtype=self.dtype) for bb, _ in bbs]
+        users = OrderedDict()
+        for k, (bb, _) in enumerate(bbs):
+            for cid in self._chunk_ids(bb):
+                users.setdefault(cid, []).append(k)
 
         def load(cid):
             data = self.read_chunk(cid)
-            if data is None:
-                return
             beg, end = self._chunk_bb(cid)
-            src, dst = [], []
-            for s, b, e in zip(bb, beg, end):
-                lo, hi = max(s.start, b), min(s.stop, e)
-                src.append(slice(lo - b, hi - b))
-                dst.append(slice(lo - s.start, hi - s.start))
-            out[tuple(dst)] = data[tuple(src)]
+            for k in users[cid]:
+                bb = bbs[k][0]
+                src, dst = [], []
+                for s, b, e in zip(bb, beg, end):
+                    lo, hi = max(s.start, b), min(s.stop, e)
+                    src.append(slice(lo - b, hi - b))
+                    dst.append(slice(lo - s.start, hi - s.start))
+                outs[k][tuple(dst)] = self._fill if data is None else data[tuple(src)]
 
-        self._map(load, self._chunk_ids(bb))
-        return out.squeeze(axis=squeeze) if squeeze else out
+        self._map(load, list(users))
+        return [o.squeeze(axis=sq) if sq else o for o, (_, sq) in zip(outs, bbs)]
 
     def __setitem__(self, index, value):
         bb, _ = _normalize_index(index, self.shape)

@@ -9,6 +9,7 @@ keeps the dataset I/O, the outer/inner bounding boxes (_get_bbs, :252-264) and t
 "processed block"/"processed job" log protocol.  Input reads of the next batch and output
 writes of the previous one overlap the GPU work of the current batch.
 """
+import contextlib
 import json
 import os
 import shutil
@@ -144,8 +145,9 @@ def _get_bbs(blocking, block_id, config):
     return input_bb, inner_bb, output_bb
 
 
-def _read_block(blocking, block_id, ds_in, ds_out, mask, config, pass_id):
-    """Everything `_ws_block` reads for one block (watershed.py:287-303), as a libctws block."""
+def _read_block(blocking, block_id, ds_in, ds_out, mask, config, pass_id, read_input=True):
+    """Everything `_ws_block` reads for one block (watershed.py:287-303), as a libctws block
+    (read_input=False: the input's index in 'input_index' instead, for a batched read)."""
     input_bb, inner_bb, output_bb = _get_bbs(blocking, block_id, config)
     b = {'block_id': block_id, 'output_bb': output_bb, 'crop_relabel': output_bb != input_bb,
          'inner_begin': [s.start for s in inner_bb], 'inner_shape': [s.stop - s.start for s in inner_bb]}
@@ -157,9 +159,13 @@ def _read_block(blocking, block_id, ds_in, ds_out, mask, config, pass_id):
         b['mask'] = in_mask.view('uint8')
     if ds_in.ndim == 4:
         cb, ce = config.get('channel_begin', 0), config.get('channel_end', None)
-        b['input'] = ds_in[(slice(cb, ce),) + input_bb]
+        index = (slice(cb, ce),) + input_bb
     else:
-        b['input'] = ds_in[input_bb]
+        index = input_bb
+    if read_input:
+        b['input'] = ds_in[index]
+    else:
+        b['input_index'] = index
     if pass_id == 1:
         b['initial_seeds'] = ds_out[input_bb]
     return b
@@ -236,7 +242,8 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
         lib_config['channel_begin'], lib_config['channel_end'] = 0, None
     if config.get('non_maximum_suppression', True if pass_id == 1 else False):
         fu.log("non-maximum suppression was activated, but is not available")
-    batch_blocks = batch_blocks or int(config.get('gpu_batch_blocks', 16))
+    # keep (in-job relabel): small batches, so that the GPU runs a batch while the next is read
+    batch_blocks = batch_blocks or int(config.get('gpu_batch_blocks') or (4 if keep is not None else 16))
     batches = make_batches(blocking, block_list, config, pass_id, batch_blocks)
     n_io = max(1, int(config.get('threads_per_job', 1)))
     ds_in.n_threads = ds_out.n_threads = max(n_io, 4)
@@ -245,7 +252,14 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
         ds_in.cache_bytes = int(float(config.get('read_cache_gb', 2.0)) * (1 << 30))
 
     def read_batch(ids):
-        return [_read_block(blocking, bid, ds_in, ds_out, mask, config, pass_id) for bid in ids]
+        batched = hasattr(ds_in, 'read_many')
+        blocks = [_read_block(blocking, bid, ds_in, ds_out, mask, config, pass_id, read_input=not batched)
+                  for bid in ids]
+        if batched:
+            need = [b for b in blocks if 'input_index' in b]
+            for b, x in zip(need, ds_in.read_many([b.pop('input_index') for b in need])):
+                b['input'] = x
+        return blocks
 
     uniques_path = config.get('uniques_path')
 
@@ -265,9 +279,11 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
                 np.save(block_uniques_file(uniques_path, b['block_id']), u)
             fu.log_block_success(b['block_id'])
 
-    with ctws.Handle(_device()) as h, futures.ThreadPoolExecutor(2) as io:
-        on_device = keep is not None and _keep_on_device(blocking, block_list, config)
+    with futures.ThreadPoolExecutor(2) as io, contextlib.ExitStack() as stack:
+        # the first read overlaps the HIP (and torch) start-up
         nxt = io.submit(read_batch, batches[0]) if batches else None
+        h = stack.enter_context(ctws.Handle(_device()))
+        on_device = keep is not None and _keep_on_device(blocking, block_list, config)
         pending_write = None
         for bi in range(len(batches)):
             blocks = nxt.result()

@@ -95,6 +95,23 @@ def test_n5_layout_is_standard(tmp_path):
     assert np.array_equal(data, np.arange(60))
 
 
+@pytest.mark.parametrize('ext', ['n5', 'zr'])
+def test_read_many_missing_chunks_and_overlaps(tmp_path, ext):
+    """read_many: overlapping indices share chunks; chunks never written read as the fill."""
+    path = str(tmp_path / ('d.' + ext))
+    x = np.arange(20 * 30 * 40, dtype='float32').reshape(20, 30, 40)
+    with vu.file_reader(path) as f:
+        ds = f.create_dataset('x', shape=x.shape, chunks=(8, 8, 8), dtype='float32', compression='gzip')
+        ds[0:8, :, :] = x[0:8]
+        ds.n_threads = 3
+        idx = [np.s_[2:19, 3:29, 5:33], np.s_[0:20, 0:30, 0:40], np.s_[7:9, 4, 1:39], np.s_[:, :, :]]
+        got = ds.read_many(idx)
+    exp = np.zeros_like(x)
+    exp[0:8] = x[0:8]
+    for i, g in zip(idx, got):
+        assert np.array_equal(g, exp[i])
+
+
 @pytest.mark.parametrize('codec', ['libdeflate', 'zlib'])
 @pytest.mark.parametrize('ext,comp', [('n5', 'gzip'), ('n5', 'zlib'), ('zr', 'gzip'), ('zr', 'zlib'), ('n5', 'raw')])
 def test_chunk_codecs_interoperate(tmp_path, monkeypatch, codec, ext, comp):
