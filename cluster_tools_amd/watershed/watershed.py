@@ -217,7 +217,8 @@ def make_batches(blocking, block_list, config, pass_id, batch_blocks):
     return [list(block_list[k:k + batch_blocks]) for k in range(0, len(block_list), batch_blocks)]
 
 
-def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, batch_blocks=None, keep=None):
+def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, batch_blocks=None, keep=None,
+               started=None):
     """Run `_ws_block` (pass 0) or `_ws_pass2` (pass 1) for `block_list` on the GPU.
 
     Blocks are processed in batches with the same results as the reference's sequential loop:
@@ -233,6 +234,9 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
     The labels then stay in HBM (torch tensors) when the job's outputs fit in half the free
     device memory (config 'keep_on_device', default on): the relabel maps them there and each
     block crosses PCIe once, with its final ids.
+
+    started: called once the first batch's read is under way (the in-job relabel's process
+    group starts there, so that torch's import overlaps the read).
     """
     from cluster_tools_amd import ctws
     block_shape = list(config['block_shape'])
@@ -282,6 +286,8 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
     with futures.ThreadPoolExecutor(2) as io, contextlib.ExitStack() as stack:
         # the first read overlaps the HIP (and torch) start-up
         nxt = io.submit(read_batch, batches[0]) if batches else None
+        if started is not None:
+            started()
         h = stack.enter_context(ctws.Handle(_device()))
         on_device = keep is not None and _keep_on_device(blocking, block_list, config)
         pending_write = None
@@ -372,21 +378,28 @@ def run_job(job_id, config_path, pass_id=None):
 def _run_blocks_relabel(job_id, blocking, ds_in, ds_out, mask, config, rel):
     """The job's blocks, then the in-job relabel over the jobs' process group (job_relabel.py):
     the job writes its blocks with the final ids; job 0 writes the assignment table and maxId."""
-    import torch.distributed as dist
     from cluster_tools_amd import ctws
     from cluster_tools_amd.watershed import job_relabel
-    # the group first: all jobs start together, so the rendezvous is immediate; a job that dies
-    # later breaks its peers' pending collective (gloo / RCCL report the lost peer) instead of
-    # leaving them waiting out the timeout
-    job_relabel.init_group(job_id, rel['n_jobs'], rel['port'], rel['backend'], device=_device())
+    # the group as soon as the first read is under way: all jobs start together, so the
+    # rendezvous is immediate; a job that dies later breaks its peers' pending collective (gloo /
+    # RCCL report the lost peer) instead of leaving them waiting out the timeout
+    group = []
+
+    def start_group():
+        job_relabel.init_group(job_id, rel['n_jobs'], rel['port'], rel['backend'], device=_device())
+        group.append(True)
+
     keep, failed = [], None
     try:
         try:
-            run_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, pass_id=0, keep=keep)
+            run_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, pass_id=0, keep=keep,
+                       started=start_group)
         except Exception as e:  # still take part in the exchange: every job then raises
             import traceback
             traceback.print_exc()
             failed = e
+        if not group:   # (run_blocks failed before its first read)
+            start_group()
         if failed is None:
             with ctws.Handle(_device()) as h:
                 def mapper(lab, keys, vals):
@@ -403,7 +416,9 @@ def _run_blocks_relabel(job_id, blocking, ds_in, ds_out, mask, config, rel):
             job_relabel.relabel_in_job(job_id, [], ds_out, rel['tmp_folder'], rel['assignment_path'],
                                        rel['assignment_key'], None, failed=True, log=fu.log, device=_device())
     finally:
-        dist.destroy_process_group()
+        if group:
+            import torch.distributed as dist
+            dist.destroy_process_group()
     if failed is not None:
         raise failed
 
