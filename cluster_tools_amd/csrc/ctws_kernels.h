@@ -154,6 +154,7 @@ __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64
 template <int ND>
 __global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
                                const uint64_t*, uint32_t*);
+template <int U>
 __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint8_t*,
                                uint64_t*, uint64_t*, uint32_t*, uint32_t*);
 template <int ND, int CW, int CY, int CZ>
@@ -207,6 +208,7 @@ __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*,
 template <int PACKED>
 __global__ void k_hist2d(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
                          uint32_t*, int);
+template <int U>
 __global__ void k_regrow_init(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*, const uint8_t*,
                               const float*, uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*);
 __global__ void k_auto_minima(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*);

@@ -771,6 +771,7 @@ template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, c
 // flood (INF key).  Bitmaps, one word per 64 voxels of a row (the 64 lanes of a wave cover
 // exactly one word): open = not final yet, chg = final (the first "changed" set, whose
 // neighbours form the first frontier).
+template <int U>
 __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint32_t* __restrict__ par,
                                                       uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
@@ -785,7 +786,6 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
     uint32_t lev = 0;
     // word tiles (a wave's ballot is exactly one word of the open / changed bitmaps), U words
     // per step: the U chains of a lane hop together, so U dependent-load latencies overlap
-    constexpr int U = 4;
     const int wpr = (B.X + 63) >> 6;
     const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
     const int lane = threadIdx.x & 63;
@@ -847,6 +847,8 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
         if (threadIdx.x == 0 && lev) atomic_max_if(&plev[blockIdx.y], lev);
     }
 }
+template __global__ void k_descent_init<8>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
+                                           uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*, uint32_t*);
 
 // One iteration of the frontier relaxation.  frontier = (neighbours of the voxels changed in
 // the previous iteration) & open; every frontier voxel recomputes K = f(min of its

@@ -174,6 +174,7 @@ __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D,
 // reset.  The open bitmap gets the removed voxels and the changed bitmap the survivors, so
 // the first frontier is exactly the removed voxels next to a survivor (k_frontier, k_flood.hip).
 // survivors[slice (2-D) / 0 (3-D)] = 1 if any label survives there.
+template <int U>
 __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                      uint32_t size_filter, const uint32_t* __restrict__ counts,
                                                      const uint8_t* __restrict__ excl, const float* __restrict__ h,
@@ -185,7 +186,6 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
     constexpr uint64_t kLab = (1ull << 20) - 1ull;
     // word tiles (a wave's ballot is exactly one word of the open / changed bitmaps), U words per
     // step: the loads of the U words, then their dependent count loads, in flight together
-    constexpr int U = 4;
     const int wpr = (B.X + 63) >> 6;
     const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
     const int lane = threadIdx.x & 63;
@@ -255,6 +255,9 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
         }
     }
 }
+template __global__ void k_regrow_init<4>(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*,
+                                          const uint8_t*, const float*, uint64_t*, uint8_t*, uint64_t*, uint64_t*,
+                                          uint32_t*);
 
 // Auto-seeded regrow: a slice (2-D) / block (3-D) whose every segment was removed leaves
 // watershedsNew an all-zero seed image, and vigra then seeds from the strict local minima of
