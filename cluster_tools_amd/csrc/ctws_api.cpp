@@ -1205,7 +1205,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         HIPCHK(hipMemsetAsync(w.fseed, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
         CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed};
         if (pl.nd_ws == 3) {
-            using T = CcTile<3>;
+            using T = CcTileM<3, CC_SEED>;  // (= the plateau tile)
             const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
             k_tile_cc<3, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_tile_merge<3, CC_PLATEAU><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);

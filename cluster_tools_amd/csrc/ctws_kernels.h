@@ -133,6 +133,17 @@ template <>
 struct CcTile<2> {
     static constexpr int TZ = 1, TY = 32, TX = 64;
 };
+// the tile of one CC mode: 3-D plateau / seed CC in 8-deep tiles (half the z faces of
+// k_tile_merge: config 4's seeds stage 11.98 -> 11.29 ms); the crop CC keeps 4-deep tiles
+// (its k_tile_cc at 8 deep: 5.6 -> 7.7 ms per step, more than the merge saves)
+template <int ND, int MODE>
+struct CcTileM : CcTile<ND> {};
+template <>
+struct CcTileM<3, CC_PLATEAU> {
+    static constexpr int TZ = 8, TY = 16, TX = 32;
+};
+template <>
+struct CcTileM<3, CC_SEED> : CcTileM<3, CC_PLATEAU> {};
 template <int ND, int MODE>
 __global__ void k_tile_cc(const BlockDesc*, const BlockStat*, CcArgs, uint32_t*);
 template <int ND>

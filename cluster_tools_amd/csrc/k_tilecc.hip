@@ -10,7 +10,7 @@
 //
 // A global union-find over every voxel (one atomicCAS chain per neighbour pair through HBM)
 // costs ~100x a streaming pass on large components.  Here a workgroup first solves its tile
-// (3-D: 4x16x32, 2-D: 1x32x64) completely in LDS: parents are tile-local positions and a
+// (CcTileM: 3-D 8x16x32, crop 4x16x32; 2-D 1x32x64) completely in LDS: parents are tile-local positions and a
 // union links the root with the larger *order key* under the smaller (atomicCAS in LDS), so
 // every tile component is rooted at its smallest key.  For SEED/CROP the order key is the local F-order index
 // (x most significant, then y, then z — vigra scan order, A.0), so the tile root is the
@@ -126,7 +126,7 @@ __device__ __forceinline__ void domain_dims(const BlockDesc& B, int& nz, int& ny
 template <int ND, int MODE>
 __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D, const BlockStat* S, CcArgs a,
                                                  uint32_t* __restrict__ Pg) {
-    using T = CcTile<ND>;
+    using T = CcTileM<ND, MODE>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, TN = TZ * TY * TX, PER = TN / 256;
     static_assert(TN % 256 == 0, "");
     __shared__ uint32_t sv[TN];  // values, C-layout c = (lz * TY + ly) * TX + lx
@@ -299,7 +299,7 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
 template <int ND, int MODE>
 __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict__ D, const BlockStat* S, CcArgs a,
                                                     uint32_t* __restrict__ Pg) {
-    using T = CcTile<ND>;
+    using T = CcTileM<ND, MODE>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX;
     const BlockDesc& B = D[blockIdx.y];
     const BlockStat& st = S[blockIdx.y];
