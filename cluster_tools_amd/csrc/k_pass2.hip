@@ -183,16 +183,28 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
+    const int lane = threadIdx.x & 63;
     BLOCK_LOOP(i, B) {
+        // a wave holds 64 consecutive voxels (only trailing lanes can be past the block's end):
+        // keys come in runs, and the first lane of each run looks its key up for the run
         const uint64_t k = key[B.base + i];
+        const uint64_t kp = shfl_u64(k, (lane + 63) & 63);
+        const bool start = lane == 0 || kp != k;
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+        const int s0 = 63 - __builtin_clzll(__ballot(start) & upto);
+        uint32_t pos = 0u, l = 0u;
+        if (start && k != kEmptyKey) {
+            const int64_t s = hash_find(hkey + B.hbase, B.hcap, k);
+            pos = s >= 0 ? hpos[B.hbase + s] : 0u;  // s < 0 cannot happen after insert
+            l = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, pos) + 1u;
+        }
+        pos = (uint32_t)__shfl((int)pos, s0);
+        l = (uint32_t)__shfl((int)l, s0);
         if (k == kEmptyKey) {
             lab[B.base + i] = 0;
             fixedv[B.base + i] = 0;
             continue;  // key stays kEmptyKey == kInfKey
         }
-        const int64_t s = hash_find(hkey + B.hbase, B.hcap, k);
-        const uint32_t pos = s >= 0 ? hpos[B.hbase + s] : 0u;  // s < 0 cannot happen after insert
-        const uint32_t l = bitmap_rank(Wg + B.wbase, Wpg + B.wbase, pos) + 1u;
         lab[B.base + i] = l | kFixedBit;
         key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
         fixedv[B.base + i] = 1;
