@@ -293,13 +293,14 @@ def pcie_rates(dev, nbytes=1 << 30, reps=4):
     return out
 
 
-def end_to_end(cfg_id, dev, z_extent=64, max_jobs=4, threads=4):
+def end_to_end(cfg_id, dev, z_extent=None, max_jobs=4, threads=4):
     """The product path from file to file: WatershedWorkflow
-    (target 'local', GPU jobs) from an n5 gzip input to the relabelled n5 uint64 output
-    (Watershed -> FindUniques -> FindLabeling -> Write), on a z_extent x Y x X sub-volume of the
-    config (the whole config 3 volume would take minutes of gzip alone).  Run twice: with the
-    datasets gzip-compressed (n5 default, watershed.py:80-83) and uncompressed; the difference
-    is the gzip share.  The input file is written before the timed region."""
+    (target 'local', GPU jobs, the relabel inside the watershed jobs) from an n5 gzip input to the
+    relabelled n5 uint64 output with its assignment table and maxId, on the whole config volume
+    (z_extent slices of it when given, or when the temp file system cannot hold the uncompressed
+    leg: 64).  Run twice: with the datasets gzip-compressed (n5 default, watershed.py:80-83) and
+    uncompressed; the difference is the gzip share.  The input file is written before the timed
+    region."""
     import json as _json
     import shutil
     import subprocess
@@ -308,11 +309,16 @@ def end_to_end(cfg_id, dev, z_extent=64, max_jobs=4, threads=4):
     from cluster_tools_amd.synthetic import boundary_map_torch
     from cluster_tools_amd.utils import volume_utils as vu
     cfg = CONFIGS[cfg_id]
+    if z_extent is None:
+        # the raw leg holds the float32 input and the uint64 output uncompressed
+        raw_bytes = 12 * int(np.prod(cfg['shape']))
+        z_extent = cfg['shape'][0] if shutil.disk_usage(tempfile.gettempdir()).free > 3 * raw_bytes else 64
     shape = (min(z_extent, cfg['shape'][0]),) + tuple(cfg['shape'][1:])
     x = boundary_map_torch(shape, seed=cfg['seed'], device=dev, dtype=cfg.get('dtype', 'float32'),
                            pitch=cfg.get('pitch', (24, 24, 24))).cpu().numpy()
     out = {'volume': list(shape), 'block_shape': list(cfg['block_shape']), 'max_jobs': max_jobs,
-           'threads_per_job': threads, 'workflow': 'WatershedWorkflow(target=local) + RelabelWorkflow, GPU jobs'}
+           'threads_per_job': threads,
+           'workflow': 'WatershedWorkflow(target=local), GPU jobs, relabel in the jobs (relabel_in_job)'}
     root = tempfile.mkdtemp(prefix='ctws_e2e_')
     try:
         for comp in ('gzip', 'raw'):
@@ -666,7 +672,8 @@ def main():
     ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end n5 workflow run')
     ap.add_argument('--no-strong', action='store_true', help='skip the strong-scaling config 4 run')
     ap.add_argument('--strong-steps', type=int, default=3)
-    ap.add_argument('--e2e-z', type=int, default=64, help='z extent of the end-to-end sub-volume')
+    ap.add_argument('--e2e-z', type=int, default=None,
+                    help='z extent of the end-to-end volume (default: the whole config volume)')
     ap.add_argument('--cpu-cores', type=int, default=0, help='cap on the CPU baseline jobs (0: usable cores)')
     ap.add_argument('--scaling', choices=('weak', 'strong'), default='weak',
                     help='weak: every rank runs the config\'s single-GPU workload (default); strong: the '
