@@ -299,11 +299,23 @@ __device__ __forceinline__ int xcd_swizzle(int b, int n) {
         const int64_t wid_ = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) +     \
                              (threadIdx.x >> 6);                                                             \
         const int64_t wend_ = wid_ * per_ + per_ < nwords_ ? wid_ * per_ + per_ : nwords_;                   \
+        /* (row, word, z, y) advanced word by word: one 64-bit division per wave, not per word */            \
+        int64_t row_ = (wid_ * per_) / wpr;                                                                  \
+        int xw_ = (int)(wid_ * per_ - row_ * wpr);                                                           \
+        int z_ = (int)(row_ / (ny)), y_ = (int)(row_ - (int64_t)z_ * (ny));                                  \
         for (int64_t w_ = wid_ * per_; w_ < wend_; ++w_) {                                                   \
-            const int64_t row = w_ / wpr;                                                                    \
-            const int xw = (int)(w_ - row * wpr);                                                            \
-            const int z = (int)(row / (ny));                                                                 \
-            const int y = (int)(row - (int64_t)z * (ny));                                                    \
+            const int64_t row = row_;                                                                        \
+            const int xw = xw_;                                                                              \
+            const int z = z_;                                                                                \
+            const int y = y_;                                                                                \
+            if (++xw_ == wpr) {                                                                              \
+                xw_ = 0;                                                                                     \
+                ++row_;                                                                                      \
+                if (++y_ == (ny)) {                                                                          \
+                    y_ = 0;                                                                                  \
+                    ++z_;                                                                                    \
+                }                                                                                            \
+            }                                                                                                \
             const int x = xw * 64 + lane;                                                                    \
             const bool valid = x < (nx);                                                                     \
             const int64_t i = row * (nx) + x;                                                                \
@@ -312,6 +324,16 @@ __device__ __forceinline__ int xcd_swizzle(int b, int n) {
             __VA_ARGS__                                                                                      \
         }                                                                                                    \
     }
+
+// n / d for 0 <= n < 2^31, 0 < d and a quotient below 2^22, by the float reciprocal `inv` =
+// 1.0f / d and one correction (the estimate's error is about q * 2^-23, so it is off by at most
+// one): a few instructions instead of the emulated integer division's long dependent chain
+__device__ __forceinline__ int div_small(int n, int d, float inv) {
+    int q = (int)((float)n * inv);
+    const int r = n - q * d;
+    q += r < 0 ? -1 : (r >= d ? 1 : 0);
+    return q;
+}
 
 __device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
     return (uint64_t)__shfl_up((long long)v, d);

@@ -80,9 +80,11 @@ __device__ __forceinline__ void localmax_words(const BlockDesc& B, const BlockSt
     const float NEG = -__builtin_huge_valf();
     const gptr_t<float> gp = gbl(p);
     for (int64_t un = ubeg; un < uend; ++un) {
-        const int gy = (int)(un % ngy);
-        const int64_t strip = un / ngy;
-        const int xw = (int)(strip % wpr), z = (int)(strip / wpr);
+        // (32-bit unsigned division: a block has < 2^31 units; the emulated 64-bit one is long)
+        const uint32_t un32 = (uint32_t)un;
+        const int gy = (int)(un32 % (uint32_t)ngy);
+        const uint32_t strip = un32 / (uint32_t)ngy;
+        const int xw = (int)(strip % (uint32_t)wpr), z = (int)(strip / (uint32_t)wpr);
         const int y0 = gy * U;
         const int x = xw * 64 + lane;
         const int xc = min(x, X - 1);
@@ -471,6 +473,11 @@ __global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict
     const gwptr_t<uint64_t> out = gblw(B.out);
     uint32_t mx = 0;
     bool zero_in = false;
+    // a member's tile root r lies in this tile: its offset from the tile's first voxel is
+    // (lz * ny + ly) * nx + lx with lz < TZ, ly < TY, lx < TX, split by div_small
+    const uint32_t tb = (uint32_t)(((int64_t)z0 * ny + y0) * nx + x0);
+    const int plane = ny * nx;
+    const float inv_nx = 1.0f / (float)nx, inv_plane = 1.0f / (float)plane;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         if (!in[j]) continue;
@@ -479,11 +486,11 @@ __global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict
             if (root[j]) {
                 l = sl[threadIdx.x + j * 256];
             } else {
-                // member: its tile root lies in this tile
-                const uint32_t r = e[j];
-                const int rx = (int)(r % (uint32_t)nx), rr = (int)(r / (uint32_t)nx);
-                const int ry = rr % ny, rz = rr / ny;
-                l = sl[((rz - z0) * TY + (ry - y0)) * TX + (rx - x0)];
+                const int d = (int)(e[j] - tb);
+                const int lz = TZ > 1 ? div_small(d, plane, inv_plane) : 0;
+                const int rem = d - lz * plane;
+                const int ly = div_small(rem, nx, inv_nx);
+                l = sl[(lz * TY + ly) * TX + (rem - ly * nx)];
             }
         }
         const int c = threadIdx.x + j * 256;

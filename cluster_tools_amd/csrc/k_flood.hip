@@ -793,6 +793,8 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
     const int64_t per = (nwords + nwaves - 1) / nwaves;
     const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    // (row, word in the row) of the wave's next word, advanced word by word (no 64-bit division)
+    int row_n = (int)(wbeg / wpr), xw_n = (int)(wbeg - (int64_t)row_n * wpr);
     for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
         int64_t gi[U];
         bool valid[U];
@@ -801,8 +803,12 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t wu = w0 + u;
-            const int64_t row = wu / wpr;
-            const int x = (int)(wu - row * wpr) * 64 + lane;
+            const int64_t row = row_n;
+            const int x = xw_n * 64 + lane;
+            if (++xw_n == wpr) {
+                xw_n = 0;
+                ++row_n;
+            }
             valid[u] = wu < wend && x < B.X;
             gi[u] = B.base + (valid[u] ? row * B.X + x : 0);
             e[u] = gbl(par)[gi[u]];
@@ -1278,10 +1284,12 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
     for (int64_t un0 = ubeg; un0 < uend; un0 += 64) {
       uint64_t lw[U];
       {
+        // (32-bit unsigned division: a block has < 2^31 units; the emulated 64-bit one is long)
         const int64_t ul = un0 + lane;
-        const int gyl = (int)(ul % ngy);
-        const int64_t sl = ul / ngy;
-        const int xwl = (int)(sl % wpr), zl = (int)(sl / wpr);
+        const uint32_t ul32 = (uint32_t)ul;
+        const int gyl = (int)(ul32 % (uint32_t)ngy);
+        const uint32_t sl = ul32 / (uint32_t)ngy;
+        const int xwl = (int)(sl % (uint32_t)wpr), zl = (int)(sl / (uint32_t)wpr);
 #pragma unroll
         for (int u = 0; u < U; ++u)
             lw[u] = (ul < uend && gyl * U + u < B.Y) ? gbl(open)[B.fbase + ((int64_t)zl * B.Y + gyl * U + u) * wpr + xwl]
@@ -1292,9 +1300,10 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
         const int src = __builtin_ctzll(todo);
         todo &= todo - 1;
         const int64_t un = un0 + src;
-        const int gy = (int)(un % ngy);
-        const int64_t strip = un / ngy;
-        const int xw = (int)(strip % wpr), z = (int)(strip / wpr);
+        const uint32_t un32 = (uint32_t)un;
+        const int gy = (int)(un32 % (uint32_t)ngy);
+        const uint32_t strip = un32 / (uint32_t)ngy;
+        const int xw = (int)(strip % (uint32_t)wpr), z = (int)(strip / (uint32_t)wpr);
         const int y0 = gy * U;
         // open words of the unit's rows
         uint64_t ow[U];

@@ -193,21 +193,27 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
     const int64_t per = (nwords + nwaves - 1) / nwaves;
     const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    // (row, word in the row) of the wave's next word, advanced word by word: no 64-bit division
+    // per word (the emulated scalar divisions cost more issue time than the loads)
+    int row_n = (int)(wbeg / wpr), xw_n = (int)(wbeg - (int64_t)row_n * wpr);
     for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
         int64_t gi[U];
         bool valid[U];
-        int zs[U];
+        int rows[U];
         uint64_t kv[U];
         uint8_t fx[U];
         float hv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t row = (w0 + u) / wpr;
-            const int x = (int)(w0 + u - row * wpr) * 64 + lane;
+            rows[u] = row_n;
+            const int x = xw_n * 64 + lane;
+            if (++xw_n == wpr) {
+                xw_n = 0;
+                ++row_n;
+            }
             valid[u] = w0 + u < wend && x < B.X;
-            zs[u] = (int)(row / B.Y);
             // loads unconditional (clamped index): key and seed flag together
-            gi[u] = B.base + (valid[u] ? row * B.X + x : 0);
+            gi[u] = B.base + (valid[u] ? (int64_t)rows[u] * B.X + x : 0);
             kv[u] = key[gi[u]];
             fx[u] = fixedv[gi[u]];
         }
@@ -248,7 +254,7 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
                 open[B.fbase + w0 + u] = op;
                 chg[B.fbase + w0 + u] = kp;
                 if (kp) {
-                    uint32_t* sv = survivors + B.sbase + (B.nd_ws == 2 ? zs[u] : 0);
+                    uint32_t* sv = survivors + B.sbase + (B.nd_ws == 2 ? rows[u] / B.Y : 0);
                     if (!*sv) *sv = 1;
                 }
             }

@@ -44,6 +44,9 @@ def make_cases():
     # dt with Y^2 + X^2 >= 2^24 (vigra's float arithmetic: k_edt_real_* with T = float)
     xw1100 = _x(seed=15, shape=(8, 10, 1100))
     xw4096 = _x(seed=16, shape=(2, 24, 4096))
+    # 4096-voxel rows with a larger x radius than y: the x pass is the separate row kernel, whose
+    # 1 KiB + 16 B per voxel of LDS is above 64 KiB (the opt-in launch)
+    xw4096_3d = _x(seed=18, shape=(4, 12, 4096))
     # a mask of random blobs: the masked region is a non-convex plateau with holes, so the
     # plateau fill's run scans (k_plateau.hip) miss paths that the frontier has to correct
     rs = np.random.RandomState(17)
@@ -55,6 +58,7 @@ def make_cases():
         '3d_pitch_bigdmax': (dict(D3, pixel_pitch=(600, 1, 1)), dict(input=x)),
         '2d_wide4096_bigdmax': ({}, dict(input=xw4096)),
         '3d_wide1100': (dict(D3), dict(input=xw1100)),
+        '3d_wide4096_aniso': (dict(D3, sigma_seeds=(1., 1., 3.), sigma_weights=(1., 1., 3.)), dict(input=xw4096_3d)),
         '2d_sigma22': (dict(sigma_seeds=22.0), dict(input=x)),
         '3d_sparse_fg': (dict(D3), dict(input=xs)),
         '2d_sparse_fg': ({}, dict(input=xs)),
