@@ -110,6 +110,16 @@ def test_read_many_missing_chunks_and_overlaps(tmp_path, ext):
     exp[0:8] = x[0:8]
     for i, g in zip(idx, got):
         assert np.array_equal(g, exp[i])
+    # 4-D (channel-first) input with a channel range, as _read_block indexes it
+    x4 = np.arange(3 * 9 * 20 * 21, dtype='float32').reshape(3, 9, 20, 21)
+    with vu.file_reader(path) as f:
+        ds = f.create_dataset('x4', shape=x4.shape, chunks=(1, 4, 8, 8), dtype='float32', compression='gzip')
+        ds[:] = x4
+        ds.n_threads = 4
+        idx = [(slice(1, 3), slice(0, 9), slice(2, 18), slice(0, 21)), (slice(0, None), slice(3, 4), slice(5, 6), slice(7, 20))]
+        got = ds.read_many(idx)
+    for i, g in zip(idx, got):
+        assert np.array_equal(g, x4[i])
 
 
 @pytest.mark.parametrize('codec', ['libdeflate', 'zlib'])
