@@ -1012,6 +1012,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     const int64_t wpw = (int64_t)kWordWaves * h->words_per_wave;
     // (x extents rounded to a multiple of 8: xcd_swizzle's id % 8 then labels one XCD per grid row)
     auto r8 = [](int64_t v) { return (unsigned)std::min<int64_t>(v > 8 ? (v + 7) / 8 * 8 : v, 65528); };
+    // one workgroup per tile, rounded up to a multiple of 8 for xcd_swizzle (no cap: every tile
+    // needs its workgroup; the extra ones return at once)
+    auto tiles8 = [](int64_t v) { return (unsigned)(v > 8 ? (v + 7) / 8 * 8 : v); };
     const dim3 wtg(r8((maxRows * ((maxX + 63) / 64) + wpw - 1) / wpw), nb);
     const dim3 wtig(r8((maxIRows * ((maxIX + 63) / 64) + wpw - 1) / wpw), nb);
     size_t ev = 0;
@@ -1206,7 +1209,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed};
         if (pl.nd_ws == 3) {
             using T = CcTileM<3, CC_SEED>;  // (= the plateau tile)
-            const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
+            const dim3 tg(tiles8(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
             k_tile_cc<3, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_tile_merge<3, CC_PLATEAU><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
@@ -1214,7 +1217,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_tile_merge<3, CC_SEED><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
         } else {
             using T = CcTile<2>;
-            const dim3 tg((unsigned)(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
+            const dim3 tg(tiles8(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
             k_tile_cc<2, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_tile_merge<2, CC_PLATEAU><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
@@ -1304,7 +1307,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
         // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
         const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
-        const dim3 dg((unsigned)(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
+        const dim3 dg(tiles8(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
         {
             if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
             else k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
@@ -1556,12 +1559,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;
-                const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
+                const dim3 tg(tiles8(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
                 k_tile_cc<3, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
                 k_tile_merge<3, CC_CROP><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             } else {
                 using T = CcTile<2>;
-                const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
+                const dim3 tg(tiles8(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
                 k_tile_cc<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
                 k_tile_merge<2, CC_CROP><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             }
@@ -1586,11 +1589,11 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (crop_tiles) {
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;
-                const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
+                const dim3 tg(tiles8(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
                 k_output_crop<3><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0);
             } else {
                 using T = CcTile<2>;
-                const dim3 tg((unsigned)(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
+                const dim3 tg(tiles8(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
                 k_output_crop<2><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0);
             }
         }

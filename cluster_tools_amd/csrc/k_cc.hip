@@ -438,7 +438,9 @@ __global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict
     if (!S[blockIdx.y].active || !B.crop) return;
     const int nz = B.IZ, ny = B.IY, nx = B.IX;
     const int ntx = (nx + TX - 1) / TX, nty = (ny + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
-    const int t = blockIdx.x;
+    // XCD-contiguous tiles (gridDim.x is a multiple of 8): the uint64 rows of neighbouring tiles
+    // share lines in one L2 (config 3 output 3.1 -> 2.8 ms)
+    const int t = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
     if (t >= ntx * nty * ntz) return;
     const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
     const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;

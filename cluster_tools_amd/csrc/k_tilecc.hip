@@ -140,6 +140,8 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
     int nz, ny, nx;
     domain_dims<MODE>(B, nz, ny, nx);
     const int ntx = (nx + TX - 1) / TX, nty = (ny + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
+    // (dispatch order, not xcd_swizzle: XCD-contiguous tiles measured slower for the seed CC;
+    // gridDim.x may be rounded up to a multiple of 8)
     const int t = blockIdx.x;
     if (t >= ntx * nty * ntz) return;
     const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
