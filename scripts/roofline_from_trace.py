@@ -22,7 +22,8 @@ from stage_map import classify, short as kshort  # noqa: E402
 def main():
     trace, bench, runs = sys.argv[1], sys.argv[2], int(sys.argv[3])
     rows = []
-    with open(trace) as f:
+    import gzip
+    with (gzip.open(trace, 'rt') if trace.endswith('.gz') else open(trace)) as f:
         for r in csv.DictReader(f):
             rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']))
     rows.sort()
