@@ -1199,7 +1199,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             list_next[base + __popcll(pm & ((1ull << lane) - 1ull))] = ((uint32_t)bi << kWlChunkBits) | (uint32_t)cand;
     }
 }
-// chunk bricks: 2-D ws (CZ = 1) and 3-D; CTWS_FRONTIER_CHUNK selects one (frontier_chunk_dims)
+// chunk bricks: 2-D ws (CZ = 1) and 3-D; CTWS_FRONTIER_CHUNK2D / _3D select one (frontier_chunk_kind)
 #define CTWS_FRONTIER_INST(ND, CW, CY, CZ)                                                                           \
     template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
                                                         const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,  \
@@ -1209,23 +1209,14 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     template __global__ void k_frontier_list0<CW, CY, CZ>(const BlockDesc*, const BlockStat*, const uint64_t*, \
                                                           uint32_t*, uint32_t*);
 CTWS_FRONTIER_INST(2, 1, 64, 1)
-CTWS_FRONTIER_INST(2, 2, 32, 1)
 CTWS_FRONTIER_INST(2, 4, 16, 1)
-CTWS_FRONTIER_INST(2, 8, 8, 1)
 CTWS_FRONTIER_INST(3, 1, 8, 8)
-CTWS_FRONTIER_INST(3, 2, 8, 4)
-CTWS_FRONTIER_INST(3, 1, 16, 4)
-CTWS_FRONTIER_INST(3, 4, 4, 4)
 CTWS_FRONTIER_INST(3, 8, 8, 1)
 CTWS_FRONTIER_INST(3, 1, 32, 2)
 CTWS_LIST0_INST(1, 64, 1)
-CTWS_LIST0_INST(2, 32, 1)
 CTWS_LIST0_INST(4, 16, 1)
-CTWS_LIST0_INST(8, 8, 1)
 CTWS_LIST0_INST(1, 8, 8)
-CTWS_LIST0_INST(2, 8, 4)
-CTWS_LIST0_INST(1, 16, 4)
-CTWS_LIST0_INST(4, 4, 4)
+CTWS_LIST0_INST(8, 8, 1)
 CTWS_LIST0_INST(1, 32, 2)
 #undef CTWS_FRONTIER_INST
 #undef CTWS_LIST0_INST

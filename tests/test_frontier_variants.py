@@ -18,9 +18,8 @@ pytestmark = pytest.mark.gpu
 
 CASES = make_cases()
 VARIANTS = {
-    'bricks_a': {'CTWS_FRONTIER_CHUNK2D': '4x16x1', 'CTWS_FRONTIER_CHUNK3D': '2x8x4'},
-    'bricks_b': {'CTWS_FRONTIER_CHUNK2D': '8x8x1', 'CTWS_FRONTIER_CHUNK3D': '4x4x4'},
-    'bricks_c': {'CTWS_FRONTIER_CHUNK2D': '2x32x1', 'CTWS_FRONTIER_CHUNK3D': '1x16x4'},
+    'bricks_a': {'CTWS_FRONTIER_CHUNK2D': '4x16x1', 'CTWS_FRONTIER_CHUNK3D': '1x32x2'},
+    'bricks_b': {'CTWS_FRONTIER_CHUNK3D': '8x8x1'},
     'rows_3d_one_sweep': {'CTWS_FRONTIER_CHUNK3D': '8x8x1', 'CTWS_FRONTIER_REPS': '1'},
     'one_sweep': {'CTWS_FRONTIER_REPS': '1'},
     # masked blocks' plateaus relaxed hop by hop instead of filled by run scans (k_plateau.hip)
