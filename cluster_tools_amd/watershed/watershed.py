@@ -324,7 +324,8 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
 
 
 def _keep_on_device(blocking, block_list, config):
-    """Whether the job's uint64 outputs fit in half the free memory of its GPU."""
+    """Whether the job's uint64 outputs fit in its share of half the free memory of its GPU
+    (the jobs of the task that share the GPU -- job_id % n_gpus -- decide at the same time)."""
     if not config.get('keep_on_device', True):
         return False
     import torch
@@ -332,8 +333,10 @@ def _keep_on_device(blocking, block_list, config):
     for bid in block_list:
         _, inner_bb, _ = _get_bbs(blocking, bid, config)
         need += 8 * int(np.prod([s.stop - s.start for s in inner_bb]))
+    n_jobs = int((config.get('relabel') or {}).get('n_jobs', 1))
+    share = max(1, -(-n_jobs // max(1, torch.cuda.device_count())))
     free, _ = torch.cuda.mem_get_info(_device())
-    return need <= free // 2
+    return need <= free // (2 * share)
 
 
 def _ws_blocks_resident(h, lib_config, block_shape, todo):
