@@ -237,3 +237,21 @@ def test_watershed_task_writes_job_configs_and_fails_loudly_without_gpu(tmp_path
     assert os.path.exists(str(tmp / 'watershed_failed.log'))
     assert os.path.exists(str(tmp / 'watershed.py'))
     assert open(str(tmp / 'watershed.py')).readline().strip() == '#! ' + sys.executable
+
+
+def test_keep_on_device_divides_free_memory_across_the_jobs_of_a_gpu(monkeypatch):
+    """watershed._keep_on_device: a job keeps its uint64 outputs in HBM only while they fit in
+    its share of half the free memory -- the relabel's n_jobs spread over the visible GPUs."""
+    import torch
+    from cluster_tools_amd.watershed import watershed as ws
+    blocking = Blocking([0, 0, 0], [64, 64, 64], [32, 32, 32])
+    need = 8 * 8 * 32 ** 3                    # all 8 inner blocks, uint64
+    cfg = {'block_shape': [32, 32, 32], 'halo': [4, 4, 4], 'relabel': {'n_jobs': 4}}
+    monkeypatch.setattr(torch.cuda, 'device_count', lambda: 1)
+    monkeypatch.setattr(torch.cuda, 'mem_get_info', lambda d=None: (2 * 4 * need, 1 << 40))
+    assert ws._keep_on_device(blocking, list(range(8)), cfg)
+    monkeypatch.setattr(torch.cuda, 'mem_get_info', lambda d=None: (2 * 4 * need - 1, 1 << 40))
+    assert not ws._keep_on_device(blocking, list(range(8)), cfg)
+    monkeypatch.setattr(torch.cuda, 'device_count', lambda: 2)   # 2 jobs per GPU now
+    assert ws._keep_on_device(blocking, list(range(8)), cfg)
+    assert not ws._keep_on_device(blocking, list(range(8)), dict(cfg, keep_on_device=False))
