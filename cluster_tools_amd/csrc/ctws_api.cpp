@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstdio>
+#include <climits>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -119,6 +120,9 @@ struct ctws_handle {
     DevBuf edt_scratch;  // k_edt_real_line: per-thread parabola stacks
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
+    // ThresholdedComponents (k_threshcc.hip): forest, root bitmap, chunk counts / offsets, word
+    // offsets, min / max + any flag, host-pointer staging
+    DevBuf tc_P, tc_bits, tc_cnt, tc_offs, tc_woff, tc_red, tc_in, tc_mask, tc_out;
     // evaluation (k_eval.hip): gt / seg / pair hash tables with counts, state, sums, staging
     DevBuf ev_ka, ev_ca, ev_kb, ev_cb, ev_kp, ev_cp, ev_state, ev_out, ev_stage;
     int64_t ev_cap_a = 0, ev_cap_b = 0, ev_cap_p = 0;
@@ -2285,7 +2289,8 @@ void ctws_close(ctws_handle* h) {
                     h->edt_fh.p, h->edt_scratch.p, h->p2_hint_dev.p, h->rl_sorted.p, h->rl_uniq.p, h->rl_counts.p, h->rl_tmp.p,
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
                     h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p,
-                    w.fplat, w.plev, w.fseed};
+                    w.fplat, w.plev, w.fseed, h->tc_P.p, h->tc_bits.p, h->tc_cnt.p, h->tc_offs.p, h->tc_woff.p,
+                    h->tc_red.p, h->tc_in.p, h->tc_mask.p, h->tc_out.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);
@@ -2690,6 +2695,122 @@ int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, 
     if (!on_device) HIPCHK(hipMemcpyAsync(labels, dl, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     if (n_missing) *n_missing = (int64_t)hm;
+    return CTWS_OK;
+}
+
+
+// ---- ThresholdedComponentsWorkflow: BlockComponents (k_threshcc.hip) -----------------------
+int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t* mask, int64_t nz, int64_t ny,
+                              int64_t nx, int on_device, int mode, double threshold, int normalize, uint64_t* out,
+                              int64_t* n_labels) {
+    if (!h || !n_labels || nz < 0 || ny < 0 || nx < 0 || mode < 0 || mode > 2) return CTWS_EINVAL;
+    const int64_t n = nz * ny * nx;
+    if ((!input || !out) && n > 0) return CTWS_EINVAL;
+    h->err.clear();
+    HIPCHK(hipSetDevice(h->device));
+    *n_labels = 0;
+    if (n == 0) return CTWS_OK;
+    if (n >= (int64_t)kNoParent || nz > INT32_MAX || ny > INT32_MAX || nx > INT32_MAX) {
+        h->err = "ctws_threshold_components: block too large (needs < 2^32 - 1 voxels)";
+        return CTWS_EINVAL;
+    }
+    int r;
+    const float* din = input;
+    const uint8_t* dmask = mask;
+    uint64_t* dout = out;
+    if (!on_device) {
+        if ((r = grow(h, h->tc_in, sizeof(float) * (size_t)n)) != CTWS_OK) return r;
+        if ((r = grow(h, h->tc_out, sizeof(uint64_t) * (size_t)n)) != CTWS_OK) return r;
+        HIPCHK(hipMemcpyAsync(h->tc_in.p, input, sizeof(float) * (size_t)n, hipMemcpyHostToDevice, h->stream));
+        din = (const float*)h->tc_in.p;
+        dout = (uint64_t*)h->tc_out.p;
+        if (mask) {
+            if ((r = grow(h, h->tc_mask, (size_t)n)) != CTWS_OK) return r;
+            HIPCHK(hipMemcpyAsync(h->tc_mask.p, mask, (size_t)n, hipMemcpyHostToDevice, h->stream));
+            dmask = (const uint8_t*)h->tc_mask.p;
+        }
+    }
+    const int64_t nw = (n + 63) / 64, nc = (nw + 255) / 256;
+    if ((r = grow(h, h->tc_P, sizeof(uint32_t) * (size_t)n)) != CTWS_OK) return r;
+    if ((r = grow(h, h->tc_bits, sizeof(uint64_t) * (size_t)nw)) != CTWS_OK) return r;
+    if ((r = grow(h, h->tc_cnt, sizeof(uint32_t) * (size_t)nc)) != CTWS_OK) return r;
+    if ((r = grow(h, h->tc_offs, sizeof(uint64_t) * (size_t)(nc + 1))) != CTWS_OK) return r;
+    if ((r = grow(h, h->tc_woff, sizeof(uint32_t) * (size_t)nw)) != CTWS_OK) return r;
+    if ((r = grow(h, h->tc_red, 4 * sizeof(uint32_t))) != CTWS_OK) return r;
+    uint32_t* red = (uint32_t*)h->tc_red.p;  // [0] min, [1] max (ordered float bits), [2] any member
+    const uint32_t init[3] = {0xFFFFFFFFu, 0u, 0u};
+    HIPCHK(hipMemcpyAsync(red, init, sizeof(init), hipMemcpyHostToDevice, h->stream));
+    TcParams p;
+    p.nz = (int)nz;
+    p.ny = (int)ny;
+    p.nx = (int)nx;
+    p.mode = mode;
+    p.normalize = normalize ? 1 : 0;
+    p.thr = (float)threshold;
+    if (normalize) {
+        const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 2048);
+        k_tc_minmax<<<g, 256, 0, h->stream>>>(din, n, red);
+    }
+    const int64_t tiles = ((nx + 63) / 64) * ((ny + 7) / 8) * ((nz + 7) / 8);
+    uint32_t* P = (uint32_t*)h->tc_P.p;
+    k_tc_tile<<<(unsigned)tiles, 256, 0, h->stream>>>(din, dmask, p, red, P, red + 2);
+    LAUNCHCHK();
+    uint32_t any = 0;
+    HIPCHK(hipMemcpyAsync(&any, red + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (!any) return CTWS_OK;  // an empty block: no labels, the output is not written
+    k_tc_merge<<<(unsigned)std::min<int64_t>(tiles, 4096), 256, 0, h->stream>>>(p, P);
+    const unsigned gv = (unsigned)((n + 255) / 256);
+    k_tc_roots<<<gv, 256, 0, h->stream>>>(P, n, (uint64_t*)h->tc_bits.p);
+    k_bits_chunk_count<<<(unsigned)nc, 256, 0, h->stream>>>((const uint64_t*)h->tc_bits.p, nw,
+                                                           (uint32_t*)h->tc_cnt.p);
+    k_scan_chunks<<<1, 256, 0, h->stream>>>((const uint32_t*)h->tc_cnt.p, nc, (uint64_t*)h->tc_offs.p);
+    k_tc_wordoff<<<(unsigned)nc, 256, 0, h->stream>>>((const uint64_t*)h->tc_bits.p, nw,
+                                                     (const uint64_t*)h->tc_offs.p, (uint32_t*)h->tc_woff.p);
+    k_tc_label<<<gv, 256, 0, h->stream>>>(P, n, (const uint64_t*)h->tc_bits.p, (const uint32_t*)h->tc_woff.p, dout);
+    LAUNCHCHK();
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, (uint64_t*)h->tc_offs.p + nc, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    if (!on_device) HIPCHK(hipMemcpyAsync(out, dout, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    *n_labels = (int64_t)total;
+    return CTWS_OK;
+}
+
+
+// ---- ThresholdedComponentsWorkflow: MergeAssignments (host) --------------------------------
+// nifty.ufd.boost_ufd(n).merge(pairs); find(arange(n)) (merge_assignments.py:125-130): boost's
+// disjoint_sets with union by rank -- link(find(a), find(b)) puts the root of lower rank under
+// the other and, at equal ranks, the first root under the second (whose rank grows).  The
+// representatives depend on the merge order, so this stays a sequential pass over the pairs.
+int ctws_ufd_find(int64_t n, const uint64_t* pairs, int64_t n_pairs, uint64_t* out) {
+    if (n < 0 || n_pairs < 0 || (!out && n > 0) || (!pairs && n_pairs > 0)) return CTWS_EINVAL;
+    std::vector<uint64_t> parent((size_t)n);
+    std::vector<uint8_t> rank((size_t)n, 0);
+    for (int64_t i = 0; i < n; ++i) parent[(size_t)i] = (uint64_t)i;
+    auto find = [&](uint64_t a) {
+        uint64_t r = a;
+        while (parent[r] != r) r = parent[r];
+        while (parent[a] != r) {  // full path compression (boost's default find)
+            const uint64_t nx = parent[a];
+            parent[a] = r;
+            a = nx;
+        }
+        return r;
+    };
+    for (int64_t k = 0; k < n_pairs; ++k) {
+        const uint64_t a = pairs[2 * k], b = pairs[2 * k + 1];
+        if (a >= (uint64_t)n || b >= (uint64_t)n) return CTWS_EINVAL;
+        const uint64_t i = find(a), j = find(b);
+        if (i == j) continue;
+        if (rank[i] > rank[j]) {
+            parent[j] = i;
+        } else {
+            parent[i] = j;
+            if (rank[i] == rank[j]) ++rank[j];
+        }
+    }
+    for (int64_t i = 0; i < n; ++i) out[i] = find((uint64_t)i);
     return CTWS_OK;
 }
 

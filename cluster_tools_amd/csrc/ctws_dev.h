@@ -150,6 +150,39 @@ __device__ __forceinline__ void uf_union(uint32_t* P, uint32_t a, uint32_t b) {
     }
 }
 
+// LDS union-find of the tile CC kernels (k_tilecc.hip, k_threshcc.hip)
+// find with path halving: a non-root's parent is replaced by its grandparent (always an
+// ancestor with a smaller key, so concurrent finds and CAS links stay consistent)
+__device__ __forceinline__ uint32_t lds_find(uint32_t* sp, uint32_t a) {
+    uint32_t p = __atomic_load_n(&sp[a], __ATOMIC_RELAXED);
+    while (p != a) {
+        const uint32_t gp = __atomic_load_n(&sp[p], __ATOMIC_RELAXED);
+        if (gp != p) __atomic_store_n(&sp[a], gp, __ATOMIC_RELAXED);
+        a = gp;
+        p = __atomic_load_n(&sp[a], __ATOMIC_RELAXED);
+    }
+    return a;
+}
+// link the root with the larger order key under the one with the smaller; parents are indexed
+// by tile C-order position (consecutive lanes: consecutive LDS words, no bank conflicts), the
+// order key of a position is key(position)
+template <typename Key>
+__device__ __forceinline__ void lds_union(uint32_t* sp, uint32_t a, uint32_t b, Key key) {
+    while (true) {
+        a = lds_find(sp, a);
+        b = lds_find(sp, b);
+        if (a == b) return;
+        if (key(a) > key(b)) {
+            const uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        const uint32_t old = atomicCAS(&sp[b], b, a);
+        if (old == b) return;
+        b = old;
+    }
+}
+
 // vigra scan key (F order, axis 0 fastest; per slice and slice-major in 2-D ws mode)
 __device__ __forceinline__ uint32_t scan_key_of(const BlockDesc& B, int z, int y, int x) {
     return (B.nd_ws == 3) ? (uint32_t)(z + B.Z * (y + B.Y * x))

@@ -256,4 +256,18 @@ hipError_t u64_sort(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out,
 hipError_t u64_runs(void* tmp, size_t& bytes, const uint64_t* sorted, uint64_t* uniq, uint64_t* counts,
                     uint64_t* n_runs, int64_t n, hipStream_t stream);
 
+// k_threshcc.hip (ThresholdedComponents: BlockComponents)
+struct TcParams {
+    int nz, ny, nx;
+    int mode;       // 0 greater, 1 less, 2 equal
+    int normalize;  // 1: vu.normalize before the threshold (min / max from k_tc_minmax)
+    float thr;      // the threshold as float32
+};
+__global__ void k_tc_minmax(const float*, int64_t, uint32_t*);
+__global__ void k_tc_tile(const float*, const uint8_t*, TcParams, const uint32_t*, uint32_t*, uint32_t*);
+__global__ void k_tc_merge(TcParams, uint32_t*);
+__global__ void k_tc_roots(const uint32_t*, int64_t, uint64_t*);
+__global__ void k_tc_wordoff(const uint64_t*, int64_t, const uint64_t*, uint32_t*);
+__global__ void k_tc_label(const uint32_t*, int64_t, const uint64_t*, const uint32_t*, uint64_t*);
+
 }  // namespace ctws

@@ -31,38 +31,6 @@ __device__ __forceinline__ uint32_t fkey_local(int lz, int ly, int lx) {
     return (uint32_t)(lz + TZ * (ly + TY * lx));
 }
 
-// find with path halving: a non-root's parent is replaced by its grandparent (always an
-// ancestor with a smaller key, so concurrent finds and CAS links stay consistent)
-__device__ __forceinline__ uint32_t lds_find(uint32_t* sp, uint32_t a) {
-    uint32_t p = __atomic_load_n(&sp[a], __ATOMIC_RELAXED);
-    while (p != a) {
-        const uint32_t gp = __atomic_load_n(&sp[p], __ATOMIC_RELAXED);
-        if (gp != p) __atomic_store_n(&sp[a], gp, __ATOMIC_RELAXED);
-        a = gp;
-        p = __atomic_load_n(&sp[a], __ATOMIC_RELAXED);
-    }
-    return a;
-}
-// link the root with the larger order key under the one with the smaller; parents are indexed
-// by tile C-order position (consecutive lanes: consecutive LDS words, no bank conflicts), the
-// order key of a position is key(position)
-template <typename Key>
-__device__ __forceinline__ void lds_union(uint32_t* sp, uint32_t a, uint32_t b, Key key) {
-    while (true) {
-        a = lds_find(sp, a);
-        b = lds_find(sp, b);
-        if (a == b) return;
-        if (key(a) > key(b)) {
-            const uint32_t t = a;
-            a = b;
-            b = t;
-        }
-        const uint32_t old = atomicCAS(&sp[b], b, a);
-        if (old == b) return;
-        b = old;
-    }
-}
-
 // ---- per-mode domain, membership and connectivity ---------------------------------------
 
 // is voxel i (outer index) a local maximum? (k_cc.hip's is_max with the plateau flag)

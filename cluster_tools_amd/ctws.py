@@ -48,7 +48,8 @@ def lib():
             L.ctws_last_error.argtypes = [C.c_void_p]
             L.ctws_last_error.restype = C.c_char_p
             for fn in ('ctws_ws_blocks', 'ctws_ws_blocks_device', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
-                    'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end'):
+                    'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end', 'ctws_threshold_components',
+                    'ctws_ufd_find'):
                 getattr(L, fn).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_last_timings.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_unique_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
@@ -58,6 +59,10 @@ def lib():
             L.ctws_lookup_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
                                           C.c_int64, C.POINTER(C.c_int64)]
             L.ctws_set_table_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+            L.ctws_ufd_find.argtypes = [C.c_int64, C.c_void_p, C.c_int64, C.c_void_p]
+            L.ctws_threshold_components.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                                    C.c_int64, C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p,
+                                                    C.POINTER(C.c_int64)]
             L.ctws_eval_begin.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
             L.ctws_eval_add.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
             L.ctws_eval_end.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
@@ -74,7 +79,20 @@ ABI_VERSION = 2
 EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_error', 'ctws_ws_blocks',
                     'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_unique_u64', 'ctws_unique_counts_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
                     'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_debug_sqrt_int', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
-                    'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end')
+                    'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end', 'ctws_threshold_components',
+                    'ctws_ufd_find')
+
+
+def ufd_find(n_labels, pairs):
+    """nifty.ufd.boost_ufd(n_labels).merge(pairs); .find(arange(n_labels)) in libctws.so (host
+    code, no GPU handle): the representative of every label, uint64."""
+    pairs = np.ascontiguousarray(np.asarray(pairs, dtype=np.uint64).reshape(-1, 2))
+    out = np.empty(int(n_labels), dtype=np.uint64)
+    ret = lib().ctws_ufd_find(int(n_labels), pairs.ctypes.data if pairs.size else None, len(pairs),
+                              out.ctypes.data)
+    if ret != CTWS_OK:
+        raise CtwsError("ctws_ufd_find failed (%i): labels out of range" % ret)
+    return out
 
 
 class CtwsError(RuntimeError):
@@ -371,6 +389,32 @@ class Handle:
         self._check(lib().ctws_lookup_u64(self._h, labels.ctypes.data, labels.size, 0, kp, vp, nt, C.byref(miss)),
                     'ctws_lookup_u64')
         return int(miss.value)
+
+    # ---- ThresholdedComponentsWorkflow kernels --------------------------------------------
+    THRESHOLD_MODES = ('greater', 'less', 'equal')
+
+    def threshold_components(self, block, threshold, mode='greater', mask=None, normalize=True):
+        """BlockComponents of one 3-D block on the GPU (block_components.py:143-230): members =
+        (normalized) block `mode` threshold, inside the mask; their 26-connected components
+        numbered 1.. in C-order of first appearance (skimage.morphology.label).  numpy in
+        (float32; other dtypes are converted), -> (uint64 labels, n_labels); n_labels 0 = no
+        member (the labels are then all 0)."""
+        block = np.ascontiguousarray(block, dtype=np.float32)
+        assert block.ndim == 3, block.shape
+        if mode not in self.THRESHOLD_MODES:
+            raise RuntimeError("Thresholding Mode %s not supported" % mode)
+        mp = None
+        if mask is not None:
+            mask = np.ascontiguousarray(mask).astype(np.bool_, copy=False).view(np.uint8)
+            assert mask.shape == block.shape, (mask.shape, block.shape)
+            mp = mask.ctypes.data
+        out = np.zeros(block.shape, dtype=np.uint64)
+        n = C.c_int64(0)
+        self._check(lib().ctws_threshold_components(self._h, block.ctypes.data, mp, *block.shape, 0,
+                                                    self.THRESHOLD_MODES.index(mode), float(threshold),
+                                                    1 if normalize else 0, out.ctypes.data, C.byref(n)),
+                    'ctws_threshold_components')
+        return out, int(n.value)
 
     def unique_u64_device(self, labels):
         """np.unique of a uint64 (or int64) torch tensor on this GPU: the sorted uniques as a

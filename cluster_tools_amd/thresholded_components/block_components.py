@@ -1,0 +1,185 @@
+#! /usr/bin/env python
+"""BlockComponents: threshold every block and label its 26-connected components on the GPU
+(cluster_tools/thresholded_components/block_components.py:21-298; task surface unchanged).
+
+Per block the job reads the input (the next block ahead on a thread), calls
+ctws_threshold_components (k_threshcc.hip: normalize, threshold, mask, LDS-tiled union-find,
+skimage numbering) and writes the labels of a non-empty block; the per-block offsets
+(`max + 1`, 0 for an empty block) go to `connected_components_offsets_<job>.json` as in the
+reference.  The Gaussian prefilter (sigma_prefilter > 0) is not implemented and raises.
+"""
+import json
+import os
+import sys
+from concurrent import futures
+
+import numpy as np
+
+from cluster_tools_amd import luigi_compat as luigi
+import cluster_tools_amd.utils.volume_utils as vu
+import cluster_tools_amd.utils.function_utils as fu
+from cluster_tools_amd.utils.blocking import Blocking
+from cluster_tools_amd.cluster_tasks import SlurmTask, LocalTask, LSFTask
+
+
+class BlockComponentsBase(luigi.Task):
+    task_name = 'block_components'
+    src_file = os.path.abspath(__file__)
+    allow_retry = False
+
+    input_path = luigi.Parameter()
+    input_key = luigi.Parameter()
+    output_path = luigi.Parameter()
+    output_key = luigi.Parameter()
+    dependency = luigi.TaskParameter()
+    threshold = luigi.FloatParameter()
+    threshold_mode = luigi.Parameter(default='greater')
+    mask_path = luigi.Parameter(default='')
+    mask_key = luigi.Parameter(default='')
+    channel = luigi.Parameter(default=None)
+
+    threshold_modes = ('greater', 'less', 'equal')
+
+    @staticmethod
+    def default_task_config():
+        config = LocalTask.default_task_config()
+        config.update({'sigma_prefilter': 0})
+        return config
+
+    def requires(self):
+        return self.dependency
+
+    def run_impl(self):
+        shebang, block_shape, roi_begin, roi_end = self.global_config_values()
+        self.init(shebang)
+        shape = vu.get_shape(self.input_path, self.input_key)
+        assert self.threshold_mode in self.threshold_modes
+        config = self.get_task_config()
+        config.update({'input_path': self.input_path, 'input_key': self.input_key,
+                       'output_path': self.output_path, 'output_key': self.output_key,
+                       'block_shape': block_shape, 'tmp_folder': self.tmp_folder,
+                       'threshold': self.threshold, 'threshold_mode': self.threshold_mode})
+        if self.mask_path != '':
+            assert self.mask_key != ''
+            config.update({'mask_path': self.mask_path, 'mask_key': self.mask_key})
+        chunks = config.pop('chunks', None)
+        if chunks is None:
+            chunks = tuple(bs // 2 for bs in block_shape)
+        if self.channel is None:
+            assert len(shape) == 3, str(len(shape))
+        else:
+            assert isinstance(self.channel, (int, tuple, list))
+            assert len(shape) == 4, str(len(shape))
+            chans = [self.channel] if isinstance(self.channel, int) else list(self.channel)
+            assert all(isinstance(c, int) for c in chans)
+            assert shape[0] > max(chans), "%i, %i" % (shape[0], max(chans))
+            shape = shape[1:]
+            config.update({'channel': self.channel})
+        chunks = tuple(min(ch, sh) for ch, sh in zip(chunks, shape))
+        compression = config.pop('compression', 'gzip')
+        with vu.file_reader(self.output_path) as f:
+            f.require_dataset(self.output_key, shape=tuple(shape), dtype='uint64', compression=compression,
+                              chunks=chunks)
+        block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end)
+        self.run_jobs(min(len(block_list), self.max_jobs), block_list, config)
+
+
+class BlockComponentsLocal(BlockComponentsBase, LocalTask):
+    pass
+
+
+class BlockComponentsSlurm(BlockComponentsBase, SlurmTask):
+    pass
+
+
+class BlockComponentsLSF(BlockComponentsBase, LSFTask):
+    pass
+
+
+def _device():
+    return int(os.environ.get('CTWS_DEVICE', os.environ.get('LOCAL_RANK', '0')))
+
+
+def _read_block(blocking, block_id, ds_in, mask, channel):
+    """One block's input and mask (block_components.py:147-158 / :188-206): the unmasked single
+    channel block is normalized on the GPU; channels are summed in the dataset dtype."""
+    bb = vu.block_to_bb(blocking.getBlock(block_id))
+    b = {'block_id': block_id, 'bb': bb, 'mask': None}
+    if mask is not None:
+        in_mask = np.asarray(mask[bb]).astype('bool')
+        if in_mask.sum() == 0:
+            b['skip'] = True
+            return b
+        b['mask'] = in_mask
+    if channel is None:
+        b['input'] = ds_in[bb]
+    else:
+        shape = tuple(s.stop - s.start for s in bb)
+        x = np.zeros(shape, dtype=ds_in.dtype)
+        for chan in ([channel] if isinstance(channel, int) else channel):
+            x += ds_in[(slice(chan, chan + 1),) + bb].squeeze()
+        b['input'] = x
+    return b
+
+
+def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config):
+    """`_cc_block[_with_mask]` for every block of the job -> {block_id: offset}."""
+    from cluster_tools_amd import ctws
+    sigma = config.get('sigma_prefilter', 0)
+    if sigma > 0:
+        raise NotImplementedError("sigma_prefilter > 0 (vigra gaussianSmoothing) is not implemented")
+    threshold, mode = config['threshold'], config['threshold_mode']
+    channel = config.get('channel', None)
+    offsets = {}
+    with ctws.Handle(_device()) as h, futures.ThreadPoolExecutor(1) as io:
+        nxt = io.submit(_read_block, blocking, block_list[0], ds_in, mask, channel) if block_list else None
+        for k, block_id in enumerate(block_list):
+            b = nxt.result()
+            nxt = (io.submit(_read_block, blocking, block_list[k + 1], ds_in, mask, channel)
+                   if k + 1 < len(block_list) else None)
+            fu.log("start processing block %i" % block_id)
+            if b.get('skip'):
+                offsets[block_id] = 0
+                fu.log_block_success(block_id)
+                continue
+            # the unmasked, single-channel block is normalized first (vu.normalize); the masked
+            # and multi-channel ones are thresholded raw (sigma 0)
+            labels, n = h.threshold_components(b['input'], threshold, mode, mask=b['mask'],
+                                               normalize=(mask is None and channel is None))
+            if n:
+                ds_out[b['bb']] = labels
+            offsets[block_id] = n + 1 if n else 0
+            fu.log_block_success(block_id)
+    return offsets
+
+
+def block_components(job_id, config_path):
+    fu.log("start processing job %i" % job_id)
+    fu.log("reading config from %s" % config_path)
+    with open(config_path) as f:
+        config = json.load(f)
+    fu.log("Applying threshold %f with mode %s" % (config['threshold'], config['threshold_mode']))
+    channel = config.get('channel', None)
+    with vu.file_reader(config['input_path'], 'r') as f_in, vu.file_reader(config['output_path']) as f_out:
+        ds_in = f_in[config['input_key']]
+        ds_out = f_out[config['output_key']]
+        shape = list(ds_in.shape)
+        if channel is not None:
+            shape = shape[1:]
+        assert len(shape) == 3
+        blocking = Blocking([0, 0, 0], shape, list(config['block_shape']))
+        mask = None
+        if config.get('mask_path', ''):
+            mask = vu.load_mask(config['mask_path'], config['mask_key'], shape)
+        offsets = run_component_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config)
+    save_path = os.path.join(config['tmp_folder'], 'connected_components_offsets_%i.json' % job_id)
+    with open(save_path, 'w') as f:
+        json.dump({int(k): int(v) for k, v in offsets.items()}, f)
+    fu.log_job_success(job_id)
+
+
+if __name__ == '__main__':
+    path = sys.argv[1]
+    assert os.path.exists(path), path
+    job_id = int(os.path.split(path)[1].split('.')[0].split('_')[-1])
+    block_components(job_id, path)

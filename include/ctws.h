@@ -219,6 +219,30 @@ int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, 
                     const uint64_t* values, int64_t n_table, int64_t* n_missing);
 
 /*
+ * ThresholdedComponentsWorkflow, BlockComponents (thresholded_components/block_components.py:
+ * 143-230: `_cc_block` / `_cc_block_with_mask`, threshold + skimage.morphology.label) on the GPU.
+ *
+ * ctws_threshold_components: input = one float32 block (nz, ny, nx), C order; mask = uint8
+ *   (nonzero = in mask) or NULL; normalize = 1 applies vu.normalize first (the unmasked,
+ *   single-channel case); mode 0 'greater', 1 'less', 2 'equal' against threshold (compared as
+ *   float32).  out (uint64, same shape) <- the 26-connected components of the members numbered
+ *   1.. in order of first appearance in a C-order scan (skimage's numbering), 0 elsewhere;
+ *   *n_labels = their number.  A block without members leaves out unwritten and *n_labels = 0
+ *   (the reference returns 0 and writes nothing).  on_device: 1 device pointers, 0 host.
+ *   Blocks of fewer than 2^32 - 1 voxels.
+ */
+int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t* mask, int64_t nz, int64_t ny,
+                              int64_t nx, int on_device, int mode, double threshold, int normalize, uint64_t* out,
+                              int64_t* n_labels);
+/*
+ * MergeAssignments (thresholded_components/merge_assignments.py:125-130): out[i] = the
+ * representative of label i after merging the (a, b) rows of pairs (n_pairs x 2, C order) into
+ * nifty's boost_ufd(n) in row order -- boost::disjoint_sets union by rank (equal ranks: the first
+ * root goes under the second).  Host code, no handle; CTWS_EINVAL for a label >= n.
+ */
+int ctws_ufd_find(int64_t n, const uint64_t* pairs, int64_t n_pairs, uint64_t* out);
+
+/*
  * Test hooks (used by the parity tests, not by the task code): stop the pipeline after a
  * stage and read back one block's outer-shaped workspace array of the last batch.
  *   arrays: "fin" (float32 normalized input), "dt" (float32), "seedmap" (float32 smoothed
