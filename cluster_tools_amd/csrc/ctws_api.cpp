@@ -2748,7 +2748,11 @@ int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t*
     p.normalize = normalize ? 1 : 0;
     p.thr = (float)threshold;
     if (normalize) {
-        const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 2048);
+        if (reinterpret_cast<uintptr_t>(din) % 16 != 0) {
+            h->err = "ctws_threshold_components: input not 16-byte aligned";
+            return CTWS_EINVAL;
+        }
+        const unsigned g = (unsigned)std::min<int64_t>((n + 4095) / 4096, 256);
         k_tc_minmax<<<g, 256, 0, h->stream>>>(din, n, red);
     }
     const int64_t tiles = ((nx + 63) / 64) * ((ny + 7) / 8) * ((nz + 7) / 8);

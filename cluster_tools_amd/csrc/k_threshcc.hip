@@ -43,9 +43,19 @@ __device__ __forceinline__ uint32_t tc_find(const uint32_t* P, uint32_t a) {
 }
 }  // namespace
 
+// one workgroup per CU at most (the two atomics per workgroup on one address are what a wide
+// grid pays for: 4096 of them cost ~45 us); float4 loads, the tail scalar
 __global__ void __launch_bounds__(256) k_tc_minmax(const float* __restrict__ v, int64_t n, uint32_t* __restrict__ mm) {
     uint32_t lo = 0xFFFFFFFFu, hi = 0u;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * 256;
+    const float4* v4 = reinterpret_cast<const float4*>(v);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+        const float4 f = v4[i];
+        const uint32_t a = ordf(f.x), b = ordf(f.y), c = ordf(f.z), d = ordf(f.w);
+        lo = min(lo, min(min(a, b), min(c, d)));
+        hi = max(hi, max(max(a, b), max(c, d)));
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
         const uint32_t u = ordf(v[i]);
         lo = min(lo, u);
         hi = max(hi, u);
@@ -116,7 +126,8 @@ __global__ void __launch_bounds__(256) k_tc_tile(const float* __restrict__ v, co
     // the four backward rows (dz, dy) = (-1, -1), (-1, 0), (-1, 1), (0, -1), each with dx in
     // {-1, 0, 1}: one union per run of members among the three (adjacent ones share an x run);
     // a voxel that continues its run needs only q + 1 when q is no member (its x predecessor
-    // covered q - 1 and q)
+    // covered q - 1 and q); with a member right below (dz = -1), the rows (-1, -1) and (-1, +1)
+    // are its in-plane neighbours, connected through its own unions
     auto ordk = [](uint32_t c) { return c; };
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -124,11 +135,14 @@ __global__ void __launch_bounds__(256) k_tc_tile(const float* __restrict__ v, co
         const int c = threadIdx.x + j * 256;
         const int lx = c & (TX - 1), ly = (c / TX) % TY, lz = c / (TX * TY);
         const bool cont = (contm >> j) & 1u;
+        // the voxel below (dz = -1) a member: rows (-1, -1) and (-1, +1) touch it in its plane
+        const bool below = lz > 0 && sm[c - TY * TX];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int dz = r < 3 ? -1 : 0, dy = r < 3 ? r - 1 : -1;
             const int qz = lz + dz, qy = ly + dy;
             if (qz < 0 || qy < 0 || qy >= TY) continue;
+            if ((r == 0 || r == 2) && below) continue;
             const int cq = (qz * TY + qy) * TX + lx;
             const bool m0 = sm[cq] != 0;
             const bool mr = lx + 1 < TX && sm[cq + 1];
@@ -158,14 +172,18 @@ __global__ void __launch_bounds__(256) k_tc_tile(const float* __restrict__ v, co
     }
 }
 
-// unions across the tile faces: every member on a tile's low z / low y / high y / low x / high x
-// face with its backward neighbours outside the tile (the row rule of k_tc_tile over the whole
-// row; the high y face for the row (dz, dy) = (-1, +1))
+// unions across the tile faces.  Each shell voxel of a tile once: the low z plane, then (lz > 0)
+// the low / high y rows, then (lz > 0, 0 < ly < TY - 1) the low / high x columns.  A member unions
+// with its backward neighbours outside the tile by the row rule of k_tc_tile applied to the whole
+// row (the row (dz, dy) = (-1, +1) leaves through the high y face); in the planes and rows, where
+// lanes walk x, a member that continues the run of its x predecessor (also on the shell, same
+// rows) adds only q + 1 when q is no member.
 __global__ void __launch_bounds__(256) k_tc_merge(TcParams p, uint32_t* __restrict__ P) {
     constexpr int TZ = kTcTZ, TY = kTcTY, TX = kTcTX;
+    static_assert(TY > 2 && TZ > 1, "");
     const int nz = p.nz, ny = p.ny, nx = p.nx;
     const int ntx = (nx + TX - 1) / TX, nty = (ny + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
-    const int fsz[5] = {TY * TX, TZ * TX, TZ * TX, TZ * TY, TZ * TY};  // z-low, y-low, y-high, x-low, x-high
+    constexpr int fsz[5] = {TY * TX, (TZ - 1) * TX, (TZ - 1) * TX, (TZ - 1) * (TY - 2), (TZ - 1) * (TY - 2)};
     for (int t = blockIdx.x; t < ntx * nty * ntz; t += gridDim.x) {
         const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
         const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
@@ -173,26 +191,30 @@ __global__ void __launch_bounds__(256) k_tc_merge(TcParams p, uint32_t* __restri
             for (int e = threadIdx.x; e < fsz[f]; e += 256) {
                 int lz, ly, lx;
                 if (f == 0) { lz = 0; ly = e / TX; lx = e % TX; }
-                else if (f <= 2) { lz = e / TX; ly = f == 1 ? 0 : TY - 1; lx = e % TX; }
-                else { lz = e / TY; ly = e % TY; lx = f == 3 ? 0 : TX - 1; }
+                else if (f <= 2) { lz = 1 + e / TX; ly = f == 1 ? 0 : TY - 1; lx = e % TX; }
+                else { lz = 1 + e / (TY - 2); ly = 1 + e % (TY - 2); lx = f == 3 ? 0 : TX - 1; }
                 const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
                 if (z >= nz || y >= ny || x >= nx) continue;
                 const int64_t i = ((int64_t)z * ny + y) * nx + x;
                 if (P[i] == kNoParent) continue;
                 if (lx == 0 && x > 0 && P[i - 1] != kNoParent) uf_union(P, (uint32_t)i, (uint32_t)(i - 1));
+                const bool cont = f <= 2 && lx > 0 && P[i - 1] != kNoParent;
+                const bool below = z > 0 && P[i - (int64_t)ny * nx] != kNoParent;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int dz = r < 3 ? -1 : 0, dy = r < 3 ? r - 1 : -1;
                     const int qz = z + dz, qy = y + dy;
                     if (qz < 0 || qy < 0 || qy >= ny) continue;
+                    if ((r == 0 || r == 2) && below) continue;
                     const bool row_out = lz + dz < 0 || ly + dy < 0 || ly + dy >= TY;
+                    if (!row_out && lx != 0 && lx != TX - 1) continue;  // the whole row is the tile's
                     const int64_t q = ((int64_t)qz * ny + qy) * nx + x;
                     const bool m0 = P[q] != kNoParent;
-                    const bool ml = x > 0 && P[q - 1] != kNoParent;
                     const bool mr = x + 1 < nx && P[q + 1] != kNoParent;
                     if (m0) {
-                        if (row_out) uf_union(P, (uint32_t)i, (uint32_t)q);
+                        if (row_out && !cont) uf_union(P, (uint32_t)i, (uint32_t)q);
                     } else {
+                        const bool ml = !cont && x > 0 && P[q - 1] != kNoParent;
                         if (ml && (row_out || lx == 0)) uf_union(P, (uint32_t)i, (uint32_t)(q - 1));
                         if (mr && (row_out || lx == TX - 1)) uf_union(P, (uint32_t)i, (uint32_t)(q + 1));
                     }

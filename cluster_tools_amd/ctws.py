@@ -416,6 +416,30 @@ class Handle:
                     'ctws_threshold_components')
         return out, int(n.value)
 
+    def threshold_components_device(self, block, threshold, mode='greater', mask=None, normalize=True, out=None):
+        """threshold_components on torch tensors on this GPU: block float32 (Z, Y, X), mask uint8
+        or None, out int64 (uint64 bits; allocated if None) -> (out, n_labels).  Nothing crosses
+        PCIe but the member flag and the label count; out is left unwritten when n_labels is 0."""
+        import torch
+        assert block.is_cuda and block.is_contiguous() and block.dtype == torch.float32 and block.dim() == 3
+        if mode not in self.THRESHOLD_MODES:
+            raise RuntimeError("Thresholding Mode %s not supported" % mode)
+        if out is None:
+            out = torch.empty(block.shape, dtype=torch.int64, device=block.device)
+        assert out.is_contiguous() and out.element_size() == 8 and tuple(out.shape) == tuple(block.shape)
+        mp = None
+        if mask is not None:
+            assert mask.is_cuda and mask.is_contiguous() and mask.dtype == torch.uint8
+            assert tuple(mask.shape) == tuple(block.shape)
+            mp = mask.data_ptr()
+        torch.cuda.current_stream(block.device).synchronize()
+        n = C.c_int64(0)
+        self._check(lib().ctws_threshold_components(self._h, block.data_ptr(), mp, *block.shape, 1,
+                                                    self.THRESHOLD_MODES.index(mode), float(threshold),
+                                                    1 if normalize else 0, out.data_ptr(), C.byref(n)),
+                    'ctws_threshold_components')
+        return out, int(n.value)
+
     def unique_u64_device(self, labels):
         """np.unique of a uint64 (or int64) torch tensor on this GPU: the sorted uniques as a
         numpy uint64 array (the labels stay in HBM; only the uniques cross PCIe)."""

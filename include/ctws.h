@@ -25,6 +25,12 @@
  *       EvaluationWorkflow's overlaps + Measures (evaluation/evaluation_workflow.py:53-77,
  *       evaluation/measures.py:80-164, utils/validation_utils.py:60-76, 178-198).
  *
+ *   ctws_threshold_components / ctws_ufd_find
+ *       ThresholdedComponentsWorkflow: BlockComponents' per-block `_cc_block[_with_mask]`
+ *       (thresholded_components/block_components.py:143-230: normalize, threshold,
+ *       skimage.morphology.label) and MergeAssignments' nifty boost_ufd merge + find
+ *       (thresholded_components/merge_assignments.py:125-130).
+ *
  *   ctws_open / ctws_close / ctws_last_error
  *       process-level setup; the reference has none (vigra is stateless).  One handle per
  *       (process, GPU), as LocalTask runs one process per job (cluster_tasks.py:507-529).
