@@ -293,6 +293,49 @@ def pcie_rates(dev, nbytes=1 << 30, reps=4):
     return out
 
 
+def threshcc_leg(dev, shape=(128, 512, 512), reps=10):
+    """BlockComponents of ThresholdedComponentsWorkflow (k_threshcc.hip) on
+    one synthetic block of smooth blobs (uniform noise, two 5^3 box filters on the GPU),
+    normalized and thresholded at 0.5, input and labels in HBM.  The CPU oracle
+    (oracle/threshcc.py: scipy ndimage.label, one core) runs on the first quarter in z, which
+    is also checked bit-exact against the GPU."""
+    import torch
+    import torch.nn.functional as F
+    from cluster_tools_amd import ctws
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.rand((1, 1) + tuple(shape), generator=g, device=dev)
+    for _ in range(2):
+        x = F.avg_pool3d(x, 5, stride=1, padding=2, count_include_pad=False)
+    x = x[0, 0].contiguous()
+    n_vox = x.numel()
+    with ctws.Handle(dev.index or 0) as h:
+        out = torch.empty(shape, dtype=torch.int64, device=dev)
+        for _ in range(2):
+            h.threshold_components_device(x, .5, 'greater', out=out)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            _, n = h.threshold_components_device(x, .5, 'greater', out=out)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        sub = x[:shape[0] // 4].contiguous()
+        lab, _ = h.threshold_components_device(sub, .5, 'greater')
+        lab = lab.cpu().numpy().view(np.uint64)
+    from oracle import threshcc as T
+    xs = sub.cpu().numpy()
+    t0 = time.perf_counter()
+    ref, _ = T.block_components(xs, .5, 'greater')
+    t_cpu = time.perf_counter() - t0
+    return {'workload': 'BlockComponents, %s smooth blobs, normalize + threshold 0.5, 26-connected' % 'x'.join(map(str, shape)),
+            'value': round(n_vox / dt / 1e9, 3), 'unit': 'Gvoxel/s', 'ms_per_block': round(dt * 1e3, 3),
+            'n_labels': n, 'alg_bytes_per_voxel': 28,
+            'roofline': {'bound': 'hbm', 'achieved': round(28 * n_vox / dt / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(28 * n_vox / dt / 1e9 / HBM_PEAK_GBS, 4)},
+            'cpu_baseline': {'value': round(xs.size / t_cpu / 1e9, 4), 'unit': 'Gvoxel/s', 'cores': 1, 'kind': 'port',
+                             'sample': 'first %d z-slices of the block' % xs.shape[0]},
+            'bit_exact_vs_oracle_on_sample': bool(np.array_equal(lab, ref))}
+
+
 def end_to_end(cfg_id, dev, z_extent=None, max_jobs=4, threads=4):
     """The product path from file to file: WatershedWorkflow
     (target 'local', GPU jobs, the relabel inside the watershed jobs) from an n5 gzip input to the
@@ -671,6 +714,7 @@ def main():
     ap.add_argument('--no-host', action='store_true', help='skip the host-resident (PCIe-inclusive) pass')
     ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end n5 workflow run')
     ap.add_argument('--no-strong', action='store_true', help='skip the strong-scaling config 4 run')
+    ap.add_argument('--no-threshcc', action='store_true', help='skip the thresholded-components block leg')
     ap.add_argument('--strong-steps', type=int, default=3)
     ap.add_argument('--e2e-z', type=int, default=None,
                     help='z extent of the end-to-end volume (default: the whole config volume)')
@@ -747,6 +791,12 @@ def main():
         torch.cuda.empty_cache()
         e2e = end_to_end(args.config, dev, z_extent=args.e2e_z)
 
+    tcc = None
+    if rank == 0 and world == 1 and not args.no_threshcc:
+        progress('thresholded components block')
+        torch.cuda.empty_cache()
+        tcc = threshcc_leg(dev)
+
     # ---- VI of the GPU output vs the oracle on the CPU baseline's first block ---------------
     vi = None
     if ref_block is not None and ref_block[1] is not None and m['kept'] is not None:
@@ -799,6 +849,7 @@ def main():
             'strong_config4': strong,
             'host_resident': m['host'],
             'end_to_end': e2e,
+            'thresholded_components': tcc,
             'vi_vs_oracle': vi,
             'stage_ms': {k: round(v, 3) for k, v in m['stage_ms'].items()},
             'stage_ms_1stream': {k: round(v, 3) for k, v in m['stage_1'].items()},
