@@ -20,6 +20,8 @@ namespace ctws {
 
 namespace {
 constexpr int kTcTZ = 8, kTcTY = 8, kTcTX = 64, kTcTN = kTcTZ * kTcTY * kTcTX, kTcPer = kTcTN / 256;
+constexpr int kTcPairs = 2048;  // LDS union-pair list; beyond it a thread unites in place
+static_assert(kTcTN <= 4096, "pairs pack two 12-bit tile positions");
 
 __device__ __forceinline__ bool tc_member(float v, const TcParams& p, float vmin, float range) {
     // numpy in float32: v - min, divided by max(v - min) = fl(max - min) when that is positive
@@ -74,6 +76,8 @@ __global__ void __launch_bounds__(256) k_tc_tile(const float* __restrict__ v, co
     constexpr int TZ = kTcTZ, TY = kTcTY, TX = kTcTX, TN = kTcTN, PER = kTcPer;
     __shared__ uint8_t sm[TN];   // members, C layout c = (lz * TY + ly) * TX + lx
     __shared__ uint32_t sp[TN];  // tile-local parents
+    __shared__ uint32_t pbuf[kTcPairs];  // union pairs (source << 12 | target), tile positions
+    __shared__ uint32_t pcnt;
     const int nz = p.nz, ny = p.ny, nx = p.nx;
     const int ntx = (nx + TX - 1) / TX, nty = (ny + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
     const int t = blockIdx.x;
@@ -107,6 +111,7 @@ __global__ void __launch_bounds__(256) k_tc_tile(const float* __restrict__ v, co
         memb |= (m ? 1u : 0u) << j;
         sm[c] = m ? 1 : 0;
     }
+    if (threadIdx.x == 0) pcnt = 0u;
     if (__syncthreads_or(memb != 0) && threadIdx.x == 0) any[0] = 1u;
     // x runs: a wave holds one tile row (TX = 64); members link to the first voxel of their run
     const int lane = threadIdx.x & 63;
@@ -127,32 +132,57 @@ __global__ void __launch_bounds__(256) k_tc_tile(const float* __restrict__ v, co
     // {-1, 0, 1}: one union per run of members among the three (adjacent ones share an x run);
     // a voxel that continues its run needs only q + 1 when q is no member (its x predecessor
     // covered q - 1 and q); with a member right below (dz = -1), the rows (-1, -1) and (-1, +1)
-    // are its in-plane neighbours, connected through its own unions
+    // are its in-plane neighbours, connected through its own unions.
+    // The pairs are first collected into an LDS list (one atomic per wave and row) and then
+    // united by all 256 threads at once: done in place, a wave's few active lanes per row
+    // walked 64 dependent union chains one after the other (tile kernel 365 -> see DESIGN §3.2).
     auto ordk = [](uint32_t c) { return c; };
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        if (!((memb >> j) & 1u)) continue;
+        const bool mem = (memb >> j) & 1u;
         const int c = threadIdx.x + j * 256;
         const int lx = c & (TX - 1), ly = (c / TX) % TY, lz = c / (TX * TY);
         const bool cont = (contm >> j) & 1u;
-        // the voxel below (dz = -1) a member: rows (-1, -1) and (-1, +1) touch it in its plane
-        const bool below = lz > 0 && sm[c - TY * TX];
+        const bool below = mem && lz > 0 && sm[c - TY * TX];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int dz = r < 3 ? -1 : 0, dy = r < 3 ? r - 1 : -1;
             const int qz = lz + dz, qy = ly + dy;
-            if (qz < 0 || qy < 0 || qy >= TY) continue;
-            if ((r == 0 || r == 2) && below) continue;
-            const int cq = (qz * TY + qy) * TX + lx;
-            const bool m0 = sm[cq] != 0;
-            const bool mr = lx + 1 < TX && sm[cq + 1];
-            if (m0) {
-                if (!cont) lds_union(sp, (uint32_t)c, (uint32_t)cq, ordk);
-            } else {
-                const bool ml = lx > 0 && sm[cq - 1];
-                if (ml && !cont) lds_union(sp, (uint32_t)c, (uint32_t)(cq - 1), ordk);
-                if (mr) lds_union(sp, (uint32_t)c, (uint32_t)(cq + 1), ordk);
+            const bool valid = mem && qz >= 0 && qy >= 0 && qy < TY && !((r == 0 || r == 2) && below);
+            const int cq = valid ? (qz * TY + qy) * TX + lx : 0;
+            const bool m0 = valid && sm[cq] != 0;
+            const bool mr = valid && !m0 && lx + 1 < TX && sm[cq + 1];
+            const bool ml = valid && !m0 && !cont && lx > 0 && sm[cq - 1];
+            // first pair: q (m0, not cont) or q - 1 (ml); second pair: q + 1 (mr)
+            const bool has1 = (m0 && !cont) || ml, has2 = mr;
+            const uint32_t v1 = ((uint32_t)c << 12) | (uint32_t)(m0 ? cq : cq - 1);
+            const uint32_t v2 = ((uint32_t)c << 12) | (uint32_t)(cq + 1);
+            const uint64_t b1 = __ballot(has1), b2 = __ballot(has2);
+            if (b1 | b2) {
+                const int leader = __builtin_ctzll(b1 | b2);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&pcnt, (uint32_t)(__popcll(b1) + __popcll(b2)));
+                base = (uint32_t)__shfl((int)base, leader);
+                const uint64_t lt = (1ull << lane) - 1ull;
+                const uint32_t i1 = base + (uint32_t)__popcll(b1 & lt);
+                const uint32_t i2 = base + (uint32_t)__popcll(b1) + (uint32_t)__popcll(b2 & lt);
+                if (has1) {
+                    if (i1 < kTcPairs) pbuf[i1] = v1;
+                    else lds_union(sp, v1 >> 12, v1 & 0xFFFu, ordk);
+                }
+                if (has2) {
+                    if (i2 < kTcPairs) pbuf[i2] = v2;
+                    else lds_union(sp, v2 >> 12, v2 & 0xFFFu, ordk);
+                }
             }
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t np = min(pcnt, (uint32_t)kTcPairs);
+        for (uint32_t e = threadIdx.x; e < np; e += 256) {
+            const uint32_t v = pbuf[e];
+            lds_union(sp, v >> 12, v & 0xFFFu, ordk);
         }
     }
     __syncthreads();
