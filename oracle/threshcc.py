@@ -140,9 +140,11 @@ def boost_ufd_find(n, pairs):
     return np.array([find(i) for i in range(n)], dtype='uint64')
 
 
-def thresholded_components(volume, blocking, threshold, mode='greater', mask=None):
+def thresholded_components(volume, blocking, threshold, mode='greater', mask=None, normalize_input=None):
     """The whole workflow on an in-memory volume (one job per task):
-    -> (segmentation uint64, assignments uint64, offsets dict)."""
+    -> (segmentation uint64, assignments uint64, offsets dict).  normalize_input None: as the
+    reference, normalize the unmasked blocks only; False: the summed channels of a 4-D input
+    (block_components.py:152-158 compares them raw)."""
     seg = np.zeros(volume.shape, dtype='uint64')
     counts = []
     for bid in range(blocking.numberOfBlocks):
@@ -155,7 +157,8 @@ def thresholded_components(volume, blocking, threshold, mode='greater', mask=Non
                 continue
             lab, n = block_components(volume[bb], threshold, mode, mb, normalize_input=False)
         else:
-            lab, n = block_components(volume[bb], threshold, mode, None, normalize_input=True)
+            lab, n = block_components(volume[bb], threshold, mode, None,
+                                      normalize_input=True if normalize_input is None else normalize_input)
         if n:
             seg[bb] = lab
         counts.append(n + 1 if n else 0)

@@ -109,6 +109,30 @@ def test_thresholded_components_workflow_matches_oracle(tmp_path, masked, max_jo
     assert len(np.unique(seg)) > 2
 
 
+def test_thresholded_components_channels_match_oracle(tmp_path):
+    """A 4-D input with channel=[0, 2]: the channels are summed in the dataset dtype and
+    thresholded raw (block_components.py:152-158), here in 'less' mode."""
+    from conftest import luigi_build
+    from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    shape, bs = (24, 64, 130), (12, 32, 64)
+    chans = np.stack([_volume(shape, s) for s in (1, 2, 3)])
+    path = str(tmp_path / 'data.n5')
+    with vu.file_reader(path) as f:
+        f.create_dataset('x', data=chans, chunks=(1, 6, 16, 32))
+    wf = ThresholdedComponentsWorkflow(input_path=path, input_key='x', output_path=path, output_key='cc',
+                                       assignment_key='ass', threshold=.98, threshold_mode='less', channel=[0, 2],
+                                       tmp_folder=str(tmp_path / 'tmp'), config_dir=_configs(tmp_path, bs),
+                                       max_jobs=2, target='local')
+    luigi_build(wf, tmp_path / 'tmp')
+    summed = (chans[0] + chans[2]).astype(np.float32)
+    ref_seg, ref_ass, _ = T.thresholded_components(summed, Blocking([0, 0, 0], list(shape), list(bs)), .98, 'less',
+                                                   normalize_input=False)
+    with vu.file_reader(path, 'r') as f:
+        np.testing.assert_array_equal(f['ass'][:], ref_ass)
+        np.testing.assert_array_equal(f['cc'][:], ref_seg)
+    assert len(np.unique(ref_seg)) > 2
+
+
 def test_threshold_and_watershed_workflow_matches_oracle(tmp_path):
     from conftest import luigi_build
     from cluster_tools_amd.thresholded_components import ThresholdAndWatershedWorkflow
