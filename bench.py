@@ -795,7 +795,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_threshcc:
         progress('thresholded components block')
         torch.cuda.empty_cache()
-        tcc = threshcc_leg(dev)
+        try:
+            tcc = threshcc_leg(dev)
+        except Exception as e:  # a side leg never takes the headline line down
+            tcc = {'error': '%s: %s' % (type(e).__name__, e)}
 
     # ---- VI of the GPU output vs the oracle on the CPU baseline's first block ---------------
     vi = None
