@@ -789,7 +789,10 @@ def main():
         progress('end-to-end workflow run')
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        e2e = end_to_end(args.config, dev, z_extent=args.e2e_z)
+        try:
+            e2e = end_to_end(args.config, dev, z_extent=args.e2e_z)
+        except Exception as e:  # a side leg never takes the headline line down
+            e2e = {'error': '%s: %s' % (type(e).__name__, e)}
 
     tcc = None
     if rank == 0 and world == 1 and not args.no_threshcc:
