@@ -326,11 +326,18 @@ def threshcc_leg(dev, shape=(128, 512, 512), reps=10):
     t0 = time.perf_counter()
     ref, _ = T.block_components(xs, .5, 'greater')
     t_cpu = time.perf_counter() - t0
+    traffic = None
+    pmc = os.path.join(HERE, 'profiles', 'pmc_traffic_threshcc.json')
+    if os.path.exists(pmc) and tuple(shape) == (128, 512, 512):
+        with open(pmc) as f:
+            traffic = json.load(f).get('total_bytes_per_call')
     return {'workload': 'BlockComponents, %s smooth blobs, normalize + threshold 0.5, 26-connected' % 'x'.join(map(str, shape)),
             'value': round(n_vox / dt / 1e9, 3), 'unit': 'Gvoxel/s', 'ms_per_block': round(dt * 1e3, 3),
             'n_labels': n, 'alg_bytes_per_voxel': 28,
             'roofline': {'bound': 'hbm', 'achieved': round(28 * n_vox / dt / 1e9, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(28 * n_vox / dt / 1e9 / HBM_PEAK_GBS, 4)},
+                         'unit': 'GB/s', 'frac': round(28 * n_vox / dt / 1e9 / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                         'traffic_unit': 'HBM bytes per block call, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE on the same '
+                                         'block shape (profiles/pmc_traffic_threshcc.json)'},
             'cpu_baseline': {'value': round(xs.size / t_cpu / 1e9, 4), 'unit': 'Gvoxel/s', 'cores': 1, 'kind': 'port',
                              'sample': 'first %d z-slices of the block' % xs.shape[0]},
             'bit_exact_vs_oracle_on_sample': bool(np.array_equal(lab, ref))}
