@@ -235,7 +235,8 @@ int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, 
  *   1.. in order of first appearance in a C-order scan (skimage's numbering), 0 elsewhere;
  *   *n_labels = their number.  A block without members leaves out unwritten and *n_labels = 0
  *   (the reference returns 0 and writes nothing).  on_device: 1 device pointers, 0 host.
- *   Blocks of fewer than 2^32 - 1 voxels.
+ *   Blocks of fewer than 2^32 - 1 voxels; a device input is 16-byte aligned when normalize = 1
+ *   (CTWS_EINVAL otherwise; torch / hipMalloc allocations are).
  */
 int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t* mask, int64_t nz, int64_t ny,
                               int64_t nx, int on_device, int mode, double threshold, int normalize, uint64_t* out,
