@@ -85,7 +85,7 @@ def split_blocks(block_list, n_jobs, consecutive=False):
     out, start = [], 0
     for j in range(n_jobs):
         n = q + (1 if j < r else 0)
-        out.append(list(range(start, start + n)))
+        out.append(list(block_list[start:start + n]))
         start += n
     return out
 

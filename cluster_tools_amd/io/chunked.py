@@ -320,6 +320,14 @@ class Group:
             raise KeyError(key)
         return Dataset(p, self.fmt) if self._is_dataset(p) else Group(p, self.fmt, self.mode)
 
+    def __delitem__(self, key):
+        # as h5py's `del f[key]`, so callers can drop a dataset without knowing the layout
+        p = os.path.join(self.path, key)
+        if not os.path.isdir(p):
+            raise KeyError(key)
+        import shutil
+        shutil.rmtree(p)
+
     def keys(self):
         return sorted(d for d in os.listdir(self.path) if os.path.isdir(os.path.join(self.path, d)))
 

@@ -79,8 +79,7 @@ def find_labeling(job_id, config_path):
     fu.log("saving results to %s/%s" % (config['assignment_path'], config['assignment_key']))
     with vu.file_reader(config['assignment_path']) as f:
         if config['assignment_key'] in f:
-            import shutil
-            shutil.rmtree(os.path.join(config['assignment_path'], config['assignment_key']))
+            del f[config['assignment_key']]
         ds = f.create_dataset(config['assignment_key'], shape=table.shape, dtype='uint64', compression='gzip',
                               chunks=(max(1, min(1000000, len(table))), 2))
         ds.n_threads = config.get('threads_per_job', 1)

@@ -11,7 +11,6 @@ consecutive.  Also as there: if any BlockFaces job found no pair, no pair is mer
 """
 import json
 import os
-import shutil
 import sys
 
 import numpy as np
@@ -82,7 +81,7 @@ def merge_assignments(job_id, config_path):
     fu.log("reducing the number of labels from %i to %i" % (n_labels, len(np.unique(label_assignments))))
     with vu.file_reader(config['output_path']) as f:
         if config['output_key'] in f:
-            shutil.rmtree(os.path.join(config['output_path'], config['output_key']))
+            del f[config['output_key']]
         ds = f.create_dataset(config['output_key'], shape=label_assignments.shape, dtype='uint64',
                               compression='gzip', chunks=(min(65334, n_labels),))
         ds[:] = label_assignments

@@ -104,16 +104,34 @@ def _gather_rows(rows, device):
     return np.concatenate([p[:s].cpu().numpy() for p, s in zip(parts, sizes)])
 
 
-def init_group(job_id, n_jobs, port, backend, device=None, timeout_s=900):
+def _agree(err, device, what):
+    """Every rank learns whether any rank failed in the phase just ended (an all-reduce of a
+    success flag instead of a bare barrier): a job that raised while writing would otherwise
+    leave its peers waiting in the barrier until the group's timeout.  Re-raises the local
+    error, or raises for a peer's."""
+    import torch
     import torch.distributed as dist
+    ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if err is not None:
+        raise err
+    if int(ok.item()) == 0:
+        raise RuntimeError("a watershed job of the group failed while %s" % what)
+
+
+def init_group(job_id, n_jobs, rendezvous, backend, device=None, timeout_s=900):
+    """rendezvous: a TCP port on 127.0.0.1 (int) or an init_method URL such as the file store
+    the watershed task hands its jobs (no port chosen ahead of the jobs that another process
+    could take in between)."""
+    import torch.distributed as dist
+    init = rendezvous if isinstance(rendezvous, str) else 'tcp://127.0.0.1:%d' % rendezvous
+    kw = dict(init_method=init, rank=job_id, world_size=n_jobs, timeout=timedelta(seconds=timeout_s))
     if backend == 'nccl':
         import torch
         torch.cuda.set_device(device)
-        dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=job_id, world_size=n_jobs,
-                                timeout=timedelta(seconds=timeout_s), device_id=torch.device('cuda', device))
+        dist.init_process_group('nccl', device_id=torch.device('cuda', device), **kw)
     else:
-        dist.init_process_group('gloo', init_method='tcp://127.0.0.1:%d' % port, rank=job_id, world_size=n_jobs,
-                                timeout=timedelta(seconds=timeout_s))
+        dist.init_process_group('gloo', **kw)
 
 
 def relabel_in_job(job_id, results, ds_out, tmp_folder, assignment_path, assignment_key, mapper,
@@ -150,42 +168,49 @@ def relabel_in_job(job_id, results, ds_out, tmp_folder, assignment_path, assignm
             tables[bid] = (keys[dup:], vals[dup:])
             yield bid, bb, mapper(lab, keys, vals)
 
-    write_blocks(ds_out, mapped(), log)
-    # this job's table rows in block order, with each block's row count
-    bids = sorted(tables)
-    np.save(rows_file(tmp_folder, job_id), np.stack([
-        np.concatenate([tables[b][0] for b in bids]) if bids else np.zeros(0, np.uint64),
-        np.concatenate([tables[b][1] for b in bids]) if bids else np.zeros(0, np.uint64)], axis=1))
-    np.save(rows_file(tmp_folder, job_id) + '.blocks.npy',
-            np.array([[b, len(tables[b][0])] for b in bids], np.int64).reshape(-1, 2))
-    dist.barrier()
+    err = None
+    try:
+        write_blocks(ds_out, mapped(), log)
+        # this job's table rows in block order, with each block's row count
+        bids = sorted(tables)
+        np.save(rows_file(tmp_folder, job_id), np.stack([
+            np.concatenate([tables[b][0] for b in bids]) if bids else np.zeros(0, np.uint64),
+            np.concatenate([tables[b][1] for b in bids]) if bids else np.zeros(0, np.uint64)], axis=1))
+        np.save(rows_file(tmp_folder, job_id) + '.blocks.npy',
+                np.array([[b, len(tables[b][0])] for b in bids], np.int64).reshape(-1, 2))
+    except Exception as e:  # noqa: BLE001 -- re-raised after the peers have been told
+        err = e
+    _agree(err, comm_dev, 'writing its blocks')
+    err = None
     if job_id == 0:
-        # the assignment table as FindLabeling writes it (rows sorted by old id = block order),
-        # assembled from the jobs' per-block row runs without a sort, and Write's maxId
-        runs = []
-        for j in range(dist.get_world_size()):
-            rows = np.load(rows_file(tmp_folder, j))
-            blocks = np.load(rows_file(tmp_folder, j) + '.blocks.npy')
-            start = 0
-            for b, n in blocks:
-                runs.append((int(b), rows[start:start + n]))
-                start += n
-        runs.sort(key=lambda r: r[0])
-        table = np.concatenate([r for _, r in runs]) if runs else np.zeros((0, 2), np.uint64)
-        if has_zero:
-            table = np.concatenate([np.zeros((1, 2), np.uint64), table])
-        table = np.ascontiguousarray(table, dtype=np.uint64)
-        with vu.file_reader(assignment_path) as f:
-            if assignment_key in f:
-                import shutil
-                shutil.rmtree(os.path.join(assignment_path, assignment_key), ignore_errors=True)
-            ds = f.create_dataset(assignment_key, shape=table.shape, dtype='uint64', compression='gzip',
-                                  chunks=(max(1, min(1000000, len(table))), 2))
-            ds.n_threads = 8
-            ds[:] = table
-        ds_out.attrs['maxId'] = int(table[:, 1].max()) if len(table) else 0
-        for j in range(dist.get_world_size()):
-            os.remove(rows_file(tmp_folder, j))
-            os.remove(rows_file(tmp_folder, j) + '.blocks.npy')
-    dist.barrier()
+        try:
+            # the assignment table as FindLabeling writes it (rows sorted by old id = block order),
+            # assembled from the jobs' per-block row runs without a sort, and Write's maxId
+            runs = []
+            for j in range(dist.get_world_size()):
+                rows = np.load(rows_file(tmp_folder, j))
+                blocks = np.load(rows_file(tmp_folder, j) + '.blocks.npy')
+                start = 0
+                for b, n in blocks:
+                    runs.append((int(b), rows[start:start + n]))
+                    start += n
+            runs.sort(key=lambda r: r[0])
+            table = np.concatenate([r for _, r in runs]) if runs else np.zeros((0, 2), np.uint64)
+            if has_zero:
+                table = np.concatenate([np.zeros((1, 2), np.uint64), table])
+            table = np.ascontiguousarray(table, dtype=np.uint64)
+            with vu.file_reader(assignment_path) as f:
+                if assignment_key in f:
+                    del f[assignment_key]
+                ds = f.create_dataset(assignment_key, shape=table.shape, dtype='uint64', compression='gzip',
+                                      chunks=(max(1, min(1000000, len(table))), 2))
+                ds.n_threads = 8
+                ds[:] = table
+            ds_out.attrs['maxId'] = int(table[:, 1].max()) if len(table) else 0
+            for j in range(dist.get_world_size()):
+                os.remove(rows_file(tmp_folder, j))
+                os.remove(rows_file(tmp_folder, j) + '.blocks.npy')
+        except Exception as e:  # noqa: BLE001
+            err = e
+    _agree(err, comm_dev, 'writing the assignment table')
     return n_new

@@ -96,17 +96,17 @@ def ws_task_setup(task, block_shape):
 
 
 def relabel_job_config(task, n_jobs):
-    """The in-job relabel of the local jobs: rendezvous port, group size and backend (RCCL when
-    every job owns a GPU, gloo when jobs share one; CTWS_JOB_DIST_BACKEND overrides)."""
-    import socket
+    """The in-job relabel of the local jobs: rendezvous, group size and backend (RCCL when
+    every job owns a GPU, gloo when jobs share one; CTWS_JOB_DIST_BACKEND overrides).  The
+    rendezvous is a file store in tmp_folder, fresh per run (a TCP port picked here could be
+    taken by another process before the jobs bind it)."""
+    import uuid
     from cluster_tools_amd.cluster_tasks import _count_gpus
-    with socket.socket() as sk:
-        sk.bind(('127.0.0.1', 0))
-        port = sk.getsockname()[1]
+    store = os.path.join(os.path.abspath(task.tmp_folder), 'relabel_rendezvous_%s' % uuid.uuid4().hex)
     n_gpus = _count_gpus()
     backend = 'nccl' if (n_gpus >= n_jobs and 'CTWS_DEVICE' not in os.environ) else 'gloo'
     backend = os.environ.get('CTWS_JOB_DIST_BACKEND', backend)
-    return {'n_jobs': n_jobs, 'port': port, 'backend': backend, 'tmp_folder': task.tmp_folder,
+    return {'n_jobs': n_jobs, 'rendezvous': 'file://' + store, 'backend': backend, 'tmp_folder': task.tmp_folder,
             'assignment_path': task.assignment_path, 'assignment_key': task.assignment_key}
 
 
@@ -389,7 +389,7 @@ def _run_blocks_relabel(job_id, blocking, ds_in, ds_out, mask, config, rel):
     group = []
 
     def start_group():
-        job_relabel.init_group(job_id, rel['n_jobs'], rel['port'], rel['backend'], device=_device())
+        job_relabel.init_group(job_id, rel['n_jobs'], rel['rendezvous'], rel['backend'], device=_device())
         group.append(True)
 
     keep, failed = [], None

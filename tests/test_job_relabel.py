@@ -62,9 +62,9 @@ def _reference(blocks):
     return vol, new, np.stack([u, np.arange(start, start + len(u), dtype=np.uint64)], 1)
 
 
-def _worker(rank, world, port, root):
+def _worker(rank, world, port, root, fail_rank=-1):
     from cluster_tools_amd.utils import volume_utils as vu
-    jr.init_group(rank, world, port, 'gloo')
+    jr.init_group(rank, world, port, 'gloo', timeout_s=120)
     try:
         blocks = _blocks()
         mine = [b for b in sorted(blocks) if b % world == rank]   # block_list[job::n_jobs]
@@ -74,6 +74,8 @@ def _worker(rank, world, port, root):
             results.append((b, bb, None if lab is None else lab.copy(), None if lab is None else np.unique(lab)))
 
         def mapper(lab, keys, vals):
+            if rank == fail_rank:
+                raise OSError("injected write failure")
             nz = lab != 0
             if len(keys):
                 lab[nz] = vals[np.searchsorted(keys, lab[nz])]
@@ -81,8 +83,14 @@ def _worker(rank, world, port, root):
 
         with vu.file_reader(os.path.join(root, 'ws.n5')) as f:
             ds = f['ws']
-            jr.relabel_in_job(rank, results, ds, root, os.path.join(root, 'ws.n5'), 'relabel_watershed', mapper,
-                              log=lambda m: None)
+            try:
+                jr.relabel_in_job(rank, results, ds, root, os.path.join(root, 'ws.n5'), 'relabel_watershed',
+                                  mapper, log=lambda m: None)
+            except Exception as e:
+                if fail_rank < 0:
+                    raise
+                with open(os.path.join(root, 'err_%d.txt' % rank), 'w') as fe:
+                    fe.write(str(e))
     finally:
         dist.destroy_process_group()
 
@@ -99,7 +107,8 @@ def test_two_jobs_relabel_like_relabel_workflow(tmp_path):
     root = str(tmp_path)
     with vu.file_reader(os.path.join(root, 'ws.n5')) as f:
         f.create_dataset('ws', shape=SHAPE, dtype='uint64', chunks=BLOCK)
-    tmp.spawn(_worker, args=(2, _free_port(), root), nprocs=2, join=True)
+    # the file-store rendezvous the watershed task hands its jobs (watershed.relabel_job_config)
+    tmp.spawn(_worker, args=(2, 'file://' + os.path.join(root, 'rendezvous'), root), nprocs=2, join=True)
     vol, new, table = _reference(_blocks())
     with vu.file_reader(os.path.join(root, 'ws.n5'), 'r') as f:
         got = f['ws'][:]
@@ -108,3 +117,19 @@ def test_two_jobs_relabel_like_relabel_workflow(tmp_path):
     np.testing.assert_array_equal(got, new)
     np.testing.assert_array_equal(got_table, table)
     assert not any(n.startswith('watershed_relabel_rows') for n in os.listdir(root))
+
+
+
+def test_a_job_failing_while_writing_fails_every_job_fast(tmp_path):
+    """a job that raises after the id exchange (here in its block mapping) must not
+    leave its peers in the final barrier until the group timeout: every job raises."""
+    import time
+    from cluster_tools_amd.utils import volume_utils as vu
+    root = str(tmp_path)
+    with vu.file_reader(os.path.join(root, 'ws.n5')) as f:
+        f.create_dataset('ws', shape=SHAPE, dtype='uint64', chunks=BLOCK)
+    t0 = time.time()
+    tmp.spawn(_worker, args=(2, _free_port(), root, 1), nprocs=2, join=True)
+    assert time.time() - t0 < 60
+    assert open(os.path.join(root, 'err_1.txt')).read() == "injected write failure"
+    assert "failed while writing its blocks" in open(os.path.join(root, 'err_0.txt')).read()

@@ -255,3 +255,15 @@ def test_keep_on_device_divides_free_memory_across_the_jobs_of_a_gpu(monkeypatch
     monkeypatch.setattr(torch.cuda, 'device_count', lambda: 2)   # 2 jobs per GPU now
     assert ws._keep_on_device(blocking, list(range(8)), cfg)
     assert not ws._keep_on_device(blocking, list(range(8)), dict(cfg, keep_on_device=False))
+
+
+def test_split_blocks_consecutive_keeps_block_ids():
+    """consecutive runs are runs of the block LIST (a ROI or a block_list_path
+    gives ids that are not 0..N-1), the round-robin split is block_list[j::n_jobs]
+    (cluster_tasks.py:328 of the reference)."""
+    from cluster_tools_amd.cluster_tasks import split_blocks
+    bl = [3, 4, 7, 8, 11, 12, 30]
+    runs = split_blocks(bl, 3, consecutive=True)
+    assert runs == [[3, 4, 7], [8, 11], [12, 30]]
+    assert sum(runs, []) == bl
+    assert split_blocks(bl, 3) == [[3, 8, 30], [4, 11], [7, 12]]

@@ -243,3 +243,32 @@ def test_watershed_low_res_mask(tmp_path):
     assert (raw == 0).any() and ((raw == 0) == (ref == 0)).all()
     vis, vim = vi_scores(raw, ref, [0])
     assert vis + vim <= 0.01, (vis, vim)
+
+
+@pytest.mark.parametrize('with_mask', [False, True])
+def test_watershed_workflow_roi_relabel_in_job(tmp_path, with_mask):
+    """the in-job relabel hands each job a consecutive run of the block list; with a
+    ROI that list is not 0..N-1.  Both relabel modes must process exactly the ROI's blocks and
+    agree on the volume, the table and maxId."""
+    from cluster_tools_amd.watershed import WatershedWorkflow
+    cfg_dir, inp, x, c = _setup(tmp_path, 'ws_3d', with_mask)
+    g = json.loads((tmp_path / 'configs' / 'global.config').read_text())
+    g['roi_begin'], g['roi_end'] = [10, 64, 0], [40, 128, 128]
+    (tmp_path / 'configs' / 'global.config').write_text(json.dumps(g))
+    mask_kw = dict(mask_path=inp, mask_key='mask') if with_mask else {}
+    res = {}
+    for rij in (True, False):
+        out = str(tmp_path / ('ws_%d.n5' % rij))
+        wf = WatershedWorkflow(input_path=inp, input_key='boundaries', output_path=out, output_key='ws',
+                               config_dir=cfg_dir, tmp_folder=str(tmp_path / ('tmp_%d' % rij)), target='local',
+                               max_jobs=2, relabel_in_job=rij, **mask_kw)
+        _build(wf, tmp_path / ('tmp_%d' % rij))
+        with vu.file_reader(out, 'r') as f:
+            res[rij] = (f['ws'][:], f['relabel_watershed'][:], f['ws'].attrs['maxId'])
+    np.testing.assert_array_equal(res[True][0], res[False][0])
+    np.testing.assert_array_equal(res[True][1], res[False][1])
+    assert res[True][2] == res[False][2]
+    vol = res[True][0]
+    # blocks outside the ROI are never written
+    assert not vol[:10].any() and not vol[:, :64].any()
+    assert vol[10:, 64:].any()
