@@ -15,6 +15,10 @@ CTWS_BLOCK_WRITTEN, CTWS_BLOCK_SKIPPED_MASK, CTWS_BLOCK_EMPTY, CTWS_BLOCK_EMPTY_
 
 _DTYPE_CODES = {np.dtype('uint8'): CTWS_U8, np.dtype('uint16'): CTWS_U16,
                 np.dtype('float32'): CTWS_F32, np.dtype('float64'): CTWS_F64}
+# ctws_threshold_components_ex also takes the integer dtypes (include/ctws.h CTWS_I8 .. CTWS_U64)
+TC_DTYPE_CODES = dict(_DTYPE_CODES)
+TC_DTYPE_CODES.update({np.dtype('int8'): 5, np.dtype('int16'): 6, np.dtype('int32'): 7, np.dtype('uint32'): 8,
+                       np.dtype('int64'): 9, np.dtype('uint64'): 10})
 
 
 class CtwsCfg(C.Structure):

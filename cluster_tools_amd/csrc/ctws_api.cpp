@@ -122,7 +122,7 @@ struct ctws_handle {
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
     // ThresholdedComponents (k_threshcc.hip): forest, root bitmap, chunk counts / offsets, word
     // offsets, min / max + any flag, host-pointer staging
-    DevBuf tc_P, tc_bits, tc_cnt, tc_offs, tc_woff, tc_red, tc_in, tc_mask, tc_out;
+    DevBuf tc_P, tc_bits, tc_cnt, tc_offs, tc_woff, tc_red, tc_in, tc_mask, tc_out, tc_raw, tc_tmp, tc_taps;
     // evaluation (k_eval.hip): gt / seg / pair hash tables with counts, state, sums, staging
     DevBuf ev_ka, ev_ca, ev_kb, ev_cb, ev_kp, ev_cp, ev_state, ev_out, ev_stage;
     int64_t ev_cap_a = 0, ev_cap_b = 0, ev_cap_p = 0;
@@ -2290,7 +2290,7 @@ void ctws_close(ctws_handle* h) {
                     h->fs_vals.p, h->fs_sorted.p, h->fs_off.p, h->fs_tmp.p, h->ev_ka.p, h->ev_ca.p, h->ev_kb.p,
                     h->ev_cb.p, h->ev_kp.p, h->ev_cp.p, h->ev_state.p, h->ev_out.p, h->ev_stage.p,
                     w.fplat, w.plev, w.fseed, h->tc_P.p, h->tc_bits.p, h->tc_cnt.p, h->tc_offs.p, h->tc_woff.p,
-                    h->tc_red.p, h->tc_in.p, h->tc_mask.p, h->tc_out.p};
+                    h->tc_red.p, h->tc_in.p, h->tc_mask.p, h->tc_out.p, h->tc_raw.p, h->tc_tmp.p, h->tc_taps.p};
     for (void* p : ptrs)
         if (p) hipFree(p);
     for (auto e : h->events) hipEventDestroy(e);
@@ -2700,10 +2700,52 @@ int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, 
 
 
 // ---- ThresholdedComponentsWorkflow: BlockComponents (k_threshcc.hip) -----------------------
+extern "C++" {
+namespace {
+size_t tc_dtype_size(int dt) {
+    switch (dt) {
+        case CTWS_U8: case CTWS_I8: return 1;
+        case CTWS_U16: case CTWS_I16: return 2;
+        case CTWS_F32: case CTWS_I32: case CTWS_U32: return 4;
+        case CTWS_F64: case CTWS_I64: case CTWS_U64: return 8;
+        default: return 0;
+    }
+}
+// dispatch a k_tc_* template over the dataset dtype (float32 is the caller's own case)
+template <class F>
+void tc_dispatch(int dt, F f) {
+    switch (dt) {
+        case CTWS_U8: f((const uint8_t*)nullptr); break;
+        case CTWS_I8: f((const int8_t*)nullptr); break;
+        case CTWS_U16: f((const uint16_t*)nullptr); break;
+        case CTWS_I16: f((const int16_t*)nullptr); break;
+        case CTWS_U32: f((const uint32_t*)nullptr); break;
+        case CTWS_I32: f((const int32_t*)nullptr); break;
+        case CTWS_U64: f((const uint64_t*)nullptr); break;
+        case CTWS_I64: f((const int64_t*)nullptr); break;
+        case CTWS_F64: f((const double*)nullptr); break;
+        default: break;
+    }
+}
+}  // namespace
+}  // extern "C++"
+
 int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t* mask, int64_t nz, int64_t ny,
                               int64_t nx, int on_device, int mode, double threshold, int normalize, uint64_t* out,
                               int64_t* n_labels) {
-    if (!h || !n_labels || nz < 0 || ny < 0 || nx < 0 || mode < 0 || mode > 2) return CTWS_EINVAL;
+    return ctws_threshold_components_ex(h, input, CTWS_F32, mask, nz, ny, nx, on_device, mode, threshold, normalize,
+                                        0.0, out, n_labels);
+}
+
+int ctws_threshold_components_ex(ctws_handle* h, const void* input, int dtype, const uint8_t* mask, int64_t nz,
+                                 int64_t ny, int64_t nx, int on_device, int mode, double threshold, int normalize,
+                                 double sigma, uint64_t* out, int64_t* n_labels) {
+    if (!h || !n_labels || nz < 0 || ny < 0 || nx < 0 || mode < 0 || mode > 2 || !(sigma >= 0.0)) return CTWS_EINVAL;
+    const size_t esz = tc_dtype_size(dtype);
+    if (!esz) {
+        h->err = "ctws_threshold_components_ex: unsupported dtype";
+        return CTWS_EINVAL;
+    }
     const int64_t n = nz * ny * nx;
     if ((!input || !out) && n > 0) return CTWS_EINVAL;
     h->err.clear();
@@ -2714,15 +2756,24 @@ int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t*
         h->err = "ctws_threshold_components: block too large (needs < 2^32 - 1 voxels)";
         return CTWS_EINVAL;
     }
+    std::vector<double> taps;
+    if (sigma > 0.0) {
+        taps = gaussian_taps(sigma);
+        const int64_t rad = (int64_t)taps.size() / 2;
+        if (nz < rad + 1 || ny < rad + 1 || nx < rad + 1) {  // vigra: "kernel longer than line"
+            h->err = "ctws_threshold_components_ex: block shorter than the Gaussian radius + 1 along an axis";
+            return CTWS_EINVAL;
+        }
+    }
     int r;
-    const float* din = input;
+    const void* dsrc = input;
     const uint8_t* dmask = mask;
     uint64_t* dout = out;
     if (!on_device) {
-        if ((r = grow(h, h->tc_in, sizeof(float) * (size_t)n)) != CTWS_OK) return r;
+        if ((r = grow(h, h->tc_raw, esz * (size_t)n)) != CTWS_OK) return r;
         if ((r = grow(h, h->tc_out, sizeof(uint64_t) * (size_t)n)) != CTWS_OK) return r;
-        HIPCHK(hipMemcpyAsync(h->tc_in.p, input, sizeof(float) * (size_t)n, hipMemcpyHostToDevice, h->stream));
-        din = (const float*)h->tc_in.p;
+        HIPCHK(hipMemcpyAsync(h->tc_raw.p, input, esz * (size_t)n, hipMemcpyHostToDevice, h->stream));
+        dsrc = h->tc_raw.p;
         dout = (uint64_t*)h->tc_out.p;
         if (mask) {
             if ((r = grow(h, h->tc_mask, (size_t)n)) != CTWS_OK) return r;
@@ -2740,6 +2791,8 @@ int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t*
     uint32_t* red = (uint32_t*)h->tc_red.p;  // [0] min, [1] max (ordered float bits), [2] any member
     const uint32_t init[3] = {0xFFFFFFFFu, 0u, 0u};
     HIPCHK(hipMemcpyAsync(red, init, sizeof(init), hipMemcpyHostToDevice, h->stream));
+    const unsigned gs = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);  // grid of the streaming passes
+    const unsigned gm = (unsigned)std::min<int64_t>((n + 4095) / 4096, 256);  // k_tc_minmax
     TcParams p;
     p.nz = (int)nz;
     p.ny = (int)ny;
@@ -2747,13 +2800,62 @@ int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t*
     p.mode = mode;
     p.normalize = normalize ? 1 : 0;
     p.thr = (float)threshold;
-    if (normalize) {
+    const float* din = (const float*)dsrc;  // the float32 values k_tc_tile thresholds
+    const bool raw_cmp = !normalize && sigma == 0.0 && dtype != CTWS_F32;
+    if (raw_cmp || dtype != CTWS_F32) {
+        if ((r = grow(h, h->tc_in, sizeof(float) * (size_t)n)) != CTWS_OK) return r;
+        float* f = (float*)h->tc_in.p;
+        if (raw_cmp) {
+            // numpy's float64 comparison of the raw values; k_tc_tile tests the 0 / 1 result
+            tc_dispatch(dtype, [&](auto tp) {
+                using T = std::remove_cv_t<std::remove_pointer_t<decltype(tp)>>;
+                k_tc_raw_members<T><<<gs, 256, 0, h->stream>>>((const T*)dsrc, n, mode, threshold, f);
+            });
+            p.mode = 0;
+            p.thr = 0.5f;
+        } else {
+            tc_dispatch(dtype, [&](auto tp) {
+                using T = std::remove_cv_t<std::remove_pointer_t<decltype(tp)>>;
+                k_tc_to_f32<T><<<gs, 256, 0, h->stream>>>((const T*)dsrc, n, f);
+            });
+        }
+        LAUNCHCHK();
+        din = f;
+    }
+    if (sigma > 0.0) {
+        // x (float32) -> [normalize] -> Gaussian z, y, x -> normalized by k_tc_tile
+        if ((r = grow(h, h->tc_tmp, sizeof(float) * (size_t)n)) != CTWS_OK) return r;
+        if ((r = grow(h, h->tc_taps, sizeof(double) * taps.size())) != CTWS_OK) return r;
+        if (din == (const float*)dsrc) {  // float32 input: work on a copy, the caller's buffer is const
+            if ((r = grow(h, h->tc_in, sizeof(float) * (size_t)n)) != CTWS_OK) return r;
+            HIPCHK(hipMemcpyAsync(h->tc_in.p, din, sizeof(float) * (size_t)n, hipMemcpyDeviceToDevice, h->stream));
+            din = (const float*)h->tc_in.p;
+        }
+        float* a = (float*)h->tc_in.p;
+        float* b = (float*)h->tc_tmp.p;
+        if (normalize) {
+            k_tc_minmax<<<gm, 256, 0, h->stream>>>(a, n, red);
+            k_tc_normalize<<<gs, 256, 0, h->stream>>>(a, n, red);
+            HIPCHK(hipMemcpyAsync(red, init, sizeof(init), hipMemcpyHostToDevice, h->stream));
+        }
+        // (pageable upload: the host vector is gone after this call returns, the copy is not)
+        HIPCHK(hipMemcpy(h->tc_taps.p, taps.data(), sizeof(double) * taps.size(), hipMemcpyHostToDevice));
+        const int rad = (int)taps.size() / 2;
+        for (int axis = 0; axis < 3; ++axis) {
+            k_tc_gauss<<<gs, 256, 0, h->stream>>>(a, b, (int)nz, (int)ny, (int)nx, axis,
+                                                  (const double*)h->tc_taps.p, rad);
+            std::swap(a, b);
+        }
+        LAUNCHCHK();
+        din = a;
+        p.normalize = 1;  // vu.normalize of the smoothed block
+    }
+    if (p.normalize) {
         if (reinterpret_cast<uintptr_t>(din) % 16 != 0) {
             h->err = "ctws_threshold_components: input not 16-byte aligned";
             return CTWS_EINVAL;
         }
-        const unsigned g = (unsigned)std::min<int64_t>((n + 4095) / 4096, 256);
-        k_tc_minmax<<<g, 256, 0, h->stream>>>(din, n, red);
+        k_tc_minmax<<<gm, 256, 0, h->stream>>>(din, n, red);
     }
     const int64_t tiles = ((nx + 63) / 64) * ((ny + 7) / 8) * ((nz + 7) / 8);
     uint32_t* P = (uint32_t*)h->tc_P.p;

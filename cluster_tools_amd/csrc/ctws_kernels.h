@@ -269,5 +269,11 @@ __global__ void k_tc_merge(TcParams, uint32_t*);
 __global__ void k_tc_roots(const uint32_t*, int64_t, uint64_t*);
 __global__ void k_tc_wordoff(const uint64_t*, int64_t, const uint64_t*, uint32_t*);
 __global__ void k_tc_label(const uint32_t*, int64_t, const uint64_t*, const uint32_t*, uint64_t*);
+template <class T>
+__global__ void k_tc_to_f32(const T*, int64_t, float*);
+template <class T>
+__global__ void k_tc_raw_members(const T*, int64_t, int, double, float*);
+__global__ void k_tc_normalize(float*, int64_t, const uint32_t*);
+__global__ void k_tc_gauss(const float*, float*, int, int, int, int, const double*, int);
 
 }  // namespace ctws

@@ -70,6 +70,74 @@ __global__ void __launch_bounds__(256) k_tc_minmax(const float* __restrict__ v, 
     }
 }
 
+// ---- inputs other than a raw float32 block (ctws_threshold_components_ex) ---------------------
+// astype('float32') of the dataset's values (numpy rounds to nearest, as the conversions here)
+template <class T>
+__global__ void __launch_bounds__(256) k_tc_to_f32(const T* __restrict__ in, int64_t n, float* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        out[i] = (float)in[i];
+}
+// the raw comparison of `_cc_block_with_mask` / the channel sum (block_components.py:199-220) for
+// a float64 or integer dataset: numpy compares `x > python float` in float64 there (NEP 50; every
+// integer converts to the nearest double, as numpy's cast); members become 1.0f, the others 0.0f
+// (k_tc_tile then tests > 0.5)
+template <class T>
+__global__ void __launch_bounds__(256) k_tc_raw_members(const T* __restrict__ in, int64_t n, int mode, double thr,
+                                                        float* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const double v = (double)in[i];
+        const bool m = mode == 0 ? v > thr : (mode == 1 ? v < thr : v == thr);
+        out[i] = m ? 1.0f : 0.0f;
+    }
+}
+#define CTWS_TC_DT(T)                                                                              \
+    template __global__ void k_tc_to_f32<T>(const T*, int64_t, float*);                            \
+    template __global__ void k_tc_raw_members<T>(const T*, int64_t, int, double, float*);
+CTWS_TC_DT(uint8_t)
+CTWS_TC_DT(int8_t)
+CTWS_TC_DT(uint16_t)
+CTWS_TC_DT(int16_t)
+CTWS_TC_DT(uint32_t)
+CTWS_TC_DT(int32_t)
+CTWS_TC_DT(uint64_t)
+CTWS_TC_DT(int64_t)
+CTWS_TC_DT(double)
+#undef CTWS_TC_DT
+
+// vu.normalize in place (the normalize before the prefilter of a masked block): v - min, divided
+// by fl(max - min) when positive, in float32 (min / max from k_tc_minmax)
+__global__ void __launch_bounds__(256) k_tc_normalize(float* __restrict__ v, int64_t n, const uint32_t* __restrict__ mm) {
+    const float vmin = unordf(mm[0]), range = unordf(mm[1]) - vmin;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        float t = v[i] - vmin;
+        if (range > 0.0f) t = t / range;
+        v[i] = t;
+    }
+}
+
+// the prefilter's vigra gaussianSmoothing along one axis (vu.apply_filter, block_components.py:161
+// / :210): out[x] = float(sum over p = x - r .. x + r ascending of taps[r + x - p] * in[reflect(p)])
+// in double without FMA contraction (the Makefile's -ffp-contract=off), as the oracle's
+// convolve_line_reflect and k_gauss.hip.  One thread per output voxel: the prefilter is an
+// option of a small workflow, not a hot path (lanes along x keep the loads coalesced).
+__global__ void __launch_bounds__(256) k_tc_gauss(const float* __restrict__ in, float* __restrict__ out, int nz,
+                                                  int ny, int nx, int axis, const double* __restrict__ taps, int r) {
+    const int64_t n = (int64_t)nz * ny * nx;
+    const int64_t st = axis == 0 ? (int64_t)ny * nx : (axis == 1 ? nx : 1);
+    const int L = axis == 0 ? nz : (axis == 1 ? ny : nx);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int64_t rest = i % (int64_t)nx, row = i / nx;
+        const int c = axis == 2 ? (int)rest : (axis == 1 ? (int)(row % ny) : (int)(row / ny));
+        const int64_t base = i - (int64_t)c * st;
+        double sum = 0.0;
+        for (int p = c - r; p <= c + r; ++p) {
+            const int q = p < 0 ? -p : (p >= L ? 2 * (L - 1) - p : p);
+            sum += taps[r + c - p] * (double)in[base + (int64_t)q * st];
+        }
+        out[i] = (float)sum;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_tc_tile(const float* __restrict__ v, const uint8_t* __restrict__ mask,
                                                  TcParams p, const uint32_t* __restrict__ mm,
                                                  uint32_t* __restrict__ P, uint32_t* __restrict__ any) {

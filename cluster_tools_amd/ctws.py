@@ -49,7 +49,7 @@ def lib():
             L.ctws_last_error.restype = C.c_char_p
             for fn in ('ctws_ws_blocks', 'ctws_ws_blocks_device', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
                     'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end', 'ctws_threshold_components',
-                    'ctws_ufd_find'):
+                    'ctws_threshold_components_ex', 'ctws_ufd_find'):
                 getattr(L, fn).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_last_timings.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
             L.ctws_unique_u64.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
@@ -63,6 +63,9 @@ def lib():
             L.ctws_threshold_components.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
                                                     C.c_int64, C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p,
                                                     C.POINTER(C.c_int64)]
+            L.ctws_threshold_components_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int64,
+                                                       C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_double, C.c_int,
+                                                       C.c_double, C.c_void_p, C.POINTER(C.c_int64)]
             L.ctws_eval_begin.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
             L.ctws_eval_add.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
             L.ctws_eval_end.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
@@ -80,7 +83,7 @@ EXPORTED_SYMBOLS = ('ctws_abi_version', 'ctws_open', 'ctws_close', 'ctws_last_er
                     'ctws_ws_blocks_device', 'ctws_last_timings', 'ctws_unique_u64', 'ctws_unique_counts_u64', 'ctws_set_table_u64', 'ctws_lookup_u64',
                     'ctws_debug_set_stop', 'ctws_debug_read', 'ctws_debug_sqrt_int', 'ctws_ws_from_seeds', 'ctws_ws_from_seeds_device',
                     'ctws_eval_begin', 'ctws_eval_add', 'ctws_eval_end', 'ctws_threshold_components',
-                    'ctws_ufd_find')
+                    'ctws_threshold_components_ex', 'ctws_ufd_find')
 
 
 def ufd_find(n_labels, pairs):
@@ -393,13 +396,19 @@ class Handle:
     # ---- ThresholdedComponentsWorkflow kernels --------------------------------------------
     THRESHOLD_MODES = ('greater', 'less', 'equal')
 
-    def threshold_components(self, block, threshold, mode='greater', mask=None, normalize=True):
+    def threshold_components(self, block, threshold, mode='greater', mask=None, normalize=True, sigma=0.):
         """BlockComponents of one 3-D block on the GPU (block_components.py:143-230): members =
-        (normalized) block `mode` threshold, inside the mask; their 26-connected components
-        numbered 1.. in C-order of first appearance (skimage.morphology.label).  numpy in
-        (float32; other dtypes are converted), -> (uint64 labels, n_labels); n_labels 0 = no
-        member (the labels are then all 0)."""
-        block = np.ascontiguousarray(block, dtype=np.float32)
+        block `mode` threshold inside the mask, their 26-connected components numbered 1.. in
+        C-order of first appearance (skimage.morphology.label).  `block` is the dataset's values
+        in its own dtype (float32 / float64 / any 8-64 bit integer): normalize = vu.normalize
+        first (float32); sigma > 0 = vu.normalize(gaussianSmoothing(float32 x, sigma)); raw
+        values are compared as numpy compares them with a Python float (include/ctws.h
+        ctws_threshold_components_ex).  -> (uint64 labels, n_labels); n_labels 0 = no member
+        (the labels are then all 0)."""
+        from ._abi import TC_DTYPE_CODES
+        block = np.ascontiguousarray(block)
+        if block.dtype not in TC_DTYPE_CODES:
+            raise ValueError("threshold_components: unsupported dtype %s" % block.dtype)
         assert block.ndim == 3, block.shape
         if mode not in self.THRESHOLD_MODES:
             raise RuntimeError("Thresholding Mode %s not supported" % mode)
@@ -410,10 +419,11 @@ class Handle:
             mp = mask.ctypes.data
         out = np.zeros(block.shape, dtype=np.uint64)
         n = C.c_int64(0)
-        self._check(lib().ctws_threshold_components(self._h, block.ctypes.data, mp, *block.shape, 0,
-                                                    self.THRESHOLD_MODES.index(mode), float(threshold),
-                                                    1 if normalize else 0, out.ctypes.data, C.byref(n)),
-                    'ctws_threshold_components')
+        self._check(lib().ctws_threshold_components_ex(self._h, block.ctypes.data, TC_DTYPE_CODES[block.dtype], mp,
+                                                       *block.shape, 0, self.THRESHOLD_MODES.index(mode),
+                                                       float(threshold), 1 if normalize else 0, float(sigma),
+                                                       out.ctypes.data, C.byref(n)),
+                    'ctws_threshold_components_ex')
         return out, int(n.value)
 
     def threshold_components_device(self, block, threshold, mode='greater', mask=None, normalize=True, out=None):

@@ -6,7 +6,10 @@ Per block the job reads the input (the next block ahead on a thread), calls
 ctws_threshold_components (k_threshcc.hip: normalize, threshold, mask, LDS-tiled union-find,
 skimage numbering) and writes the labels of a non-empty block; the per-block offsets
 (`max + 1`, 0 for an empty block) go to `connected_components_offsets_<job>.json` as in the
-reference.  The Gaussian prefilter (sigma_prefilter > 0) is not implemented and raises.
+reference.  The block crosses to the GPU in the dataset's dtype: raw values are thresholded as
+numpy compares them with the Python float threshold, and the Gaussian prefilter
+(sigma_prefilter > 0, vigra gaussianSmoothing + normalize) runs on the GPU too
+(ctws_threshold_components_ex).
 """
 import json
 import os
@@ -125,9 +128,7 @@ def _read_block(blocking, block_id, ds_in, mask, channel):
 def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config):
     """`_cc_block[_with_mask]` for every block of the job -> {block_id: offset}."""
     from cluster_tools_amd import ctws
-    sigma = config.get('sigma_prefilter', 0)
-    if sigma > 0:
-        raise NotImplementedError("sigma_prefilter > 0 (vigra gaussianSmoothing) is not implemented")
+    sigma = float(config.get('sigma_prefilter', 0) or 0)
     threshold, mode = config['threshold'], config['threshold_mode']
     channel = config.get('channel', None)
     offsets = {}
@@ -142,10 +143,12 @@ def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config):
                 offsets[block_id] = 0
                 fu.log_block_success(block_id)
                 continue
-            # the unmasked, single-channel block is normalized first (vu.normalize); the masked
-            # and multi-channel ones are thresholded raw (sigma 0)
-            labels, n = h.threshold_components(b['input'], threshold, mode, mask=b['mask'],
-                                               normalize=(mask is None and channel is None))
+            # normalized first: the unmasked single-channel block (`_cc_block`,
+            # block_components.py:150-151) and, before its prefilter, a masked block (:208-209);
+            # otherwise raw values (sigma 0) or the raw channel sum smoothed (:160-162)
+            prenorm = (mask is None and channel is None) or (mask is not None and sigma > 0)
+            labels, n = h.threshold_components(b['input'], threshold, mode, mask=b['mask'], normalize=prenorm,
+                                               sigma=sigma)
             if n:
                 ds_out[b['bb']] = labels
             offsets[block_id] = n + 1 if n else 0

@@ -50,37 +50,40 @@ class MergeOffsetsLSF(MergeOffsetsBase, LSFTask):
     pass
 
 
+def scan_block_counts(counts):
+    """{block_id: count} -> (offsets, empty_blocks, n_labels), everything in increasing block id
+    order: offsets = the exclusive prefix sum of the counts (a block's count is its `max + 1`,
+    0 when empty), empty_blocks = the positions whose count is 0, n_labels = the total + 1, which
+    is the reference's `last offset + last count + 1` (merge_offsets.py:111-122)."""
+    ids = sorted(int(b) for b in counts)
+    c = np.array([int(counts[b]) for b in ids], dtype=np.uint64)
+    offs = np.zeros(len(c), dtype=np.uint64)
+    if len(c) > 1:
+        np.cumsum(c[:-1], out=offs[1:])
+    return [int(o) for o in offs], np.flatnonzero(c == 0).tolist(), int(c.sum()) + 1
+
+
 def merge_offsets(job_id, config_path):
-    """Job entry (merge_offsets.py:83-131): block-id order, exclusive cumulative sum of the
-    per-block `max + 1`; n_labels = last offset + last count + 1."""
+    """Job entry (merge_offsets.py:83-131): the BlockComponents jobs' count files -> one scan."""
     fu.log("start processing job %i" % job_id)
     fu.log("reading config from %s" % config_path)
     with open(config_path) as f:
         config = json.load(f)
-    offsets = {}
-    for block_job_id in range(config['n_jobs']):
-        path = os.path.join(config['tmp_folder'], '%s_%i.json' % (config['save_prefix'], block_job_id))
+    counts = {}
+    for j in range(config['n_jobs']):
+        path = os.path.join(config['tmp_folder'], '%s_%i.json' % (config['save_prefix'], j))
         with open(path) as f:
-            offsets.update(json.load(f))
+            counts.update({int(b): int(v) for b, v in json.load(f).items()})
         os.remove(path)
-    blocks = [int(b) for b in offsets.keys()]
-    offset_list = list(offsets.values())
     n_blocks = config['n_blocks']
-    assert len(blocks) == len(offset_list) == n_blocks
+    assert len(counts) == n_blocks, (len(counts), n_blocks)
     fu.log("merging offsets for %i blocks" % n_blocks)
-    key_sort = np.argsort(blocks)
-    offset_list = np.array([offset_list[k] for k in key_sort], dtype='uint64')
-    last_offset = offset_list[-1]
-    empty_blocks = np.where(offset_list == 0)[0].tolist()
-    offset_list = np.roll(offset_list, 1)
-    offset_list[0] = 0
-    offset_list = np.cumsum(offset_list).tolist()
-    n_labels = int(offset_list[-1] + last_offset + 1)
+    offsets, empty_blocks, n_labels = scan_block_counts(counts)
     fu.log("number of empty blocks: %i / %i" % (len(empty_blocks), n_blocks))
     fu.log("total number of labels: %i" % n_labels)
     fu.log("dumping offsets to %s" % config['save_path'])
     with open(config['save_path'], 'w') as f:
-        json.dump({'offsets': offset_list, 'empty_blocks': empty_blocks, 'n_labels': n_labels}, f)
+        json.dump({'offsets': offsets, 'empty_blocks': empty_blocks, 'n_labels': n_labels}, f)
     fu.log_job_success(job_id)
 
 

@@ -71,6 +71,13 @@ extern "C" {
 #define CTWS_U16 2
 #define CTWS_F32 3
 #define CTWS_F64 4
+/* further dtypes of ctws_threshold_components_ex (BlockComponents thresholds the raw dataset) */
+#define CTWS_I8  5
+#define CTWS_I16 6
+#define CTWS_I32 7
+#define CTWS_U32 8
+#define CTWS_I64 9
+#define CTWS_U64 10
 
 /* agglomerate_channels */
 #define CTWS_AGG_MEAN 0
@@ -241,6 +248,22 @@ int ctws_lookup_u64(ctws_handle* h, uint64_t* labels, int64_t n, int on_device, 
 int ctws_threshold_components(ctws_handle* h, const float* input, const uint8_t* mask, int64_t nz, int64_t ny,
                               int64_t nx, int on_device, int mode, double threshold, int normalize, uint64_t* out,
                               int64_t* n_labels);
+/*
+ * ctws_threshold_components_ex: the same for any dtype of the dataset and with the Gaussian
+ * prefilter (block_components.py:150-171 `_cc_block`, :198-222 `_cc_block_with_mask`):
+ *   x = input (dtype: CTWS_U8 .. CTWS_U64); if normalize: x = vu.normalize(x) (float32);
+ *   if sigma > 0: x = vu.normalize(gaussianSmoothing(float32(x), sigma)) (vigra: radius
+ *   int(3 sigma + 0.5), reflect border, double accumulation, float32 between the axes);
+ *   members = x `mode` threshold.  The comparison is numpy's for `x > python float`: float32
+ *   against the threshold rounded to float32 when x is float32 (normalized, smoothed or a
+ *   float32 dataset), float64 otherwise (float64 and integer datasets, NEP 50).  The caller
+ *   passes normalize = 1 for an unmasked single-channel block (`_cc_block` normalizes the raw
+ *   block) and for a masked block with sigma > 0 (`_cc_block_with_mask` normalizes before the
+ *   filter).  A line shorter than radius + 1 along any axis is refused as vigra refuses it.
+ */
+int ctws_threshold_components_ex(ctws_handle* h, const void* input, int dtype, const uint8_t* mask, int64_t nz,
+                                 int64_t ny, int64_t nx, int on_device, int mode, double threshold, int normalize,
+                                 double sigma, uint64_t* out, int64_t* n_labels);
 /*
  * MergeAssignments (thresholded_components/merge_assignments.py:125-130): out[i] = the
  * representative of label i after merging the (a, b) rows of pairs (n_pairs x 2, C order) into

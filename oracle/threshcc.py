@@ -2,7 +2,8 @@
 
 Restates, for the parity tests of k_threshcc.hip / ctws_ufd_find and the task chain:
   block_components   thresholded_components/block_components.py:143-230 (`_cc_block`,
-                     `_cc_block_with_mask`) with utils/volume_utils.py:113-120 (normalize) and
+                     `_cc_block_with_mask`) with utils/volume_utils.py:113-120 (normalize), the
+                     sigma_prefilter Gaussian (vigra restatement of the C++ oracle) and
                      skimage.morphology.label (full 26-connectivity, background 0; labels in
                      order of first appearance in a C-order scan)
   merge_offsets      thresholded_components/merge_offsets.py:96-130
@@ -51,10 +52,31 @@ def label26(members):
     return new[lab], int(len(ids))
 
 
-def members(block, threshold, mode='greater', mask=None, normalize_input=True):
-    """The thresholded block of `_cc_block` (normalize) / `_cc_block_with_mask` (raw values)."""
-    x = normalize(block) if normalize_input else np.asarray(block, dtype='float32')
-    thr = np.float32(threshold)
+def gaussian(x, sigma):
+    """vu.apply_filter(x, 'gaussianSmoothing', sigma) with a scalar sigma: vigra's
+    gaussianSmoothing (fastfilters is absent in the reference env, volume_utils.py:15-20) on the
+    float32 values -- the oracle's C++ restatement (ctws_oracle.cpp gaussian_smoothing)."""
+    from oracle import oracle as O
+    return O.gaussian_smoothing(np.ascontiguousarray(x, dtype='float32'), float(sigma))
+
+
+def members(block, threshold, mode='greater', mask=None, normalize_input=True, sigma=0.):
+    """The thresholded block of `_cc_block` (block_components.py:150-171: the single-channel
+    block normalized, a channel sum raw; with sigma the Gaussian and a normalize) and
+    `_cc_block_with_mask` (:198-222: raw values; with sigma normalize, Gaussian, normalize).
+    The comparison is the reference's `input_ > threshold` with a Python float, i.e. numpy's
+    promotion: float32 values against the threshold as float32, float64 and integer values in
+    float64."""
+    x = block
+    if mask is None:
+        if normalize_input:
+            x = normalize(x)
+        if sigma > 0:
+            x = normalize(gaussian(x, sigma))
+    elif sigma > 0:
+        x = normalize(gaussian(normalize(x), sigma))
+    x = np.asarray(x)
+    thr = float(threshold)
     if mode == 'greater':
         m = x > thr
     elif mode == 'less':
@@ -68,10 +90,10 @@ def members(block, threshold, mode='greater', mask=None, normalize_input=True):
     return m
 
 
-def block_components(block, threshold, mode='greater', mask=None, normalize_input=True):
+def block_components(block, threshold, mode='greater', mask=None, normalize_input=True, sigma=0.):
     """-> (uint64 labels, n_labels); n_labels 0 = no member (the reference returns offset 0 and
     writes nothing; the labels are all 0 here)."""
-    m = members(block, threshold, mode, mask, normalize_input)
+    m = members(block, threshold, mode, mask, normalize_input, sigma)
     if not m.any():
         return np.zeros(m.shape, dtype='uint64'), 0
     return label26(m)
@@ -140,7 +162,7 @@ def boost_ufd_find(n, pairs):
     return np.array([find(i) for i in range(n)], dtype='uint64')
 
 
-def thresholded_components(volume, blocking, threshold, mode='greater', mask=None, normalize_input=None):
+def thresholded_components(volume, blocking, threshold, mode='greater', mask=None, normalize_input=None, sigma=0.):
     """The whole workflow on an in-memory volume (one job per task):
     -> (segmentation uint64, assignments uint64, offsets dict).  normalize_input None: as the
     reference, normalize the unmasked blocks only; False: the summed channels of a 4-D input
@@ -155,10 +177,11 @@ def thresholded_components(volume, blocking, threshold, mode='greater', mask=Non
             if not mb.any():
                 counts.append(0)
                 continue
-            lab, n = block_components(volume[bb], threshold, mode, mb, normalize_input=False)
+            lab, n = block_components(volume[bb], threshold, mode, mb, normalize_input=False, sigma=sigma)
         else:
             lab, n = block_components(volume[bb], threshold, mode, None,
-                                      normalize_input=True if normalize_input is None else normalize_input)
+                                      normalize_input=True if normalize_input is None else normalize_input,
+                                      sigma=sigma)
         if n:
             seg[bb] = lab
         counts.append(n + 1 if n else 0)

@@ -143,3 +143,13 @@ def test_workflow_fails_loudly_without_gpu(tmp_path):
                                        config_dir=_configs(tmp_path, (8, 16, 16)), max_jobs=2, target='local')
     assert not luigi.build([wf], local_scheduler=True)
     assert os.path.exists(str(tmp_path / 'tmp' / 'block_components_job_0.config'))
+
+
+def test_scan_block_counts_matches_oracle_merge_offsets():
+    from cluster_tools_amd.thresholded_components.merge_offsets import scan_block_counts
+    rng = np.random.default_rng(2)
+    for n in (1, 2, 7, 64):
+        c = rng.integers(0, 50, n) * (rng.random(n) > .3)
+        ids = rng.permutation(n)
+        got = scan_block_counts({int(b): int(c[b]) for b in ids})
+        assert got == T.merge_offsets(c.tolist())

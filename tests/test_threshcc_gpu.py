@@ -161,3 +161,94 @@ def test_threshold_and_watershed_workflow_matches_oracle(tmp_path):
         res = f['seg'][:]
     np.testing.assert_array_equal(res, ref)
     assert (res != 0).mean() > .9
+
+
+def _dtype_cases():
+    """Raw (masked / channel-sum) blocks in the dataset's own dtype: the
+    reference compares `ds_in[bb] > threshold` with a Python float, float64 for float64 and
+    integer data -- values straddling the threshold within float32's rounding, integers above
+    2^24 that float32 cannot tell apart."""
+    rng = np.random.default_rng(5)
+    sh = (12, 40, 150)
+    m = (rng.random(sh) > .2).astype(np.uint8)
+    thr = 0.3
+    f64 = np.where(rng.random(sh) > .5, thr + 1e-12, thr - 1e-12)          # all round to float32(0.3)
+    big = np.int64(2 ** 24 + 1)
+    i32 = np.where(rng.random(sh) > .5, big, big - 1).astype(np.int32)      # 2^24 and 2^24+1 are one float32
+    u64 = np.where(rng.random(sh) > .5, 2 ** 53 + 2, 2 ** 40).astype(np.uint64)
+    return [('f64_straddle', f64, thr, 'greater', m), ('f64_less', f64, thr, 'less', m),
+            ('i32_equal_2p24', i32, float(big), 'equal', m), ('i32_greater', i32, float(big - 1), 'greater', m),
+            ('u64_greater', u64, 2.0 ** 41, 'greater', m),
+            ('u8_raw', rng.integers(0, 256, sh).astype(np.uint8), 99.5, 'greater', m),
+            ('i16_less', rng.integers(-300, 300, sh).astype(np.int16), -7.0, 'less', m),
+            ('i8_equal', rng.integers(-3, 3, sh).astype(np.int8), -1.0, 'equal', m)]
+
+
+@pytest.mark.parametrize('case', _dtype_cases(), ids=lambda c: c[0])
+def test_block_components_raw_dtypes_match_numpy(gpu_handle, case):
+    name, x, thr, mode, mask = case
+    lab, n = gpu_handle.threshold_components(x, thr, mode, mask=mask, normalize=False)
+    ref, rn = T.block_components(x, thr, mode, mask, normalize_input=False)
+    assert rn > 0 and n == rn
+    np.testing.assert_array_equal(lab, ref)
+    if name in ('f64_straddle', 'i32_equal_2p24'):
+        # the float32 path would have classified these differently
+        f32, _ = T.block_components(x.astype(np.float32), thr, mode, mask, normalize_input=False)
+        assert not np.array_equal(f32 != 0, ref != 0)
+
+
+@pytest.mark.parametrize('sigma', [1.0, 2.0])
+@pytest.mark.parametrize('kind', ['unmasked', 'masked', 'channel_sum_u8', 'f64_unmasked'])
+def test_block_components_sigma_prefilter_match_oracle(gpu_handle, kind, sigma):
+    """sigma_prefilter > 0 (block_components.py:160-162 / :208-211): vigra gaussianSmoothing and
+    normalize on the GPU, bit-exact against the oracle's vigra restatement."""
+    rng = np.random.default_rng(int(sigma * 10))
+    sh = (20, 64, 140)
+    x = _volume(sh, 9)
+    mask = None
+    if kind == 'masked':
+        mask = (rng.random(sh) > .1).astype(np.uint8)
+        x = (x * 1000).astype(np.float32)
+    elif kind == 'channel_sum_u8':
+        x = (x * 120).astype(np.uint8) + rng.integers(0, 3, sh).astype(np.uint8)
+    elif kind == 'f64_unmasked':
+        x = x.astype(np.float64) * 3 - 1
+    prenorm = kind in ('unmasked', 'f64_unmasked') or mask is not None
+    lab, n = gpu_handle.threshold_components(x, .5, 'greater', mask=mask, normalize=prenorm, sigma=sigma)
+    ref, rn = T.block_components(x, .5, 'greater', mask, normalize_input=prenorm and mask is None, sigma=sigma)
+    assert rn > 0 and n == rn
+    np.testing.assert_array_equal(lab, ref)
+
+
+def test_block_components_sigma_longer_than_block_refused(gpu_handle):
+    from cluster_tools_amd.ctws import CtwsError
+    with pytest.raises(CtwsError):
+        gpu_handle.threshold_components(np.zeros((4, 32, 32), np.float32), .5, sigma=2.0)
+
+
+def test_thresholded_components_workflow_sigma_prefilter(tmp_path):
+    """The workflow with sigma_prefilter = 1.0 in block_components.config, masked."""
+    from conftest import luigi_build
+    from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    from cluster_tools_amd.thresholded_components.block_components import BlockComponentsLocal
+    shape, bs = (32, 96, 160), (16, 48, 64)
+    x = _volume(shape, 8)
+    path = str(tmp_path / 'data.n5')
+    mask = np.zeros(shape, np.uint8)
+    mask[:, 10:90, 5:150] = 1
+    with vu.file_reader(path) as f:
+        f.create_dataset('x', data=x, chunks=(8, 16, 32))
+        f.create_dataset('mask', data=mask, chunks=(8, 16, 32))
+    bc = BlockComponentsLocal.default_task_config()
+    bc['sigma_prefilter'] = 1.0
+    wf = ThresholdedComponentsWorkflow(input_path=path, input_key='x', output_path=path, output_key='cc',
+                                       assignment_key='ass', threshold=.5, tmp_folder=str(tmp_path / 'tmp'),
+                                       config_dir=_configs(tmp_path, bs, {'block_components': bc}), max_jobs=2,
+                                       target='local', mask_path=path, mask_key='mask')
+    luigi_build(wf, tmp_path / 'tmp')
+    ref_seg, ref_ass, _ = T.thresholded_components(x, Blocking([0, 0, 0], list(shape), list(bs)), .5, 'greater',
+                                                   mask=mask, sigma=1.0)
+    with vu.file_reader(path, 'r') as f:
+        np.testing.assert_array_equal(f['ass'][:], ref_ass)
+        np.testing.assert_array_equal(f['cc'][:], ref_seg)
+    assert len(np.unique(ref_seg)) > 2
