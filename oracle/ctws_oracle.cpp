@@ -444,7 +444,9 @@ int g_flood_model = 0;
 // tie orders for the tie-order experiment (scripts/tie_order_experiment.py): the GPU's
 // order is 1 (kDMax = 4095 in cluster_tools_amd/csrc/ctws_dev.h).  Orders 2 and 6 have no
 // unique fixpoint (equal keys along plateau paths), so no parallel relaxation can promise them.  2: (C, label), no hop distance; 3: (C, d, -label); 4: (C, d, push count) = FIFO
-// inside an equal-(C, d) front; 5: (C, push count) = FIFO on a plateau; 6: (C, min(d, 1), label)
+// inside an equal-(C, d) front; 5: (C, push count) = FIFO on a plateau; 6: (C, min(d, 1), label);
+// 7: (C, label, d) -- the label before the hop distance, which still grows along every parent
+// edge (so the fixpoint stays unique)
 int g_tie_order = 1;
 
 inline uint32_t ordf(float f) {
@@ -461,6 +463,12 @@ struct ModelEntry {
 };
 struct ModelCompare {
     bool operator()(const ModelEntry& a, const ModelEntry& b) const {
+        if (g_tie_order == 7) {  // (C, label, d)
+            const uint32_t ca = (uint32_t)(a.key >> 32), cb = (uint32_t)(b.key >> 32);
+            if (ca != cb) return ca > cb;
+            if (a.label != b.label) return a.label > b.label;
+            return (a.key & 0xFFFFFFFFull) > (b.key & 0xFFFFFFFFull);
+        }
         if (a.key != b.key) return a.key > b.key;
         switch (g_tie_order) {
             case 3: return a.label < b.label;

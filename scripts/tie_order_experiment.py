@@ -13,6 +13,9 @@ oracle watersheds_model restates it.  Orders compared (oracle g_tie_order):
   4 (C, d, push count): FIFO inside an equal-(C, d) front
   5 (C, push count):    FIFO on a plateau
   6 (C, min(d, 1), label): the hop distance reduced to "entered at its own height or not"
+  7 (C, label, d): the label before the hop distance; the key still strictly
+    increases along parent edges (C rises, or C and the label are kept and d grows), so unlike
+    2 and 6 the fixpoint is unique
 Orders 2 and 6 are closest to the heap on the tie-dominated inputs, but (C, d) no longer strictly
 increases along parent edges: the fixpoint is not unique (a cycle of equal-key plateau voxels
 can keep a stale label) and the GPU's relaxation reached another one (round 4) -- not adopted.
@@ -50,7 +53,7 @@ def main():
         heap = run()
         ign = [0] if block.get('mask') is not None else None
         row = {}
-        for order in (1, 2, 3, 4, 5, 6):
+        for order in (1, 2, 3, 4, 5, 6, 7):
             L.orc_set_tie_order(order)
             with O.flood_model():
                 m = run()
