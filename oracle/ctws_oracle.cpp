@@ -437,7 +437,7 @@ struct PQCompare {
 // Model of the GPU flood (cluster_tools_amd/csrc/k_flood.hip): the same label-on-push
 // region growing, but the priority is the total order key K = (C, d) then the label, with
 // C the minimax height (float bits, order-preserving) and d the hop distance inside an
-// equal-C plateau.  vigra breaks equal-C ties by heap position instead; this model is what
+// equal-C plateau (g_tie_order 1; the other orders are the tie-order experiment's).  vigra breaks equal-C ties by heap position instead; this model is what
 // the GPU must reproduce bit for bit, and VI(model, vigra) is the tie-break gap.
 // ---------------------------------------------------------------------------------------
 int g_flood_model = 0;
@@ -445,8 +445,9 @@ int g_flood_model = 0;
 // order is 1 (kDMax = 4095 in cluster_tools_amd/csrc/ctws_dev.h).  Orders 2 and 6 have no
 // unique fixpoint (equal keys along plateau paths), so no parallel relaxation can promise them.  2: (C, label), no hop distance; 3: (C, d, -label); 4: (C, d, push count) = FIFO
 // inside an equal-(C, d) front; 5: (C, push count) = FIFO on a plateau; 6: (C, min(d, 1), label);
-// 7: (C, label, d) -- the label before the hop distance, which still grows along every parent
-// edge (so the fixpoint stays unique)
+// 7: (C, label, d) -- the label before the hop distance; the fixpoint is unique, but a parallel
+// relaxation does not reach it: round 5 on the GPU, a label whose source's C later drops stays
+// on as a phantom whose d counts up to the saturation (count to infinity), DESIGN §4
 int g_tie_order = 1;
 
 inline uint32_t ordf(float f) {

@@ -13,9 +13,12 @@ oracle watersheds_model restates it.  Orders compared (oracle g_tie_order):
   4 (C, d, push count): FIFO inside an equal-(C, d) front
   5 (C, push count):    FIFO on a plateau
   6 (C, min(d, 1), label): the hop distance reduced to "entered at its own height or not"
-  7 (C, label, d): the label before the hop distance; the key still strictly
-    increases along parent edges (C rises, or C and the label are kept and d grows), so unlike
-    2 and 6 the fixpoint is unique
+  7 (C, label, d): the label before the hop distance.  The key still strictly
+    increases along parent edges, so the fixpoint is unique, and on these inputs it is as close
+    to the heap as order 2.  Built on the GPU in round 5 it did not converge: the relaxation's
+    keys are not monotone (a voxel's label can rise when its argmin's C drops), a label that has
+    lost its source survives as a phantom whose d counts up until the 12-bit field saturates
+    (frontier iterations that never empty; the fixpoint check fails) -- not adopted
 Orders 2 and 6 are closest to the heap on the tie-dominated inputs, but (C, d) no longer strictly
 increases along parent edges: the fixpoint is not unique (a cycle of equal-key plateau voxels
 can keep a stale label) and the GPU's relaxation reached another one (round 4) -- not adopted.
