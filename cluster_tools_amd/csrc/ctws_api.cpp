@@ -135,6 +135,7 @@ struct ctws_handle {
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
     int output_tile = 1;   // CTWS_OUTPUT_TILE=0: cropped blocks through the word-tiled k_output
+    int crop_short = 1;    // CTWS_CROP_SHORT=0: every crop voxel through the tile unions
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int words_per_wave = 32;    // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels
@@ -1210,7 +1211,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
         // the seed CC's member bitmap (CcArgs::troot for SEED): its parents are members-only
         HIPCHK(hipMemsetAsync(w.fseed, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed};
+        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed, nullptr, nullptr};
         if (pl.nd_ws == 3) {
             using T = CcTileM<3, CC_SEED>;  // (= the plateau tile)
             const dim3 tg(tiles8(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
@@ -1312,12 +1313,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
         const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
         const dim3 dg(tiles8(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
-        {
-            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
-            else k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
-            LAUNCHCHK();
-        }
-        mark("descent_tile");
         if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
         // masked blocks: their plateau leaves the open set until the rest is flooded (k_plateau.hip);
         // the plateau level comes out of the descent pass
@@ -1325,8 +1320,26 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         for (int i = 0; i < nb; ++i) any_mask |= desc[i].mask != nullptr;
         const bool plat_fill = h->plateau_fill && packed && any_mask;
         if (plat_fill) HIPCHK(hipMemsetAsync(w.plev, 0, sizeof(uint32_t) * (size_t)nb, h->stream));
+        // the tile kernel finishes the chains that end inside their tile (key, fixed flag, open /
+        // changed bits) and marks the others pending in w.fplat (free until k_plat_mark); 3-D
+        // tiles write 16-bit parts of the bitmap words (atomics on zeroed words), 2-D tile rows
+        // are whole words
+        if (pl.nd_ws == 3) {
+            HIPCHK(hipMemsetAsync(w.fopen, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+            HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+            HIPCHK(hipMemsetAsync(w.fplat, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+            k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P, w.key, w.cls,
+                                                         w.fopen, w.front0, w.fplat, fst,
+                                                         plat_fill ? w.plev : nullptr);
+        } else {
+            k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P, w.key, w.cls,
+                                                         w.fopen, w.front0, w.fplat, fst,
+                                                         plat_fill ? w.plev : nullptr);
+        }
+        LAUNCHCHK();
+        mark("descent_tile");
         // 8 words in flight per wave step (4: +0.1 ms on config 3, +0.6 ms on config 4)
-        k_descent_init<8><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
+        k_descent_init<8><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fplat, w.key, w.cls, w.fopen,
                                                      w.front0, fst, plat_fill ? w.plev : nullptr);
         LAUNCHCHK();
         if (plat_fill) {
@@ -1556,10 +1569,25 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         mark("finalize");
 
         // ---- halo crop CC (labelVolumeWithBackground) + uint64 output --------------------------
+        // crop CC shortcut (unmasked cropped blocks; CTWS_CROP_SHORT=0 off): labels that meet no
+        // inner face with a halo beyond it are whole components (k_tilecc.hip); per label in the
+        // (free) dt / sm arrays: touched flags, first voxel in scan order
+        uint32_t* crop_touched = (uint32_t*)w.dt;
+        uint32_t* crop_first = (uint32_t*)w.sm;
+        const bool crop_short = any_crop && h->crop_short;
         if (any_crop) {
             // tile roots of the crop CC marked in the (free) frontier bitmap front0
             HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0};
+            HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0, nullptr, nullptr};
+            const dim3 lg((unsigned)std::min<int64_t>((maxN + 255) / 256, 1024), nb);
+            if (crop_short) {
+                ca.touched = crop_touched;
+                ca.first = crop_first;
+                k_crop_init<<<lg, 256, 0, h->stream>>>(w.desc, w.stat, crop_touched, crop_first);
+                k_crop_faces<<<dim3((unsigned)std::min<int64_t>((maxN / 16 + 255) / 256 + 1, 1024), nb), 256, 0,
+                               h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, crop_touched);
+            }
             const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;
@@ -1572,7 +1600,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 k_tile_cc<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
                 k_tile_merge<2, CC_CROP><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             }
-            HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+            if (crop_short) k_crop_short_roots<<<lg, 256, 0, h->stream>>>(w.desc, w.stat, crop_touched, crop_first, w.W);
             k_flatten_tile_roots<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0, w.W);
             k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
             k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
@@ -1589,16 +1617,16 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const bool crop_tiles = any_crop && h->output_tile;
         // (k_output still writes the uncropped blocks and the empty ones: constant offset)
         k_output<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
-                                             (unsigned long long*)w.W, crop_tiles ? 1 : 0);
+                                             (unsigned long long*)w.W, crop_tiles ? 1 : 0, crop_first);
         if (crop_tiles) {
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;
                 const dim3 tg(tiles8(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
-                k_output_crop<3><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0);
+                k_output_crop<3><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0, crop_first);
             } else {
                 using T = CcTile<2>;
                 const dim3 tg(tiles8(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
-                k_output_crop<2><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0);
+                k_output_crop<2><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0, crop_first);
             }
         }
         if (any_plain) k_count_ids<<<dim3(64, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.W);
@@ -2266,6 +2294,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_DIR")) h->frontier_dir = std::atoi(t) ? 1 : 0;
+    if (const char* t = std::getenv("CTWS_CROP_SHORT")) h->crop_short = std::atoi(t) ? 1 : 0;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * kTapSlot * sizeof(double), hipHostMallocDefault) != hipSuccess) {

@@ -123,6 +123,14 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
     // space) so that all of a thread's loads are in flight together; non-members and positions
     // outside the domain are selected away afterwards.  Same values as cc_value.
     uint32_t vv[PER];
+    // CROP shortcut (a.touched, unmasked blocks): a label that meets no inner face with a halo
+    // beyond never left the inner block, and a flood label's region is connected (every voxel
+    // took its label from a neighbour, back to the seed component), so it is one component of
+    // the crop CC, rooted at its first voxel in scan order.  Its voxels skip the unions: P =
+    // kShortBit | label, and the run starts along x fold their scan key into first[label].
+    const bool shortcut = MODE == CC_CROP && a.touched && !B.mask;
+    uint32_t sl_lab[PER];
+    uint32_t shortm = 0;
     {
         uint64_t l0[PER];
         uint32_t l1[PER];
@@ -167,6 +175,7 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
                                       : ((uint32_t)l0[j] & ~kFixedBit);
                 if (!l1[j]) l = 0u;  // masked
                 v = l ? l : kLNone;
+                sl_lab[j] = l;
             } else if (MODE == CC_PLATEAU) {
                 v = (l0[j] & 2) ? (l1[j] == 0x80000000u ? 0u : l1[j]) : kLNone;
             } else {
@@ -181,6 +190,17 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
                 }
             }
             vv[j] = ((inm >> j) & 1u) ? v : kLNone;
+        }
+        if (shortcut) {
+            uint32_t tch[PER];
+#pragma unroll
+            for (int j = 0; j < PER; ++j) tch[j] = vv[j] != kLNone ? gbl(a.touched)[B.base + vv[j]] : 1u;
+#pragma unroll
+            for (int j = 0; j < PER; ++j)
+                if (!tch[j]) {
+                    shortm |= 1u << j;
+                    vv[j] = kLNone;  // no unions
+                }
         }
     }
 #pragma unroll
@@ -249,6 +269,18 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             }
             if (!mem) continue;
         }
+        if (shortcut) {
+            // the x-run starts of the short voxels (the smallest scan key of the run: smallest x)
+            const bool sh = (shortm >> j) & 1u;
+            const uint32_t lp = (uint32_t)__shfl_up((int)sl_lab[j], 1);
+            const bool shp = __shfl_up((int)sh, 1) != 0;
+            const bool start = sh && (lane == 0 || (c % TX) == 0 || !shp || lp != sl_lab[j]);
+            if (start) atomic_min_if(&a.first[B.base + sl_lab[j]], (uint32_t)(z + nz * (y + ny * x)));
+            if (sh) {
+                P[((int64_t)z * ny + y) * nx + x] = kShortBit | sl_lab[j];
+                continue;
+            }
+        }
         if (z >= nz || y >= ny || x >= nx) continue;
         uint32_t g = kNoParent;
         const int64_t gi = ((int64_t)z * ny + y) * nx + x;
@@ -307,7 +339,8 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                     // the members only (the member bitmap a.troot says which)
                     const bool mi = MODE == CC_SEED ? bit_of(a.troot, B, i)
                                                     : (MODE != CC_PLATEAU || (a.cls[B.base + i] & 2));
-                    const uint32_t pi = mi ? P[i] : kNoParent;
+                    uint32_t pi = mi ? P[i] : kNoParent;
+                    if (MODE == CC_CROP && (pi & kShortBit) && pi != kNoParent) pi = kNoParent;  // one component already
                     if (pi != kNoParent) {
                         // the backward neighbours of (z, y, x) that leave the tile through face f
                         // (a diagonal through the tile corner belongs to the y face)
@@ -322,7 +355,7 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                             if (MODE == CC_PLATEAU && !(a.cls[B.base + q] & 2)) continue;
                             if (MODE == CC_SEED && !bit_of(a.troot, B, q)) continue;
                             const uint32_t pq = P[q];
-                            if (pq == kNoParent) continue;
+                            if (pq == kNoParent || (MODE == CC_CROP && (pq & kShortBit))) continue;
                             if (MODE != CC_SEED &&
                                 cc_value<MODE>(B, a, true, z, y, x) != cc_value<MODE>(B, a, true, qz, qy, qx))
                                 continue;

@@ -40,6 +40,10 @@ class BlockComponentsBase(luigi.Task):
     mask_path = luigi.Parameter(default='')
     mask_key = luigi.Parameter(default='')
     channel = luigi.Parameter(default=None)
+    # the merge tail in the jobs (merge_in_job.py; set by ThresholdedComponentsWorkflow for a local
+    # target): the assignment dataset, MergeOffsets' offsets file and BlockFaces' max_jobs
+    assignment_key = luigi.Parameter(default='')
+    offsets_path = luigi.Parameter(default='')
 
     threshold_modes = ('greater', 'less', 'equal')
 
@@ -84,7 +88,18 @@ class BlockComponentsBase(luigi.Task):
             f.require_dataset(self.output_key, shape=tuple(shape), dtype='uint64', compression=compression,
                               chunks=chunks)
         block_list = vu.blocks_in_volume(shape, block_shape, roi_begin, roi_end)
-        self.run_jobs(min(len(block_list), self.max_jobs), block_list, config)
+        n_jobs = min(len(block_list), self.max_jobs)
+        consecutive = False
+        if self.assignment_key != '' and isinstance(self, LocalTask):
+            from cluster_tools_amd.watershed.watershed import job_group_config
+            merge = job_group_config(self.tmp_folder, n_jobs)
+            merge.update({'assignment_key': self.assignment_key, 'offsets_path': self.offsets_path,
+                          'output_path': self.output_path, 'faces_max_jobs': self.max_jobs,
+                          'block_list': list(block_list)})
+            config['merge'] = merge
+            self.allow_retry = False   # the offsets, pairs and ids depend on every block
+            consecutive = True         # face planes of consecutive blocks stay in the job
+        self.run_jobs(n_jobs, block_list, config, consecutive_blocks=consecutive)
 
 
 class BlockComponentsLocal(BlockComponentsBase, LocalTask):
@@ -125,8 +140,10 @@ def _read_block(blocking, block_id, ds_in, mask, channel):
     return b
 
 
-def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config):
-    """`_cc_block[_with_mask]` for every block of the job -> {block_id: offset}."""
+def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config, keep=None):
+    """`_cc_block[_with_mask]` for every block of the job -> {block_id: offset}.  keep (a list):
+    the blocks' labels are collected there as (block_id, bb, labels or None, count) instead of
+    written (the in-job merge writes the final ids)."""
     from cluster_tools_amd import ctws
     sigma = float(config.get('sigma_prefilter', 0) or 0)
     threshold, mode = config['threshold'], config['threshold_mode']
@@ -141,7 +158,10 @@ def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config):
             fu.log("start processing block %i" % block_id)
             if b.get('skip'):
                 offsets[block_id] = 0
-                fu.log_block_success(block_id)
+                if keep is not None:
+                    keep.append((block_id, b['bb'], None, 0))
+                else:
+                    fu.log_block_success(block_id)
                 continue
             # normalized first: the unmasked single-channel block (`_cc_block`,
             # block_components.py:150-151) and, before its prefilter, a masked block (:208-209);
@@ -149,9 +169,12 @@ def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config):
             prenorm = (mask is None and channel is None) or (mask is not None and sigma > 0)
             labels, n = h.threshold_components(b['input'], threshold, mode, mask=b['mask'], normalize=prenorm,
                                                sigma=sigma)
+            offsets[block_id] = n + 1 if n else 0
+            if keep is not None:
+                keep.append((block_id, b['bb'], labels if n else None, offsets[block_id]))
+                continue
             if n:
                 ds_out[b['bb']] = labels
-            offsets[block_id] = n + 1 if n else 0
             fu.log_block_success(block_id)
     return offsets
 
@@ -174,11 +197,45 @@ def block_components(job_id, config_path):
         mask = None
         if config.get('mask_path', ''):
             mask = vu.load_mask(config['mask_path'], config['mask_key'], shape)
+        if config.get('merge'):
+            _run_blocks_merge(job_id, blocking, ds_in, ds_out, mask, config)
+            fu.log_job_success(job_id)
+            return
         offsets = run_component_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config)
     save_path = os.path.join(config['tmp_folder'], 'connected_components_offsets_%i.json' % job_id)
     with open(save_path, 'w') as f:
         json.dump({int(k): int(v) for k, v in offsets.items()}, f)
     fu.log_job_success(job_id)
+
+
+def _run_blocks_merge(job_id, blocking, ds_in, ds_out, mask, config):
+    """The job's blocks, then the merge tail over the jobs' process group (merge_in_job.py)."""
+    from cluster_tools_amd.thresholded_components.merge_in_job import merge_in_job
+    from cluster_tools_amd.watershed import job_relabel
+    from cluster_tools_amd.cluster_tasks import split_blocks
+    m = config['merge']
+    block_list = m['block_list']
+    owner = {}
+    for j, blocks in enumerate(split_blocks(block_list, m['n_jobs'], consecutive=True)):
+        for b in blocks:
+            owner[b] = j
+    job_relabel.init_group(job_id, m['n_jobs'], m['rendezvous'], m['backend'], device=_device())
+    failed = None
+    keep = []
+    try:
+        try:
+            run_component_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, keep=keep)
+        except Exception as e:  # still take part in the exchange: every job then raises
+            import traceback
+            traceback.print_exc()
+            failed = e
+        merge_in_job(job_id, [] if failed else keep, blocking, block_list, owner, dict(m, tmp_folder=config['tmp_folder']),
+                     ds_out, log=fu.log, device=_device(), failed=failed is not None)
+    finally:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    if failed is not None:
+        raise failed
 
 
 if __name__ == '__main__':

@@ -3,7 +3,8 @@
 parameters, task chain and config keys).
 
 BlockComponents (GPU, k_threshcc.hip) -> MergeOffsets -> BlockFaces -> MergeAssignments
-(boost_ufd representatives, libctws.so) -> Write in place with the offsets (GPU lookup); the
+(boost_ufd representatives, libctws.so) -> Write in place with the offsets (GPU lookup) -- for
+a local target folded into the BlockComponents jobs (merge_in_job.py, merge_in_job=True); the
 threshold-and-watershed variant then grows the components as seeds with WatershedFromSeeds
 (k_seeded.hip) into the same dataset.
 """
@@ -31,6 +32,9 @@ class ThresholdedComponentsWorkflow(WorkflowBase):
     mask_path = luigi.Parameter(default='')
     mask_key = luigi.Parameter(default='')
     channel = luigi.Parameter(default=None)
+    # local target: MergeOffsets -> BlockFaces -> MergeAssignments -> Write run inside the
+    # BlockComponents jobs (merge_in_job.py), same outputs; False keeps the five-task chain
+    merge_in_job = luigi.BoolParameter(default=True)
 
     def requires(self):
         block_task = getattr(block_tasks, self._get_task_name('BlockComponents'))
@@ -46,6 +50,13 @@ class ThresholdedComponentsWorkflow(WorkflowBase):
             shape = shape[1:]
         offset_path = os.path.join(self.tmp_folder, 'cc_offsets.json')
         common = dict(tmp_folder=self.tmp_folder, config_dir=self.config_dir, max_jobs=self.max_jobs)
+        if self.merge_in_job and self.target == 'local':
+            return block_task(input_path=self.input_path, input_key=self.input_key,
+                              output_path=self.output_path, output_key=self.output_key,
+                              threshold=self.threshold, threshold_mode=self.threshold_mode,
+                              mask_path=self.mask_path, mask_key=self.mask_key, channel=self.channel,
+                              dependency=self.dependency, assignment_key=self.assignment_key,
+                              offsets_path=offset_path, **common)
         dep = block_task(input_path=self.input_path, input_key=self.input_key,
                          output_path=self.output_path, output_key=self.output_key,
                          threshold=self.threshold, threshold_mode=self.threshold_mode,
@@ -85,9 +96,11 @@ class ThresholdAndWatershedWorkflow(WorkflowBase):
     mask_path = luigi.Parameter(default='')
     mask_key = luigi.Parameter(default='')
     channel = luigi.IntParameter(default=None)
+    merge_in_job = luigi.BoolParameter(default=True)
 
     def requires(self):
         dep = ThresholdedComponentsWorkflow(tmp_folder=self.tmp_folder, max_jobs=self.max_jobs,
+                                            merge_in_job=self.merge_in_job,
                                             config_dir=self.config_dir, target=self.target,
                                             input_path=self.input_path, input_key=self.input_key,
                                             output_path=self.output_path, output_key=self.output_key,

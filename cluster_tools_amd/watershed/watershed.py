@@ -95,19 +95,24 @@ def ws_task_setup(task, block_shape):
     return shape, cfg
 
 
-def relabel_job_config(task, n_jobs):
-    """The in-job relabel of the local jobs: rendezvous, group size and backend (RCCL when
+def job_group_config(tmp_folder, n_jobs):
+    """The process group of a task's local jobs: rendezvous, group size and backend (RCCL when
     every job owns a GPU, gloo when jobs share one; CTWS_JOB_DIST_BACKEND overrides).  The
     rendezvous is a file store in tmp_folder, fresh per run (a TCP port picked here could be
     taken by another process before the jobs bind it)."""
     import uuid
     from cluster_tools_amd.cluster_tasks import _count_gpus
-    store = os.path.join(os.path.abspath(task.tmp_folder), 'relabel_rendezvous_%s' % uuid.uuid4().hex)
+    store = os.path.join(os.path.abspath(tmp_folder), 'job_rendezvous_%s' % uuid.uuid4().hex)
     n_gpus = _count_gpus()
     backend = 'nccl' if (n_gpus >= n_jobs and 'CTWS_DEVICE' not in os.environ) else 'gloo'
     backend = os.environ.get('CTWS_JOB_DIST_BACKEND', backend)
-    return {'n_jobs': n_jobs, 'rendezvous': 'file://' + store, 'backend': backend, 'tmp_folder': task.tmp_folder,
-            'assignment_path': task.assignment_path, 'assignment_key': task.assignment_key}
+    return {'n_jobs': n_jobs, 'rendezvous': 'file://' + store, 'backend': backend, 'tmp_folder': tmp_folder}
+
+
+def relabel_job_config(task, n_jobs):
+    """The in-job relabel of the local jobs: their process group and the assignment table."""
+    return dict(job_group_config(task.tmp_folder, n_jobs), assignment_path=task.assignment_path,
+                assignment_key=task.assignment_key)
 
 
 def block_uniques_file(folder, block_id):

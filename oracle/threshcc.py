@@ -110,30 +110,36 @@ def merge_offsets(counts):
     return offs.tolist(), empty, int(offs[-1] + last + 1)
 
 
-def block_faces(seg, blocking, offsets, empty_blocks):
-    """Unique (a, b) label pairs across every block's upper faces (block_faces.py:116-177)."""
+def block_faces(seg, blocking, offsets, empty_blocks, faces_jobs=1):
+    """Unique (a, b) label pairs across every block's upper faces (block_faces.py:116-177), from
+    `faces_jobs` BlockFaces jobs (block_list[j::n]): empty when one of the jobs found no pair --
+    MergeAssignments then merges nothing (merge_assignments.py:116-123)."""
     empty = set(empty_blocks)
-    out = []
-    for bid in range(blocking.numberOfBlocks):
-        if bid in empty:
-            continue
-        for axis in range(3):
-            ngb = blocking.getNeighborId(bid, axis, False)
-            if ngb == -1 or ngb in empty:
+    n_jobs = max(1, min(blocking.numberOfBlocks, faces_jobs))
+    jobs = []
+    for j in range(n_jobs):
+        out = []
+        for bid in range(j, blocking.numberOfBlocks, n_jobs):
+            if bid in empty:
                 continue
-            blk = blocking.getBlock(bid)
-            face = tuple(slice(b, e) if d != axis else slice(e - 1, e + 1)
-                         for d, (b, e) in enumerate(zip(blk.begin, blk.end)))
-            f = seg[face]
-            la = np.take(f, 0, axis=axis).ravel().astype('uint64')
-            lb = np.take(f, 1, axis=axis).ravel().astype('uint64')
-            have = (la != 0) & (lb != 0)
-            la, lb = la[have] + np.uint64(offsets[bid]), lb[have] + np.uint64(offsets[ngb])
-            if la.size:
-                out.append(np.unique(np.stack([la, lb], axis=1), axis=0))
-    if not out:
+            for axis in range(3):
+                ngb = blocking.getNeighborId(bid, axis, False)
+                if ngb == -1 or ngb in empty:
+                    continue
+                blk = blocking.getBlock(bid)
+                face = tuple(slice(b, e) if d != axis else slice(e - 1, e + 1)
+                             for d, (b, e) in enumerate(zip(blk.begin, blk.end)))
+                f = seg[face]
+                la = np.take(f, 0, axis=axis).ravel().astype('uint64')
+                lb = np.take(f, 1, axis=axis).ravel().astype('uint64')
+                have = (la != 0) & (lb != 0)
+                la, lb = la[have] + np.uint64(offsets[bid]), lb[have] + np.uint64(offsets[ngb])
+                if la.size:
+                    out.append(np.unique(np.stack([la, lb], axis=1), axis=0))
+        jobs.append(np.unique(np.concatenate(out, axis=0), axis=0) if out else np.zeros((0, 2), dtype='uint64'))
+    if not all(p.size for p in jobs):
         return np.zeros((0, 2), dtype='uint64')
-    return np.unique(np.concatenate(out, axis=0), axis=0)
+    return np.unique(np.concatenate(jobs, axis=0), axis=0)
 
 
 def boost_ufd_find(n, pairs):
@@ -162,8 +168,9 @@ def boost_ufd_find(n, pairs):
     return np.array([find(i) for i in range(n)], dtype='uint64')
 
 
-def thresholded_components(volume, blocking, threshold, mode='greater', mask=None, normalize_input=None, sigma=0.):
-    """The whole workflow on an in-memory volume (one job per task):
+def thresholded_components(volume, blocking, threshold, mode='greater', mask=None, normalize_input=None, sigma=0.,
+                           faces_jobs=1):
+    """The whole workflow on an in-memory volume (one job per task, `faces_jobs` BlockFaces jobs):
     -> (segmentation uint64, assignments uint64, offsets dict).  normalize_input None: as the
     reference, normalize the unmasked blocks only; False: the summed channels of a 4-D input
     (block_components.py:152-158 compares them raw)."""
@@ -186,7 +193,7 @@ def thresholded_components(volume, blocking, threshold, mode='greater', mask=Non
             seg[bb] = lab
         counts.append(n + 1 if n else 0)
     offsets, empty, n_labels = merge_offsets(counts)
-    pairs = block_faces(seg, blocking, offsets, empty)
+    pairs = block_faces(seg, blocking, offsets, empty, faces_jobs)
     assignments = boost_ufd_find(n_labels, pairs) if len(pairs) else np.arange(n_labels, dtype='uint64')
     out = np.zeros_like(seg)
     for bid in range(blocking.numberOfBlocks):

@@ -1,7 +1,8 @@
 """End-to-end ThresholdedComponentsWorkflow on n5 (gzip) on one MI355X: a synthetic blob volume
-is written, then BlockComponents (GPU) runs as its own luigi build and the rest of the chain
-(MergeOffsets, BlockFaces, MergeAssignments, Write) as a second one, each timed; the result is
-checked against the CPU oracle on the whole volume.  One JSON line on stdout.
+is written, then the workflow runs -- with --merge-in-job 1 (the default) as one task whose jobs
+merge among themselves (merge_in_job.py), with 0 as the five-task chain, BlockComponents timed
+as its own luigi build and the rest (MergeOffsets, BlockFaces, MergeAssignments, Write) as a
+second one; the result is checked against the CPU oracle on the whole volume.  One JSON line.
 """
 import argparse
 import json
@@ -22,6 +23,7 @@ def main():
     ap.add_argument('--block', default='64,256,256')
     ap.add_argument('--max-jobs', type=int, default=4)
     ap.add_argument('--no-check', action='store_true')
+    ap.add_argument('--merge-in-job', type=int, default=1)
     args = ap.parse_args()
     shape = tuple(int(s) for s in args.shape.split(','))
     bs = [int(s) for s in args.block.split(',')]
@@ -53,24 +55,32 @@ def main():
         common = dict(tmp_folder=os.path.join(tmp, 'tmp'), config_dir=cfg, max_jobs=args.max_jobs)
         from cluster_tools_amd.utils.task_utils import DummyTask
         t0 = time.perf_counter()
-        ok1 = luigi.build([BlockComponentsLocal(input_path=path, input_key='x', output_path=path, output_key='cc',
-                                                threshold=.5, dependency=DummyTask(), **common)],
-                          local_scheduler=True)
-        t1 = time.perf_counter()
+        if args.merge_in_job:
+            ok1 = True
+            t1 = t0
+        else:
+            ok1 = luigi.build([BlockComponentsLocal(input_path=path, input_key='x', output_path=path,
+                                                    output_key='cc', threshold=.5, dependency=DummyTask(),
+                                                    **common)], local_scheduler=True)
+            t1 = time.perf_counter()
         ok2 = luigi.build([ThresholdedComponentsWorkflow(input_path=path, input_key='x', output_path=path,
                                                          output_key='cc', assignment_key='ass', threshold=.5,
-                                                         target='local', **common)], local_scheduler=True)
+                                                         target='local', merge_in_job=bool(args.merge_in_job),
+                                                         **common)], local_scheduler=True)
         t2 = time.perf_counter()
         n = int(np.prod(shape))
         rec = {'workload': 'ThresholdedComponentsWorkflow, %s float32 blobs (n5 gzip), blocks %s, %d jobs'
                            % ('x'.join(map(str, shape)), 'x'.join(map(str, bs)), args.max_jobs),
-               'ok': bool(ok1 and ok2), 'block_components_s': round(t1 - t0, 2), 'rest_s': round(t2 - t1, 2),
-               'total_s': round(t2 - t0, 2), 'gvoxel_s': round(n / (t2 - t0) / 1e9, 4),
-               'block_components_gvoxel_s': round(n / (t1 - t0) / 1e9, 4)}
+               'merge_in_job': bool(args.merge_in_job), 'ok': bool(ok1 and ok2),
+               'total_s': round(t2 - t0, 2), 'gvoxel_s': round(n / (t2 - t0) / 1e9, 4)}
+        if not args.merge_in_job:
+            rec.update(block_components_s=round(t1 - t0, 2), rest_s=round(t2 - t1, 2),
+                       block_components_gvoxel_s=round(n / (t1 - t0) / 1e9, 4))
         if ok1 and ok2 and not args.no_check:
             from oracle import threshcc as T
             t3 = time.perf_counter()
-            ref, ref_ass, _ = T.thresholded_components(x, Blocking([0, 0, 0], list(shape), bs), .5, 'greater')
+            ref, ref_ass, _ = T.thresholded_components(x, Blocking([0, 0, 0], list(shape), bs), .5, 'greater',
+                                                       faces_jobs=args.max_jobs)
             rec['cpu_oracle_s'] = round(time.perf_counter() - t3, 2)
             with vu.file_reader(path, 'r') as f:
                 rec['bit_exact'] = bool(np.array_equal(f['cc'][:], ref) and np.array_equal(f['ass'][:], ref_ass))

@@ -26,6 +26,8 @@ VARIANTS = {
     'no_plateau_fill': {'CTWS_PLATEAU_FILL': '0'},
     # cropped blocks' uint64 output through the word-tiled k_output instead of k_output_crop
     'output_words': {'CTWS_OUTPUT_TILE': '0'},
+    # every crop voxel through the tile unions (no shortcut for the labels inside the inner block)
+    'crop_short_off': {'CTWS_CROP_SHORT': '0'},
 }
 
 

@@ -153,3 +153,77 @@ def test_scan_block_counts_matches_oracle_merge_offsets():
         ids = rng.permutation(n)
         got = scan_block_counts({int(b): int(c[b]) for b in ids})
         assert got == T.merge_offsets(c.tolist())
+
+
+# ---- the merge tail in the BlockComponents jobs (merge_in_job.py): 2 gloo jobs ---------------
+MJ_SHAPE, MJ_BLOCK = (32, 96, 160), (16, 32, 64)
+
+
+def _mj_worker(rank, world, root, faces_max_jobs, masked):
+    import torch.distributed as dist
+    from cluster_tools_amd.cluster_tasks import split_blocks
+    from cluster_tools_amd.thresholded_components.merge_in_job import merge_in_job
+    from cluster_tools_amd.utils.blocking import Blocking
+    from cluster_tools_amd.utils import volume_utils as vu
+    from cluster_tools_amd.watershed import job_relabel
+    x = _volume(MJ_SHAPE, 7)
+    mask = _mj_mask() if masked else None
+    blocking = Blocking([0, 0, 0], list(MJ_SHAPE), list(MJ_BLOCK))
+    block_list = list(range(blocking.numberOfBlocks))
+    runs = split_blocks(block_list, world, consecutive=True)
+    owner = {b: j for j, r in enumerate(runs) for b in r}
+    job_relabel.init_group(rank, world, 'file://' + os.path.join(root, 'rdv'), 'gloo', timeout_s=120)
+    try:
+        results = []
+        for b in runs[rank]:
+            bb = vu.block_to_bb(blocking.getBlock(b))
+            if mask is not None and not mask[bb].any():
+                results.append((b, bb, None, 0))
+                continue
+            lab, n = T.block_components(x[bb], .55, 'greater', None if mask is None else mask[bb],
+                                        normalize_input=mask is None)
+            results.append((b, bb, lab if n else None, n + 1 if n else 0))
+        cfg = dict(tmp_folder=root, offsets_path=os.path.join(root, 'cc_offsets.json'),
+                   output_path=os.path.join(root, 'out.n5'), assignment_key='ass', faces_max_jobs=faces_max_jobs)
+        with vu.file_reader(cfg['output_path']) as f:
+            merge_in_job(rank, results, blocking, block_list, owner, cfg, f['cc'], log=lambda m: None)
+    finally:
+        dist.destroy_process_group()
+
+
+def _mj_mask():
+    m = np.zeros(MJ_SHAPE, bool)
+    m[:, 10:80, 20:150] = True
+    m[:, :, :64] = False
+    return m
+
+
+@pytest.mark.parametrize('masked', [False, True])
+@pytest.mark.parametrize('faces_max_jobs', [1, 100])
+def test_merge_in_job_matches_the_five_task_chain(tmp_path, masked, faces_max_jobs):
+    """Offsets, face pairs, boost_ufd assignments and the final write of two jobs over gloo
+    equal the oracle's whole pipeline; with as many BlockFaces jobs as blocks the last block has
+    no upper face, one job has no pair and the reference's merge is the identity
+    (merge_assignments.py:116-123)."""
+    import torch.multiprocessing as tmp
+    from cluster_tools_amd.utils.blocking import Blocking
+    from cluster_tools_amd.utils import volume_utils as vu
+    root = str(tmp_path)
+    with vu.file_reader(os.path.join(root, 'out.n5')) as f:
+        f.create_dataset('cc', shape=MJ_SHAPE, dtype='uint64', chunks=tuple(b // 2 for b in MJ_BLOCK))
+    tmp.spawn(_mj_worker, args=(2, root, faces_max_jobs, masked), nprocs=2, join=True)
+    x = _volume(MJ_SHAPE, 7)
+    blocking = Blocking([0, 0, 0], list(MJ_SHAPE), list(MJ_BLOCK))
+    seg, ass, oc = T.thresholded_components(x, blocking, .55, 'greater', mask=_mj_mask() if masked else None,
+                                            faces_jobs=faces_max_jobs)
+    # (with as many BlockFaces jobs as blocks the oracle's merge is the identity too)
+    assert (faces_max_jobs > 1) == np.array_equal(ass, np.arange(len(ass), dtype='uint64'))
+    with vu.file_reader(os.path.join(root, 'out.n5'), 'r') as f:
+        np.testing.assert_array_equal(f['ass'][:], ass)
+        np.testing.assert_array_equal(f['cc'][:], seg)
+        assert f['cc'].attrs['maxId'] == int(ass.max())
+    with open(os.path.join(root, 'cc_offsets.json')) as fo:
+        got = json.load(fo)
+    assert got == {'offsets': [int(o) for o in oc['offsets']], 'empty_blocks': oc['empty_blocks'],
+                   'n_labels': oc['n_labels']}
+    assert not [n for n in os.listdir(root) if n.startswith(('cc_face_', 'cc_block_pairs', 'cc_assignments_merged'))]

@@ -78,8 +78,12 @@ def _configs(tmp_path, block_shape, task_configs=None):
     return str(cfg_dir)
 
 
+@pytest.mark.parametrize('merge_in_job', [True, False])
 @pytest.mark.parametrize('masked,max_jobs', [(False, 1), (False, 3), (True, 2)])
-def test_thresholded_components_workflow_matches_oracle(tmp_path, masked, max_jobs):
+def test_thresholded_components_workflow_matches_oracle(tmp_path, masked, max_jobs, merge_in_job):
+    """merge_in_job: the merge tail in the BlockComponents jobs (merge_in_job.py), else the
+    reference's five-task chain; with max_jobs > 1 BlockFaces has several jobs (one of them
+    without any pair makes the reference's merge the identity -- both modes must agree)."""
     from conftest import luigi_build
     from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
     shape, bs = (32, 96, 160), (16, 32, 64)
@@ -96,10 +100,11 @@ def test_thresholded_components_workflow_matches_oracle(tmp_path, masked, max_jo
     wf = ThresholdedComponentsWorkflow(input_path=path, input_key='x', output_path=path, output_key='cc',
                                        assignment_key='ass', threshold=.55, tmp_folder=str(tmp_path / 'tmp'),
                                        config_dir=_configs(tmp_path, bs), max_jobs=max_jobs, target='local',
-                                       mask_path=path if masked else '', mask_key='mask' if masked else '')
+                                       mask_path=path if masked else '', mask_key='mask' if masked else '',
+                                       merge_in_job=merge_in_job)
     luigi_build(wf, tmp_path / 'tmp')
     ref_seg, ref_ass, ref_off = T.thresholded_components(x, Blocking([0, 0, 0], list(shape), list(bs)), .55,
-                                                         'greater', mask=mask)
+                                                         'greater', mask=mask, faces_jobs=max_jobs)
     with vu.file_reader(path, 'r') as f:
         seg, ass = f['cc'][:], f['ass'][:]
         max_id = f['cc'].attrs['maxId']
