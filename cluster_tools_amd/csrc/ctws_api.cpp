@@ -135,7 +135,8 @@ struct ctws_handle {
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
     int output_tile = 1;   // CTWS_OUTPUT_TILE=0: cropped blocks through the word-tiled k_output
-    int crop_short = 1;    // CTWS_CROP_SHORT=0: every crop voxel through the tile unions
+    int crop_short = 0;    // CTWS_CROP_SHORT=1: labels that never leave the inner block skip the unions
+                           // (measured no faster, DESIGN §3: off)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int words_per_wave = 32;    // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels
@@ -1313,6 +1314,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
         const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
         const dim3 dg(tiles8(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
+        {
+            if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
+            else k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
+            LAUNCHCHK();
+        }
+        mark("descent_tile");
         if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
         // masked blocks: their plateau leaves the open set until the rest is flooded (k_plateau.hip);
         // the plateau level comes out of the descent pass
@@ -1320,26 +1327,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         for (int i = 0; i < nb; ++i) any_mask |= desc[i].mask != nullptr;
         const bool plat_fill = h->plateau_fill && packed && any_mask;
         if (plat_fill) HIPCHK(hipMemsetAsync(w.plev, 0, sizeof(uint32_t) * (size_t)nb, h->stream));
-        // the tile kernel finishes the chains that end inside their tile (key, fixed flag, open /
-        // changed bits) and marks the others pending in w.fplat (free until k_plat_mark); 3-D
-        // tiles write 16-bit parts of the bitmap words (atomics on zeroed words), 2-D tile rows
-        // are whole words
-        if (pl.nd_ws == 3) {
-            HIPCHK(hipMemsetAsync(w.fopen, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-            HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-            HIPCHK(hipMemsetAsync(w.fplat, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-            k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P, w.key, w.cls,
-                                                         w.fopen, w.front0, w.fplat, fst,
-                                                         plat_fill ? w.plev : nullptr);
-        } else {
-            k_descent_tile<2><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P, w.key, w.cls,
-                                                         w.fopen, w.front0, w.fplat, fst,
-                                                         plat_fill ? w.plev : nullptr);
-        }
-        LAUNCHCHK();
-        mark("descent_tile");
         // 8 words in flight per wave step (4: +0.1 ms on config 3, +0.6 ms on config 4)
-        k_descent_init<8><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.fplat, w.key, w.cls, w.fopen,
+        k_descent_init<8><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
                                                      w.front0, fst, plat_fill ? w.plev : nullptr);
         LAUNCHCHK();
         if (plat_fill) {
@@ -1569,7 +1558,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         mark("finalize");
 
         // ---- halo crop CC (labelVolumeWithBackground) + uint64 output --------------------------
-        // crop CC shortcut (unmasked cropped blocks; CTWS_CROP_SHORT=0 off): labels that meet no
+        // crop CC shortcut (unmasked cropped blocks; CTWS_CROP_SHORT=1 on): labels that meet no
         // inner face with a halo beyond it are whole components (k_tilecc.hip); per label in the
         // (free) dt / sm arrays: touched flags, first voxel in scan order
         uint32_t* crop_touched = (uint32_t*)w.dt;
@@ -1606,6 +1595,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
             k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
             k_root_label<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp);
+            if (crop_short) k_crop_short_ids<<<lg, 256, 0, h->stream>>>(w.desc, w.stat, crop_touched, crop_first, w.PF);
             LAUNCHCHK();
         }
         mark("crop_cc");

@@ -159,6 +159,7 @@ __global__ void k_output_crop(const BlockDesc*, BlockStat*, const uint32_t*, con
 __global__ void k_crop_init(const BlockDesc*, const BlockStat*, uint32_t*, uint32_t*);
 __global__ void k_crop_faces(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, uint32_t*);
 __global__ void k_crop_short_roots(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint64_t*);
+__global__ void k_crop_short_ids(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*, const uint32_t*);
 template <int ND, int MODE>
 __global__ void k_tile_merge(const BlockDesc*, const BlockStat*, CcArgs, uint32_t*);
 
@@ -175,11 +176,10 @@ constexpr int kStatSlots = 64;  // flood statistics: counter[4 + slot * 4 + k]  
 __global__ void k_unpack_labels(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
 template <int ND>
 __global__ void k_descent_tile(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint32_t*,
-                               const uint64_t*, uint32_t*, uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint64_t*,
-                               uint32_t*, uint32_t*);
+                               const uint64_t*, uint32_t*);
 template <int U>
-__global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, const uint64_t*,
-                               uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*, uint32_t*);
+__global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint8_t*,
+                               uint64_t*, uint64_t*, uint32_t*, uint32_t*);
 template <int ND, int CW, int CY, int CZ>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,

@@ -396,7 +396,7 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
                     if (p & kRootBit) {
                         l = p & ~kRootBit;
                     } else if (p & kShortBit) {
-                        l = P[short_root(B, first[B.base + (p & ~kShortBit)])] & ~kRootBit;
+                        l = first[B.base + (p & ~kShortBit)];  // the label's id (k_crop_short_ids)
                     } else {
                         const uint32_t q = P[p];
                         l = (q & kRootBit) ? (q & ~kRootBit) : (P[q] & ~kRootBit);
@@ -470,21 +470,14 @@ __global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict
         root[j] = (gbl(TR)[B.fbase + (gi[j] >> 6)] >> (gi[j] & 63)) & 1ull;
     }
     // tile roots: their label (a global root carries it; the others point at their global root);
-    // shortcut voxels (kShortBit | label): the root slot of the label's first voxel
+    // shortcut voxels (kShortBit | label): the label's id (k_crop_short_ids)
     uint32_t rl[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const bool sh = in[j] && e[j] != kNoParent && !(e[j] & kRootBit) && (e[j] & kShortBit);
-        if (sh) {
-            rl[j] = gbl(first)[B.base + (e[j] & ~kShortBit)];
-            continue;
-        }
         const bool need = in[j] && root[j] && e[j] != kNoParent && !(e[j] & kRootBit);
-        rl[j] = P[need ? e[j] : 0u];  // unconditional: all in flight
+        rl[j] = sh ? gbl(first)[B.base + (e[j] & ~kShortBit)] : P[need ? e[j] : 0u];  // all in flight
     }
-#pragma unroll
-    for (int j = 0; j < PER; ++j)
-        if (in[j] && e[j] != kNoParent && !(e[j] & kRootBit) && (e[j] & kShortBit)) rl[j] = P[short_root(B, rl[j])];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         if (!(in[j] && root[j])) continue;
@@ -612,6 +605,22 @@ __global__ void __launch_bounds__(256) k_crop_short_roots(const BlockDesc* __res
         const uint32_t f = first[B.base + l];
         if (touched[B.base + l] || f == 0xFFFFFFFFu) continue;
         atomicOr((unsigned long long*)&Wg[B.wbase + (f >> 6)], 1ull << (f & 63));
+    }
+}
+
+// after k_root_label: a shortcut label's first voxel -> the label's output id, in place (the
+// outputs then read one table entry per voxel instead of first voxel -> root)
+__global__ void __launch_bounds__(256) k_crop_short_ids(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                        const uint32_t* __restrict__ touched, uint32_t* __restrict__ first,
+                                                        const uint32_t* __restrict__ PFg) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!crop_short_block(B, S[blockIdx.y])) return;
+    const uint32_t* P = PFg + B.ibase;
+    const int64_t n = crop_label_bound(S[blockIdx.y]);
+    for (int64_t l = 1 + (int64_t)blockIdx.x * 256 + threadIdx.x; l < n; l += (int64_t)gridDim.x * 256) {
+        const uint32_t f = first[B.base + l];
+        if (touched[B.base + l] || f == 0xFFFFFFFFu) continue;
+        first[B.base + l] = P[short_root(B, f)] & ~kRootBit;
     }
 }
 

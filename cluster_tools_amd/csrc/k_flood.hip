@@ -567,10 +567,7 @@ template <int ND>
 __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_eu(ND == 2 ? 8 : 6, 8))) k_descent_tile(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint32_t* __restrict__ lab,
                                                       const uint32_t* __restrict__ cc, const uint64_t* __restrict__ sbits,
-                                                      uint32_t* __restrict__ exitp, uint64_t* __restrict__ key,
-                                                      uint8_t* __restrict__ fixedv, uint64_t* __restrict__ open,
-                                                      uint64_t* __restrict__ chg, uint64_t* __restrict__ pend,
-                                                      uint32_t* __restrict__ nopen, uint32_t* __restrict__ plev) {
+                                                      uint32_t* __restrict__ exitp) {
     using T = DTile<ND>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, HZ = T::HZ, HY = TY + 2, HX = TX + 2;
     constexpr int HN = HZ * HY * HX, TN = TZ * TY * TX;
@@ -714,15 +711,6 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
         }
         if (!__syncthreads_or(moved)) break;
     }
-    // own heights (ordered bits) before sh[] is reused for the roots' labels
-    uint32_t ho[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int c = threadIdx.x + k * NT;
-        const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
-        ho[k] = sh[((lz + ZOFF) * HY + ly + 1) * HX + lx + 1];
-    }
-    __syncthreads();
     // tile roots: seed label (seeds) or 0 (local minima without a seed, ties), kept in sh[]
     // (the heights are no longer read).  The label comes from the seed entry loaded above: a
     // cc root carries it, a non-root cc entry needs its root's (one more load, unconditional)
@@ -747,113 +735,59 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
         }
     }
     __syncthreads();
-    // A chain that ends at a root of this tile is final here: a seed root gives the voxel its key
-    // (h, 0, label) and makes it fixed; a root without a seed (a minimum or a tie) leaves it open
-    // (INF) for the relaxation.  A chain that leaves the tile is "pending": exitp = the block index
-    // of its first voxel outside the tile, and k_descent_init follows it across tiles.  Chains
-    // enter a tile only at its face voxels, so exitp is written for the pending voxels and for
-    // the face voxels (their resolution, kDescRes | label, 0 = open) -- the interior ones need
-    // none.  Bitmap words: open / chg (resolved) / pend bits of the final and pending voxels.
-    const bool want_lev = plev && B.mask;
-    uint32_t lev = 0, cnt_open = 0;
-    const int wpr = (B.X + 63) >> 6;
-    const int lane = threadIdx.x & 63;
+    // exit entry: kDescRes | label when the chain ends at a seed root of this tile; the block
+    // index of the root when it ends at a root without a seed (the root itself: kDescRes | 0);
+    // else the block index of the first voxel outside the tile (k_descent_init follows it)
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int c = threadIdx.x + k * NT;
-        const bool in = (inm >> k) & 1u;
+        if (!((inm >> k) & 1u)) continue;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
-        const int64_t gi = (int64_t)gz * YX + (int64_t)gy * B.X + gx;
         const int p = sp[c];
-        bool pending = false, res = false, opn = false;
-        uint32_t e = 0;
-        if (in) {
-            if (p < TN) {
-                const uint32_t l = sh[p];
-                res = l != 0u;
-                opn = !res;
+        uint32_t e;
+        if (p < TN) {
+            const uint32_t l = sh[p];
+            if (l != 0u || p == c) {
                 e = kDescRes | l;
-                key[B.base + gi] = res ? pk_make(ho[k], l) : kPackInf;
-                fixedv[B.base + gi] = res ? 1 : 0;
-                const bool face = lx == 0 || lx == TX - 1 || ly == 0 || ly == TY - 1 ||
-                                  (ND == 3 && (lz == 0 || lz == TZ - 1));
-                if (face) exitp[B.base + gi] = e;
-                if (opn) {
-                    ++cnt_open;
-                    if (want_lev && !gbl(B.mask)[gi]) lev = max(lev, ho[k]);
-                }
             } else {
-                const int q = p - TN;
-                const int ex = x0 + q % HX - 1;
-                const int ey = y0 + (q / HX) % HY - 1;
-                const int ez = z0 + q / (HX * HY) - ZOFF;
-                exitp[B.base + gi] = (uint32_t)(ez * YX + (int64_t)ey * B.X + ex);
-                pending = true;
-            }
-        }
-        const uint64_t bo = __ballot(opn), br = __ballot(res), bp = __ballot(pending);
-        if (ND == 2) {
-            // a wave is one tile row = one bitmap word (TX = 64, x0 a multiple of 64)
-            if (lane == 0 && gz < B.Z && gy < B.Y) {
-                const int64_t w = B.fbase + ((int64_t)gz * B.Y + gy) * wpr + (x0 >> 6);
-                open[w] = bo;
-                chg[w] = br;
-                pend[w] = bp;
+                const int rx = p % TX, ry = (p / TX) % TY, rz = p / (TX * TY);
+                e = (uint32_t)((z0 + rz) * YX + (int64_t)(y0 + ry) * B.X + (x0 + rx));
             }
         } else {
-            // a wave is 64 / TX tile rows, each TX bits of one word (zeroed beforehand)
-            if (lx == 0 && gz < B.Z && gy < B.Y) {
-                const int sh0 = lane & ~(TX - 1);
-                const uint64_t m = (TX == 64) ? ~0ull : ((1ull << TX) - 1ull);
-                const int64_t w = B.fbase + ((int64_t)gz * B.Y + gy) * wpr + (x0 >> 6);
-                const int off = x0 & 63;
-                const uint64_t vo = ((bo >> sh0) & m) << off, vr = ((br >> sh0) & m) << off,
-                               vp = ((bp >> sh0) & m) << off;
-                if (vo) atomicOr((unsigned long long*)&open[w], (unsigned long long)vo);
-                if (vr) atomicOr((unsigned long long*)&chg[w], (unsigned long long)vr);
-                if (vp) atomicOr((unsigned long long*)&pend[w], (unsigned long long)vp);
-            }
+            const int q = p - TN;
+            const int ex = x0 + q % HX - 1;
+            const int ey = y0 + (q / HX) % HY - 1;
+            const int ez = z0 + q / (HX * HY) - ZOFF;
+            e = (uint32_t)(ez * YX + (int64_t)ey * B.X + ex);
         }
-    }
-    if (nopen) {
-        cnt_open = wg_reduce_u32(cnt_open, OpAdd());
-        if (threadIdx.x == 0 && cnt_open) atomicAdd(&nopen[blockIdx.y], cnt_open);
-    }
-    if (want_lev) {
-        lev = wg_reduce_u32(lev, OpMax());
-        if (threadIdx.x == 0 && lev) atomic_max_if(&plev[blockIdx.y], lev);
+        exitp[B.base + gz * YX + (int64_t)gy * B.X + gx] = e;
     }
 }
-#define CTWS_DESC_TILE_INST(ND)                                                                               \
-    template __global__ void k_descent_tile<ND>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,  \
-                                                const uint32_t*, const uint64_t*, uint32_t*, uint64_t*, uint8_t*,    \
-                                                uint64_t*, uint64_t*, uint64_t*, uint32_t*, uint32_t*);
-CTWS_DESC_TILE_INST(3)
-CTWS_DESC_TILE_INST(2)
-#undef CTWS_DESC_TILE_INST
+template __global__ void k_descent_tile<3>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
+                                           const uint32_t*, const uint64_t*, uint32_t*);
+template __global__ void k_descent_tile<2>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
+                                           const uint32_t*, const uint64_t*, uint32_t*);
 
-// The pending voxels of k_descent_tile (chains that leave their tile): follow the exit entries
-// across tiles (a hop per tile crossed; every hop lands on a face voxel, whose entry the tile
-// kernel wrote) to the resolution; a chain ending in a seed gives the voxel its final key and
-// makes it fixed, the others wait for the flood (INF key).  Their bits are added to the open /
-// changed bitmaps the tile kernel wrote (open = not final yet, chg = final: the first "changed"
-// set, whose neighbours form the first frontier).  Word tiles (a wave's ballot is exactly one
-// word of the bitmaps), U words per step; a word without a pending voxel costs its bitmap load.
+// voxels whose descent ends in a seed get their final key, fixed; the others wait for the
+// flood (INF key).  Bitmaps, one word per 64 voxels of a row (the 64 lanes of a wave cover
+// exactly one word): open = not final yet, chg = final (the first "changed" set, whose
+// neighbours form the first frontier).
 template <int U>
 __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint32_t* __restrict__ par,
-                                                      const uint64_t* __restrict__ pend, uint64_t* __restrict__ key,
-                                                      uint8_t* __restrict__ fixedv, uint64_t* __restrict__ open,
-                                                      uint64_t* __restrict__ chg, uint32_t* __restrict__ nopen,
-                                                      uint32_t* __restrict__ plev) {
+                                                      uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
+                                                      uint64_t* __restrict__ open, uint64_t* __restrict__ chg,
+                                                      uint32_t* __restrict__ nopen, uint32_t* __restrict__ plev) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     uint32_t cnt_open = 0;  // statistics (CTWS_TRACE): voxels left to the relaxation
     // masked blocks (k_plateau.hip): the largest height of an open masked-out voxel (the plateau
-    // level, plev[block]; the pending voxels' share, the tile kernel adds the others')
+    // level, plev[block]; the plateau fill's k_plat_level folded into this pass)
     const bool want_lev = plev && B.mask;
     uint32_t lev = 0;
+    // word tiles (a wave's ballot is exactly one word of the open / changed bitmaps), U words
+    // per step: the U chains of a lane hop together, so U dependent-load latencies overlap
     const int wpr = (B.X + 63) >> 6;
     const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
     const int lane = threadIdx.x & 63;
@@ -865,32 +799,26 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
     int row_n = (int)(wbeg / wpr), xw_n = (int)(wbeg - (int64_t)row_n * wpr);
     for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
         int64_t gi[U];
-        uint64_t pw[U];
         bool valid[U];
+        uint32_t e[U];
+        float hv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            const int64_t wu = w0 + u;
             const int64_t row = row_n;
             const int x = xw_n * 64 + lane;
             if (++xw_n == wpr) {
                 xw_n = 0;
                 ++row_n;
             }
-            const bool wok = w0 + u < wend;
-            pw[u] = wok ? gbl(pend)[B.fbase + w0 + u] : 0ull;
-            valid[u] = wok && x < B.X && ((pw[u] >> lane) & 1ull);
+            valid[u] = wu < wend && x < B.X;
             gi[u] = B.base + (valid[u] ? row * B.X + x : 0);
+            e[u] = gbl(par)[gi[u]];
+            hv[u] = gbl(h)[gi[u]];
         }
-        bool any = false;
 #pragma unroll
-        for (int u = 0; u < U; ++u) any |= pw[u] != 0ull;
-        if (!any) continue;  // (wave-uniform: every lane loaded the same words)
-        uint32_t e[U];
-        float hv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            e[u] = valid[u] ? gbl(par)[gi[u]] : kDescRes;
-            hv[u] = valid[u] ? gbl(h)[gi[u]] : 0.0f;
-        }
+        for (int u = 0; u < U; ++u)
+            if (!valid[u]) e[u] = kDescRes;
         for (int hop = 0; hop < 1 << 16; ++hop) {  // one hop per tile crossed
             bool more = false;
 #pragma unroll
@@ -905,15 +833,15 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
             const uint32_t lr = e[u] & ~kDescRes;
             const bool res = lr != 0;
             if (valid[u]) {
-                key[gi[u]] = res ? pk_make(ordf(hv[u]), lr) : kPackInf;
+                key[gi[u]] = res ? (((uint64_t)ordf(hv[u]) << 32) | (uint64_t)lr) : kPackInf;
                 fixedv[gi[u]] = res ? 1 : 0;
                 if (want_lev && !res && !gbl(B.mask)[gi[u] - B.base]) lev = max(lev, ordf(hv[u]));
             }
             const uint64_t op = __ballot(valid[u] && !res);
             const uint64_t fi = __ballot(valid[u] && res);
-            if (lane == 0 && pw[u]) {
-                if (op) open[B.fbase + w0 + u] |= op;
-                if (fi) chg[B.fbase + w0 + u] |= fi;
+            if (lane == 0 && w0 + u < wend) {
+                open[B.fbase + w0 + u] = op;
+                chg[B.fbase + w0 + u] = fi;
             }
             cnt_open += lane == 0 ? (uint32_t)__popcll(op) : 0u;
         }
@@ -928,8 +856,7 @@ __global__ void __launch_bounds__(256) k_descent_init(const BlockDesc* __restric
     }
 }
 template __global__ void k_descent_init<8>(const BlockDesc*, const BlockStat*, const float*, const uint32_t*,
-                                           const uint64_t*, uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*,
-                                           uint32_t*);
+                                           uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*, uint32_t*);
 
 // One iteration of the frontier relaxation.  frontier = (neighbours of the voxels changed in
 // the previous iteration) & open; every frontier voxel recomputes K = f(min of its

@@ -131,6 +131,15 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
     const bool shortcut = MODE == CC_CROP && a.touched && !B.mask;
     uint32_t sl_lab[PER];
     uint32_t shortm = 0;
+    // the run starts' scan keys are first folded per label in an LDS table (a tile holds a few
+    // labels): one global atomic per (tile, label) instead of one per run start (config 3:
+    // 7.5 ms -> see DESIGN §3 for the per-run-start atomics)
+    constexpr int kSlots = MODE == CC_CROP ? 64 : 1;
+    __shared__ uint32_t slk[kSlots], slv[kSlots];
+    if (shortcut && threadIdx.x < kSlots) {
+        slk[threadIdx.x] = 0u;
+        slv[threadIdx.x] = 0xFFFFFFFFu;
+    }
     {
         uint64_t l0[PER];
         uint32_t l1[PER];
@@ -192,9 +201,21 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             vv[j] = ((inm >> j) & 1u) ? v : kLNone;
         }
         if (shortcut) {
+            // one touched-flag load per run of equal labels along the wave (its first lane), the
+            // run's lanes take it by shuffle
+            const int ln = threadIdx.x & 63;
+            const uint64_t upto = ln == 63 ? ~0ull : ((2ull << ln) - 1ull);
+            int s0[PER];
             uint32_t tch[PER];
 #pragma unroll
-            for (int j = 0; j < PER; ++j) tch[j] = vv[j] != kLNone ? gbl(a.touched)[B.base + vv[j]] : 1u;
+            for (int j = 0; j < PER; ++j) {
+                const uint32_t lp = (uint32_t)__shfl_up((int)vv[j], 1);
+                const bool st = ln == 0 || ((threadIdx.x + j * 256) % TX) == 0 || lp != vv[j];
+                s0[j] = 63 - __builtin_clzll(__ballot(st) & upto);
+                tch[j] = (st && vv[j] != kLNone) ? gbl(a.touched)[B.base + vv[j]] : 1u;
+            }
+#pragma unroll
+            for (int j = 0; j < PER; ++j) tch[j] = (uint32_t)__shfl((int)tch[j], s0[j]);
 #pragma unroll
             for (int j = 0; j < PER; ++j)
                 if (!tch[j]) {
@@ -275,7 +296,21 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             const uint32_t lp = (uint32_t)__shfl_up((int)sl_lab[j], 1);
             const bool shp = __shfl_up((int)sh, 1) != 0;
             const bool start = sh && (lane == 0 || (c % TX) == 0 || !shp || lp != sl_lab[j]);
-            if (start) atomic_min_if(&a.first[B.base + sl_lab[j]], (uint32_t)(z + nz * (y + ny * x)));
+            if (start) {
+                const uint32_t L = sl_lab[j], f = (uint32_t)(z + nz * (y + ny * x));
+                uint32_t q = ((L * 0x9E3779B1u) >> 26) & (kSlots - 1);
+                bool done = false;
+                for (int p = 0; p < kSlots; ++p) {
+                    const uint32_t prev = atomicCAS(&slk[q], 0u, L);
+                    if (prev == 0u || prev == L) {
+                        atomicMin(&slv[q], f);
+                        done = true;
+                        break;
+                    }
+                    q = (q + 1) & (kSlots - 1);
+                }
+                if (!done) atomic_min_if(&a.first[B.base + L], f);  // table full
+            }
             if (sh) {
                 P[((int64_t)z * ny + y) * nx + x] = kShortBit | sl_lab[j];
                 continue;
@@ -293,6 +328,10 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
                 atomicOr((unsigned long long*)&a.troot[B.fbase + (gi >> 6)], 1ull << (gi & 63));
         }
         P[gi] = g;
+    }
+    if (shortcut) {
+        __syncthreads();
+        if (threadIdx.x < kSlots && slk[threadIdx.x]) atomic_min_if(&a.first[B.base + slk[threadIdx.x]], slv[threadIdx.x]);
     }
 }
 
