@@ -11,6 +11,7 @@ numpy compares them with the Python float threshold, and the Gaussian prefilter
 (sigma_prefilter > 0, vigra gaussianSmoothing + normalize) runs on the GPU too
 (ctws_threshold_components_ex).
 """
+import contextlib
 import json
 import os
 import sys
@@ -140,17 +141,23 @@ def _read_block(blocking, block_id, ds_in, mask, channel):
     return b
 
 
-def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config, keep=None):
+def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config, keep=None, started=None):
     """`_cc_block[_with_mask]` for every block of the job -> {block_id: offset}.  keep (a list):
     the blocks' labels are collected there as (block_id, bb, labels or None, count) instead of
-    written (the in-job merge writes the final ids)."""
+    written (the in-job merge writes the final ids).  started: called once the first read is
+    under way (the merge's process group starts there, its torch import overlapping the read)."""
     from cluster_tools_amd import ctws
     sigma = float(config.get('sigma_prefilter', 0) or 0)
     threshold, mode = config['threshold'], config['threshold_mode']
     channel = config.get('channel', None)
     offsets = {}
-    with ctws.Handle(_device()) as h, futures.ThreadPoolExecutor(1) as io:
+    # chunk inflate / deflate on a pool (libdeflate releases the GIL)
+    ds_in.n_threads = ds_out.n_threads = max(4, int(config.get('threads_per_job', 1)))
+    with futures.ThreadPoolExecutor(1) as io, contextlib.ExitStack() as stack:
         nxt = io.submit(_read_block, blocking, block_list[0], ds_in, mask, channel) if block_list else None
+        if started is not None:
+            started()
+        h = stack.enter_context(ctws.Handle(_device()))
         for k, block_id in enumerate(block_list):
             b = nxt.result()
             nxt = (io.submit(_read_block, blocking, block_list[k + 1], ds_in, mask, channel)
@@ -219,16 +226,24 @@ def _run_blocks_merge(job_id, blocking, ds_in, ds_out, mask, config):
     for j, blocks in enumerate(split_blocks(block_list, m['n_jobs'], consecutive=True)):
         for b in blocks:
             owner[b] = j
-    job_relabel.init_group(job_id, m['n_jobs'], m['rendezvous'], m['backend'], device=_device())
+    group = []
+
+    def start_group():
+        job_relabel.init_group(job_id, m['n_jobs'], m['rendezvous'], m['backend'], device=_device())
+        group.append(True)
+
     failed = None
     keep = []
     try:
         try:
-            run_component_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, keep=keep)
+            run_component_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, keep=keep,
+                                 started=start_group)
         except Exception as e:  # still take part in the exchange: every job then raises
             import traceback
             traceback.print_exc()
             failed = e
+        if not group:   # (failed before its first read)
+            start_group()
         merge_in_job(job_id, [] if failed else keep, blocking, block_list, owner, dict(m, tmp_folder=config['tmp_folder']),
                      ds_out, log=fu.log, device=_device(), failed=failed is not None)
     finally:

@@ -193,17 +193,25 @@ def merge_in_job(job_id, results, blocking, block_list, owner, config, ds_out, l
     _agree(err, comm_dev, 'merging the assignments')
     err = None
     try:
+        from cluster_tools_amd.watershed.job_relabel import write_blocks
         assignments = np.load(_assignments_file(tmp))
-        # Write (write.py:178-211): nonzero labels + the block's offset through the assignments
-        for bid, bb, lab, _ in results:
+        for bid, _, _, _ in results:
             if bid in empty:
                 log("processed block %i" % bid)
-                continue
-            seg = to_numpy(lab).astype('uint64', copy=True)
-            nz = seg != 0
-            seg[nz] = assignments[seg[nz] + np.uint64(offsets[bid])]
-            ds_out[bb] = seg
-            log("processed block %i" % bid)
+
+        def final_ids():
+            # Write (write.py:178-211): nonzero label l of the block -> assignments[l + offset],
+            # as one table lookup per voxel (the block's labels are 0..count-1)
+            for bid, bb, lab, cnt in results:
+                if bid in empty:
+                    continue
+                lut = np.zeros(cnt, dtype='uint64')
+                lut[1:] = assignments[offsets[bid] + 1:offsets[bid] + cnt]
+                lab = to_numpy(lab)
+                yield bid, bb, np.take(lut, lab.view('int64') if lab.dtype == np.uint64 else lab)
+
+        # the chunks of all blocks through one pool, each block submitted once its ids are there
+        write_blocks(ds_out, final_ids(), log)
         if job_id == 0:
             ds_out.attrs['maxId'] = int(assignments.max()) if len(assignments) else 0
     except Exception as e:  # noqa: BLE001

@@ -24,6 +24,7 @@ def main():
     ap.add_argument('--max-jobs', type=int, default=4)
     ap.add_argument('--no-check', action='store_true')
     ap.add_argument('--merge-in-job', type=int, default=1)
+    ap.add_argument('--keep-logs', default='', help='copy the jobs\' logs to this directory')
     args = ap.parse_args()
     shape = tuple(int(s) for s in args.shape.split(','))
     bs = [int(s) for s in args.block.split(',')]
@@ -55,6 +56,8 @@ def main():
         common = dict(tmp_folder=os.path.join(tmp, 'tmp'), config_dir=cfg, max_jobs=args.max_jobs)
         from cluster_tools_amd.utils.task_utils import DummyTask
         t0 = time.perf_counter()
+        import datetime
+        started_at = str(datetime.datetime.now())
         if args.merge_in_job:
             ok1 = True
             t1 = t0
@@ -72,7 +75,7 @@ def main():
         rec = {'workload': 'ThresholdedComponentsWorkflow, %s float32 blobs (n5 gzip), blocks %s, %d jobs'
                            % ('x'.join(map(str, shape)), 'x'.join(map(str, bs)), args.max_jobs),
                'merge_in_job': bool(args.merge_in_job), 'ok': bool(ok1 and ok2),
-               'total_s': round(t2 - t0, 2), 'gvoxel_s': round(n / (t2 - t0) / 1e9, 4)}
+               'started_at': started_at, 'total_s': round(t2 - t0, 2), 'gvoxel_s': round(n / (t2 - t0) / 1e9, 4)}
         if not args.merge_in_job:
             rec.update(block_components_s=round(t1 - t0, 2), rest_s=round(t2 - t1, 2),
                        block_components_gvoxel_s=round(n / (t1 - t0) / 1e9, 4))
@@ -85,6 +88,12 @@ def main():
             with vu.file_reader(path, 'r') as f:
                 rec['bit_exact'] = bool(np.array_equal(f['cc'][:], ref) and np.array_equal(f['ass'][:], ref_ass))
         print(json.dumps(rec), flush=True)
+        if args.keep_logs:
+            os.makedirs(args.keep_logs, exist_ok=True)
+            for root, _, files in os.walk(os.path.join(tmp, 'tmp')):
+                for fn in files:
+                    if fn.endswith('.log'):
+                        shutil.copy(os.path.join(root, fn), os.path.join(args.keep_logs, fn))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
