@@ -135,8 +135,6 @@ struct ctws_handle {
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
     int output_tile = 1;   // CTWS_OUTPUT_TILE=0: cropped blocks through the word-tiled k_output
-    int crop_short = 0;    // CTWS_CROP_SHORT=1: labels that never leave the inner block skip the unions
-                           // (measured no faster, DESIGN §3: off)
     int gauss_w = 0;            // CTWS_GAUSS_W (8, 16, 32): x positions per sliding-window column tile
     int gauss_yx = 1;           // CTWS_GAUSS_YX=0: separate y and x passes instead of the fused tile kernel
     int words_per_wave = 32;    // CTWS_WORDS_PER_WAVE: words per wave of the word-tiled kernels
@@ -1212,7 +1210,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
         // the seed CC's member bitmap (CcArgs::troot for SEED): its parents are members-only
         HIPCHK(hipMemsetAsync(w.fseed, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed, nullptr, nullptr};
+        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed};
         if (pl.nd_ws == 3) {
             using T = CcTileM<3, CC_SEED>;  // (= the plateau tile)
             const dim3 tg(tiles8(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
@@ -1558,25 +1556,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         mark("finalize");
 
         // ---- halo crop CC (labelVolumeWithBackground) + uint64 output --------------------------
-        // crop CC shortcut (unmasked cropped blocks; CTWS_CROP_SHORT=1 on): labels that meet no
-        // inner face with a halo beyond it are whole components (k_tilecc.hip); per label in the
-        // (free) dt / sm arrays: touched flags, first voxel in scan order
-        uint32_t* crop_touched = (uint32_t*)w.dt;
-        uint32_t* crop_first = (uint32_t*)w.sm;
-        const bool crop_short = any_crop && h->crop_short;
         if (any_crop) {
             // tile roots of the crop CC marked in the (free) frontier bitmap front0
             HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-            HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
-            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0, nullptr, nullptr};
-            const dim3 lg((unsigned)std::min<int64_t>((maxN + 255) / 256, 1024), nb);
-            if (crop_short) {
-                ca.touched = crop_touched;
-                ca.first = crop_first;
-                k_crop_init<<<lg, 256, 0, h->stream>>>(w.desc, w.stat, crop_touched, crop_first);
-                k_crop_faces<<<dim3((unsigned)std::min<int64_t>((maxN / 16 + 255) / 256 + 1, 1024), nb), 256, 0,
-                               h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, crop_touched);
-            }
+            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0};
             const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;
@@ -1589,13 +1572,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 k_tile_cc<2, CC_CROP><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
                 k_tile_merge<2, CC_CROP><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             }
-            if (crop_short) k_crop_short_roots<<<lg, 256, 0, h->stream>>>(w.desc, w.stat, crop_touched, crop_first, w.W);
+            HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
             k_flatten_tile_roots<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0, w.W);
             k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
             k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
             k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
             k_root_label<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp);
-            if (crop_short) k_crop_short_ids<<<lg, 256, 0, h->stream>>>(w.desc, w.stat, crop_touched, crop_first, w.PF);
             LAUNCHCHK();
         }
         mark("crop_cc");
@@ -1607,16 +1589,16 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const bool crop_tiles = any_crop && h->output_tile;
         // (k_output still writes the uncropped blocks and the empty ones: constant offset)
         k_output<<<wtig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, w.PF, w.sb, w.soff,
-                                             (unsigned long long*)w.W, crop_tiles ? 1 : 0, crop_first);
+                                             (unsigned long long*)w.W, crop_tiles ? 1 : 0);
         if (crop_tiles) {
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;
                 const dim3 tg(tiles8(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
-                k_output_crop<3><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0, crop_first);
+                k_output_crop<3><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0);
             } else {
                 using T = CcTile<2>;
                 const dim3 tg(tiles8(cdiv(maxIZ, T::TZ) * cdiv(maxIY, T::TY) * cdiv(maxIX, T::TX)), nb);
-                k_output_crop<2><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0, crop_first);
+                k_output_crop<2><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.front0);
             }
         }
         if (any_plain) k_count_ids<<<dim3(64, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.W);
@@ -2284,7 +2266,6 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_FRONTIER_GRID")) h->frontier_grid = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_REPS")) h->frontier_reps = std::max(1, std::atoi(t));
     if (const char* t = std::getenv("CTWS_FRONTIER_DIR")) h->frontier_dir = std::atoi(t) ? 1 : 0;
-    if (const char* t = std::getenv("CTWS_CROP_SHORT")) h->crop_short = std::atoi(t) ? 1 : 0;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counter, kCounterBytes, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&h->h_taps, 6 * kTapSlot * sizeof(double), hipHostMallocDefault) != hipSuccess) {

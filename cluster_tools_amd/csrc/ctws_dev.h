@@ -394,9 +394,6 @@ constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
 // config-1 2-D test config: VI 0.029 against the model's 0) -- not adopted.
 constexpr uint32_t kDMax = 4095;
 
-// the key of a seed or of a voxel entered from below: (h, 0, label)
-__device__ __forceinline__ uint64_t pk_make(uint32_t hb, uint32_t label) { return ((uint64_t)hb << 32) | label; }
-
 // K(q) = f_q(min over the neighbours): a neighbour key `best` pushed into voxel q of height hb
 __device__ __forceinline__ uint64_t f_packed(uint32_t hb, uint64_t best) {
     const uint32_t c = (uint32_t)(best >> 32);

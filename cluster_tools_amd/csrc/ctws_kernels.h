@@ -107,7 +107,7 @@ __global__ void k_root_label(const BlockDesc*, const BlockStat*, int, uint32_t*,
 __global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const float*,
                              uint32_t*, uint64_t*, uint8_t*, int);
 __global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
-                         const uint32_t*, const uint32_t*, unsigned long long*, int, const uint32_t*);
+                         const uint32_t*, const uint32_t*, unsigned long long*, int);
 __global__ void k_count_ids(const BlockDesc*, BlockStat*, const uint64_t*);
 
 // k_tilecc.hip: LDS block-based union-find (plateaus, seed CC, halo-crop CC)
@@ -122,15 +122,7 @@ struct CcArgs {
     uint64_t* troot;       // CROP: tile-root bitmap (inner C index, per block at fbase), zeroed;
                            // SEED: the members (seed voxels; outer rows), zeroed.  The seed forest's
                            // parents are written for members only: readers test this bitmap first
-    // CROP shortcut (unmasked blocks; null: off): per block label -> 1 if the label meets an inner
-    // face that has a halo beyond it (k_crop_faces), and the label's first voxel in scan order
-    // (atomicMin by k_tile_cc), both indexed at B.base
-    const uint32_t* touched;
-    uint32_t* first;
 };
-// P entry of a crop voxel whose label never leaves the inner block: kShortBit | label (the label
-// is one component, rooted at its first voxel; k_crop_short_roots / k_output_crop)
-constexpr uint32_t kShortBit = 0x40000000u;
 template <int ND>
 struct CcTile;
 template <>
@@ -155,11 +147,7 @@ struct CcTileM<3, CC_SEED> : CcTileM<3, CC_PLATEAU> {};
 template <int ND, int MODE>
 __global__ void k_tile_cc(const BlockDesc*, const BlockStat*, CcArgs, uint32_t*);
 template <int ND>
-__global__ void k_output_crop(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*);
-__global__ void k_crop_init(const BlockDesc*, const BlockStat*, uint32_t*, uint32_t*);
-__global__ void k_crop_faces(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, int, uint32_t*);
-__global__ void k_crop_short_roots(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, uint64_t*);
-__global__ void k_crop_short_ids(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*, const uint32_t*);
+__global__ void k_output_crop(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*);
 template <int ND, int MODE>
 __global__ void k_tile_merge(const BlockDesc*, const BlockStat*, CcArgs, uint32_t*);
 

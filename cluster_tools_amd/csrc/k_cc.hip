@@ -358,18 +358,11 @@ __device__ __forceinline__ int64_t outer_of_inner(const BlockDesc& B, int z, int
 // Uncropped blocks also mark their final labels in the (zeroed) bitmap W, so that
 // k_count_ids can count the distinct output ids (the label sets have gaps after the size
 // filter).
-// inner C index of the voxel with inner scan key f = z + IZ * (y + IY * x)
-__device__ __forceinline__ uint32_t short_root(const BlockDesc& B, uint32_t f) {
-    const uint32_t z = f % (uint32_t)B.IZ, t = f / (uint32_t)B.IZ;
-    const uint32_t y = t % (uint32_t)B.IY, x = t / (uint32_t)B.IY;
-    return (z * (uint32_t)B.IY + y) * (uint32_t)B.IX + x;
-}
-
 __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D, BlockStat* S,
                                                 const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
                                                 int packed, const uint32_t* __restrict__ PFg,
                                                 const uint32_t* __restrict__ sb, const uint32_t* __restrict__ soff,
-                                                unsigned long long* W, int skip_crop, const uint32_t* __restrict__ first) {
+                                                unsigned long long* W, int skip_crop) {
     const BlockDesc& B = D[blockIdx.y];
     const bool active = S[blockIdx.y].active;
     if (skip_crop && active && B.crop) return;  // k_output_crop writes it
@@ -388,15 +381,12 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
         if (active) {
             uint32_t l;
             if (B.crop) {
-                // member -> its tile root -> (the tile root's global root, k_flatten_tile_roots);
-                // a shortcut voxel (kShortBit | label) -> its label's first voxel, a root
+                // member -> its tile root -> (the tile root's global root, k_flatten_tile_roots)
                 const uint32_t p = gbl(P)[iq];
                 l = 0u;
                 if (p != kNoParent) {
                     if (p & kRootBit) {
                         l = p & ~kRootBit;
-                    } else if (p & kShortBit) {
-                        l = first[B.base + (p & ~kShortBit)];  // the label's id (k_crop_short_ids)
                     } else {
                         const uint32_t q = P[p];
                         l = (q & kRootBit) ? (q & ~kRootBit) : (P[q] & ~kRootBit);
@@ -440,8 +430,7 @@ __global__ void __launch_bounds__(256) k_output(const BlockDesc* __restrict__ D,
 // root's label from LDS: no dependent global load per member (k_output: two).
 template <int ND>
 __global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict__ D, BlockStat* S,
-                                                     const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ TR,
-                                                     const uint32_t* __restrict__ first) {
+                                                     const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ TR) {
     using T = CcTile<ND>;
     constexpr int TZ = T::TZ, TY = T::TY, TX = T::TX, TN = TZ * TY * TX, PER = TN / 256;
     __shared__ uint32_t sl[TN];
@@ -469,14 +458,12 @@ __global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict
         e[j] = P[gi[j]];
         root[j] = (gbl(TR)[B.fbase + (gi[j] >> 6)] >> (gi[j] & 63)) & 1ull;
     }
-    // tile roots: their label (a global root carries it; the others point at their global root);
-    // shortcut voxels (kShortBit | label): the label's id (k_crop_short_ids)
+    // tile roots: their label (a global root carries it; the others point at their global root)
     uint32_t rl[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-        const bool sh = in[j] && e[j] != kNoParent && !(e[j] & kRootBit) && (e[j] & kShortBit);
         const bool need = in[j] && root[j] && e[j] != kNoParent && !(e[j] & kRootBit);
-        rl[j] = sh ? gbl(first)[B.base + (e[j] & ~kShortBit)] : P[need ? e[j] : 0u];  // all in flight
+        rl[j] = P[need ? e[j] : 0u];  // unconditional: all in flight
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -498,11 +485,7 @@ __global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict
         if (!in[j]) continue;
         uint32_t l = 0u;
         if (e[j] != kNoParent) {
-            if (e[j] & kRootBit) {
-                l = e[j] & ~kRootBit;  // a global root (shortcut roots are no tile roots)
-            } else if (e[j] & kShortBit) {
-                l = rl[j] & ~kRootBit;
-            } else if (root[j]) {
+            if (root[j]) {
                 l = sl[threadIdx.x + j * 256];
             } else {
                 const int d = (int)(e[j] - tb);
@@ -525,104 +508,8 @@ __global__ void __launch_bounds__(256) k_output_crop(const BlockDesc* __restrict
     if (threadIdx.x == 0 && mx) atomic_max_if(&S[blockIdx.y].max_label, mx);
     if (__ballot(zero_in) && (threadIdx.x & 63) == 0 && !S[blockIdx.y]._p[0]) atomicOr(&S[blockIdx.y]._p[0], 1u);
 }
-template __global__ void k_output_crop<2>(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*,
-                                          const uint32_t*);
-template __global__ void k_output_crop<3>(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*,
-                                          const uint32_t*);
-
-// ---- crop CC shortcut (k_tile_cc<.., CC_CROP>): labels that never leave the inner block ---------
-// label range of a block after the flood and the regrow: seed labels (and auto seeds)
-__device__ __forceinline__ int64_t crop_label_bound(const BlockStat& st) {
-    return (int64_t)max(st.n_seeds, st.n_auto) + 1;
-}
-__device__ __forceinline__ bool crop_short_block(const BlockDesc& B, const BlockStat& st) {
-    return st.active && B.crop && !B.mask;
-}
-
-__global__ void __launch_bounds__(256) k_crop_init(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                   uint32_t* __restrict__ touched, uint32_t* __restrict__ first) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!crop_short_block(B, S[blockIdx.y])) return;
-    const int64_t n = crop_label_bound(S[blockIdx.y]);
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        touched[B.base + i] = 0u;
-        first[B.base + i] = 0xFFFFFFFFu;
-    }
-}
-
-// labels on an inner face with a halo beyond it (they may continue outside the inner block);
-// 2-D ws labels never cross slices, so only the y / x faces count there
-__global__ void __launch_bounds__(256) k_crop_faces(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                    const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
-                                                    int packed, uint32_t* __restrict__ touched) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!crop_short_block(B, S[blockIdx.y])) return;
-    const int64_t fz = (int64_t)B.IY * B.IX, fy = (int64_t)B.IZ * B.IX, fx = (int64_t)B.IZ * B.IY;
-    const bool zh[2] = {B.nd_ws == 3 && B.iz0 > 0, B.nd_ws == 3 && B.iz0 + B.IZ < B.Z};
-    const bool yh[2] = {B.iy0 > 0, B.iy0 + B.IY < B.Y};
-    const bool xh[2] = {B.ix0 > 0, B.ix0 + B.IX < B.X};
-    const int64_t n = 2 * (fz + fy + fx);
-    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
-        int z, y, x;
-        int64_t r = k;
-        if (r < 2 * fz) {
-            const int side = (int)(r / fz);
-            if (!zh[side]) continue;
-            r -= side * fz;
-            z = side ? B.IZ - 1 : 0;
-            y = (int)(r / B.IX);
-            x = (int)(r - (int64_t)y * B.IX);
-        } else if ((r -= 2 * fz) < 2 * fy) {
-            const int side = (int)(r / fy);
-            if (!yh[side]) continue;
-            r -= side * fy;
-            y = side ? B.IY - 1 : 0;
-            z = (int)(r / B.IX);
-            x = (int)(r - (int64_t)z * B.IX);
-        } else {
-            r -= 2 * fy;
-            const int side = (int)(r / fx);
-            if (!xh[side]) continue;
-            r -= side * fx;
-            x = side ? B.IX - 1 : 0;
-            z = (int)(r / B.IY);
-            y = (int)(r - (int64_t)z * B.IY);
-        }
-        const int64_t o = ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0);
-        const uint32_t l = flood_label(lab, key, packed, B.base + o);
-        if (l && !touched[B.base + l]) touched[B.base + l] = 1u;
-    }
-}
-
-// the shortcut labels' roots: the scan-key bit of their first voxel in W (zeroed beforehand)
-__global__ void __launch_bounds__(256) k_crop_short_roots(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                          const uint32_t* __restrict__ touched,
-                                                          const uint32_t* __restrict__ first, uint64_t* __restrict__ Wg) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!crop_short_block(B, S[blockIdx.y])) return;
-    const int64_t n = crop_label_bound(S[blockIdx.y]);
-    for (int64_t l = 1 + (int64_t)blockIdx.x * 256 + threadIdx.x; l < n; l += (int64_t)gridDim.x * 256) {
-        const uint32_t f = first[B.base + l];
-        if (touched[B.base + l] || f == 0xFFFFFFFFu) continue;
-        atomicOr((unsigned long long*)&Wg[B.wbase + (f >> 6)], 1ull << (f & 63));
-    }
-}
-
-// after k_root_label: a shortcut label's first voxel -> the label's output id, in place (the
-// outputs then read one table entry per voxel instead of first voxel -> root)
-__global__ void __launch_bounds__(256) k_crop_short_ids(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                        const uint32_t* __restrict__ touched, uint32_t* __restrict__ first,
-                                                        const uint32_t* __restrict__ PFg) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!crop_short_block(B, S[blockIdx.y])) return;
-    const uint32_t* P = PFg + B.ibase;
-    const int64_t n = crop_label_bound(S[blockIdx.y]);
-    for (int64_t l = 1 + (int64_t)blockIdx.x * 256 + threadIdx.x; l < n; l += (int64_t)gridDim.x * 256) {
-        const uint32_t f = first[B.base + l];
-        if (touched[B.base + l] || f == 0xFFFFFFFFu) continue;
-        first[B.base + l] = P[short_root(B, f)] & ~kRootBit;
-    }
-}
+template __global__ void k_output_crop<2>(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*);
+template __global__ void k_output_crop<3>(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*);
 
 // distinct ids of an uncropped block: popcount of its label bitmap (k_output) -> n_cc
 __global__ void __launch_bounds__(256) k_count_ids(const BlockDesc* __restrict__ D, BlockStat* S,

@@ -713,14 +713,15 @@ __global__ void __launch_bounds__(kDescThreads) __attribute__((amdgpu_waves_per_
     }
     // tile roots: seed label (seeds) or 0 (local minima without a seed, ties), kept in sh[]
     // (the heights are no longer read).  The label comes from the seed entry loaded above: a
-    // cc root carries it, a non-root cc entry needs its root's (one more load, unconditional)
+    // cc root carries it, a non-root cc entry needs its root's (one more load, seeds only: a
+    // wave without such a seed voxel skips the load instruction)
     {
         uint32_t rl[PER];
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const uint32_t v = sv[k];
             const bool need = cc && v != kNoParent && !(v & kRootBit) && ((seedm >> k) & 1u);
-            rl[k] = gbl(cc ? cc : lab)[B.base + (need ? v : 0u)];  // unconditional: all in flight
+            rl[k] = need ? gbl(cc)[B.base + v] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < PER; ++k) {

@@ -123,23 +123,6 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
     // space) so that all of a thread's loads are in flight together; non-members and positions
     // outside the domain are selected away afterwards.  Same values as cc_value.
     uint32_t vv[PER];
-    // CROP shortcut (a.touched, unmasked blocks): a label that meets no inner face with a halo
-    // beyond never left the inner block, and a flood label's region is connected (every voxel
-    // took its label from a neighbour, back to the seed component), so it is one component of
-    // the crop CC, rooted at its first voxel in scan order.  Its voxels skip the unions: P =
-    // kShortBit | label, and the run starts along x fold their scan key into first[label].
-    const bool shortcut = MODE == CC_CROP && a.touched && !B.mask;
-    uint32_t sl_lab[PER];
-    uint32_t shortm = 0;
-    // the run starts' scan keys are first folded per label in an LDS table (a tile holds a few
-    // labels): one global atomic per (tile, label) instead of one per run start (config 3:
-    // 7.5 ms -> see DESIGN §3 for the per-run-start atomics)
-    constexpr int kSlots = MODE == CC_CROP ? 64 : 1;
-    __shared__ uint32_t slk[kSlots], slv[kSlots];
-    if (shortcut && threadIdx.x < kSlots) {
-        slk[threadIdx.x] = 0u;
-        slv[threadIdx.x] = 0xFFFFFFFFu;
-    }
     {
         uint64_t l0[PER];
         uint32_t l1[PER];
@@ -184,7 +167,6 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
                                       : ((uint32_t)l0[j] & ~kFixedBit);
                 if (!l1[j]) l = 0u;  // masked
                 v = l ? l : kLNone;
-                sl_lab[j] = l;
             } else if (MODE == CC_PLATEAU) {
                 v = (l0[j] & 2) ? (l1[j] == 0x80000000u ? 0u : l1[j]) : kLNone;
             } else {
@@ -199,29 +181,6 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
                 }
             }
             vv[j] = ((inm >> j) & 1u) ? v : kLNone;
-        }
-        if (shortcut) {
-            // one touched-flag load per run of equal labels along the wave (its first lane), the
-            // run's lanes take it by shuffle
-            const int ln = threadIdx.x & 63;
-            const uint64_t upto = ln == 63 ? ~0ull : ((2ull << ln) - 1ull);
-            int s0[PER];
-            uint32_t tch[PER];
-#pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const uint32_t lp = (uint32_t)__shfl_up((int)vv[j], 1);
-                const bool st = ln == 0 || ((threadIdx.x + j * 256) % TX) == 0 || lp != vv[j];
-                s0[j] = 63 - __builtin_clzll(__ballot(st) & upto);
-                tch[j] = (st && vv[j] != kLNone) ? gbl(a.touched)[B.base + vv[j]] : 1u;
-            }
-#pragma unroll
-            for (int j = 0; j < PER; ++j) tch[j] = (uint32_t)__shfl((int)tch[j], s0[j]);
-#pragma unroll
-            for (int j = 0; j < PER; ++j)
-                if (!tch[j]) {
-                    shortm |= 1u << j;
-                    vv[j] = kLNone;  // no unions
-                }
         }
     }
 #pragma unroll
@@ -290,32 +249,6 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             }
             if (!mem) continue;
         }
-        if (shortcut) {
-            // the x-run starts of the short voxels (the smallest scan key of the run: smallest x)
-            const bool sh = (shortm >> j) & 1u;
-            const uint32_t lp = (uint32_t)__shfl_up((int)sl_lab[j], 1);
-            const bool shp = __shfl_up((int)sh, 1) != 0;
-            const bool start = sh && (lane == 0 || (c % TX) == 0 || !shp || lp != sl_lab[j]);
-            if (start) {
-                const uint32_t L = sl_lab[j], f = (uint32_t)(z + nz * (y + ny * x));
-                uint32_t q = ((L * 0x9E3779B1u) >> 26) & (kSlots - 1);
-                bool done = false;
-                for (int p = 0; p < kSlots; ++p) {
-                    const uint32_t prev = atomicCAS(&slk[q], 0u, L);
-                    if (prev == 0u || prev == L) {
-                        atomicMin(&slv[q], f);
-                        done = true;
-                        break;
-                    }
-                    q = (q + 1) & (kSlots - 1);
-                }
-                if (!done) atomic_min_if(&a.first[B.base + L], f);  // table full
-            }
-            if (sh) {
-                P[((int64_t)z * ny + y) * nx + x] = kShortBit | sl_lab[j];
-                continue;
-            }
-        }
         if (z >= nz || y >= ny || x >= nx) continue;
         uint32_t g = kNoParent;
         const int64_t gi = ((int64_t)z * ny + y) * nx + x;
@@ -328,10 +261,6 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
                 atomicOr((unsigned long long*)&a.troot[B.fbase + (gi >> 6)], 1ull << (gi & 63));
         }
         P[gi] = g;
-    }
-    if (shortcut) {
-        __syncthreads();
-        if (threadIdx.x < kSlots && slk[threadIdx.x]) atomic_min_if(&a.first[B.base + slk[threadIdx.x]], slv[threadIdx.x]);
     }
 }
 
@@ -378,8 +307,7 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                     // the members only (the member bitmap a.troot says which)
                     const bool mi = MODE == CC_SEED ? bit_of(a.troot, B, i)
                                                     : (MODE != CC_PLATEAU || (a.cls[B.base + i] & 2));
-                    uint32_t pi = mi ? P[i] : kNoParent;
-                    if (MODE == CC_CROP && (pi & kShortBit) && pi != kNoParent) pi = kNoParent;  // one component already
+                    const uint32_t pi = mi ? P[i] : kNoParent;
                     if (pi != kNoParent) {
                         // the backward neighbours of (z, y, x) that leave the tile through face f
                         // (a diagonal through the tile corner belongs to the y face)
@@ -394,7 +322,7 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                             if (MODE == CC_PLATEAU && !(a.cls[B.base + q] & 2)) continue;
                             if (MODE == CC_SEED && !bit_of(a.troot, B, q)) continue;
                             const uint32_t pq = P[q];
-                            if (pq == kNoParent || (MODE == CC_CROP && (pq & kShortBit))) continue;
+                            if (pq == kNoParent) continue;
                             if (MODE != CC_SEED &&
                                 cc_value<MODE>(B, a, true, z, y, x) != cc_value<MODE>(B, a, true, qz, qy, qx))
                                 continue;

@@ -26,8 +26,6 @@ VARIANTS = {
     'no_plateau_fill': {'CTWS_PLATEAU_FILL': '0'},
     # cropped blocks' uint64 output through the word-tiled k_output instead of k_output_crop
     'output_words': {'CTWS_OUTPUT_TILE': '0'},
-    # every crop voxel through the tile unions (no shortcut for the labels inside the inner block)
-    'crop_short_on': {'CTWS_CROP_SHORT': '1'},
 }
 
 
