@@ -981,7 +981,10 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     __shared__ uint64_t sdir[kFrontierWaves][6][64];
     __shared__ uint64_t sfw[kFrontierWaves][64];
     __shared__ int spre[kFrontierWaves][64];
-    __shared__ int srow[kFrontierWaves][64];
+    // per word of the chunk (lane): its first voxel's block index, (z << 16 | y), its first x
+    __shared__ uint32_t sbase[kFrontierWaves][64];
+    __shared__ uint32_t szy[kFrontierWaves][64];
+    __shared__ int sx0[kFrontierWaves][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int lx = lane % CW, ly = (lane / CW) % CY, lz = lane / (CW * CY);
     const uint32_t n_entries = *cnt;
@@ -1082,7 +1085,10 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             }
             sfw[wv][lane] = f;
             spre[wv][lane] = incl - cnt_bits;
-            srow[wv][lane] = row * 64 + xw;  // row < 2^25 (Z * Y <= 2^22)
+            // (constant over the chunk's sweeps; z, y < 2^16, block indices < 2^32)
+            sbase[wv][lane] = (uint32_t)((int64_t)row * B.X + xw * 64);
+            szy[wv][lane] = ((uint32_t)zz << 16) | (uint32_t)yy;
+            sx0[wv][lane] = xw * 64;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             // entries per lane and step: index, loads, update as three unrolled phases (the loop
@@ -1102,12 +1108,11 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                     for (int step = 32; step > 0; step >>= 1)
                         if (spre[wv][j + step] <= e) j += step;
                     const int b = av[u] ? kth_set_bit(sfw[wv][j], e - spre[wv][j]) : 0;
-                    const int rx = srow[wv][j];
-                    const int r = rx >> 6, xq = rx & 63;
-                    zv[u] = r / B.Y;
-                    yv[u] = r - zv[u] * B.Y;
-                    xv[u] = xq * 64 + b;
-                    iv[u] = (int64_t)r * B.X + xv[u];
+                    const uint32_t zy = szy[wv][j];
+                    zv[u] = (int)(zy >> 16);
+                    yv[u] = (int)(zy & 0xFFFFu);
+                    xv[u] = sx0[wv][j] + b;
+                    iv[u] = (int64_t)sbase[wv][j] + b;
                     jv[u] = j;
                     bv[u] = b;
                 }
