@@ -2,7 +2,7 @@
 # Same-box A/B of two library builds (CTWS_LIB=$ALT vs the default libctws.so), alternating,
 # single-stream flood stage times.
 cd "${GRAFT_REPO_ROOT:-.}"
-O=gpurun_out/ab_lib
+O=gpurun_out/ab_lib${TAG:+_$TAG}
 mkdir -p $O
 export TMPDIR=/tmp
 ALT=${ALT:-cluster_tools_amd/libctws_old.so}
