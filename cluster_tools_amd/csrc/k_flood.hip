@@ -1101,8 +1101,12 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                 bool av[ILP];
 #pragma unroll
                 for (int u = 0; u < ILP; ++u) {
-                    const int e = t0 + u * 64 + lane;
-                    av[u] = e < total;
+                    // odd sweeps walk the list backwards: a later step reads what an earlier
+                    // step of the same sweep wrote, so alternating the order carries changes
+                    // both ways along the list (symmetric Gauss-Seidel over the steps)
+                    const int eo = t0 + u * 64 + lane;
+                    av[u] = eo < total;
+                    const int e = ((rep & 1) && av[u]) ? total - 1 - eo : eo;
                     int j = 0;
 #pragma unroll
                     for (int step = 32; step > 0; step >>= 1)
