@@ -153,12 +153,13 @@ struct ctws_handle {
     int edt_wz = 0;  // CTWS_EDT_WZ: the same for the z pass alone (3-D DT)
     int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
     // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words).
-    // 3-D batches with a mask default to 1x32x2 instead of 1x8x8: a masked region is one flat
-    // plateau (fin = 1) that the flood crosses hop by hop, and wider bricks in y cut the launches
-    // (config 5: 104 -> 72 ms of relaxation, 156 -> 82 launches; unmasked config 4: 33 vs 41 ms)
+    // 3-D batches with a mask: 1x32x2 was their default until round 5 (a masked region is one
+    // flat plateau the flood crosses hop by hop, and wider bricks in y cut the launches: config 5
+    // 104 -> 72 ms before the plateau fill); with the plateau fill and the alternating sweep
+    // order 1x8x8 relaxes config 5 faster (39.6 -> 36.4 ms, 132 -> 101 launches per step)
     int fchunk2[3] = {1, 64, 1};
     int fchunk3[3] = {1, 8, 8};
-    int fchunk3_masked[3] = {1, 32, 2};
+    int fchunk3_masked[3] = {1, 8, 8};
     int fchunk3_env = 0;  // CTWS_FRONTIER_CHUNK3D given: used for every 3-D batch
     int fc_cur[3] = {1, 64, 1};  // the brick of the current batch (run_batch)
     int cur_max[3] = {0, 0, 0};  // largest outer block extents (Z, Y, X) of the current batch
