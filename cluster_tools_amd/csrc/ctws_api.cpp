@@ -1278,7 +1278,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     if (pl.pass2) {
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
         k_p2_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
-                                              (uint32_t*)w.Bf, (uint32_t*)w.sm, packed ? 1 : 0);
+                                              (uint32_t*)w.Bf, (uint32_t*)w.sm, packed ? 1 : 0, descent ? 0 : 1);
         excl = (uint8_t*)w.fin;  // free after the hmap
         k_p2_excl_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, excl);
         k_p2_excl<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, excl);

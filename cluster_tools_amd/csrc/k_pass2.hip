@@ -60,9 +60,11 @@ __device__ __forceinline__ int64_t hash_find(const uint64_t* hk, int64_t cap, ui
     return -1;
 }
 
+// (32-bit divisions: a block holds fewer than 2^31 voxels, ctws_api.cpp refuses larger ones)
 __device__ __forceinline__ void inner_to_zyx(int64_t i, int64_t YX, int X, int& z, int& y, int& x) {
-    z = (int)(i / YX);
-    const int rem = (int)(i - z * YX);
+    const uint32_t ii = (uint32_t)i, yx = (uint32_t)YX;
+    z = (int)(ii / yx);
+    const int rem = (int)(ii - (uint32_t)z * yx);
     y = rem / X;
     x = rem - y * X;
 }
@@ -94,8 +96,8 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
     const int64_t YX = (int64_t)B.Y * B.X;
     const uint32_t* PF = PFg + B.base;
     BLOCK_LOOP(i, B) {
-        int z, y, x;
-        inner_to_zyx(i, YX, B.X, z, y, x);
+        // the slice (2-D ws only: 3-D keys carry no position)
+        const int z = B.nd_ws == 3 ? 0 : (int)((uint32_t)i / (uint32_t)YX);
         const uint64_t u = gbl(B.init)[i];
         uint64_t k = kEmptyKey;
         if (u != 0) {
@@ -179,7 +181,7 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
                                                   const float* __restrict__ h, uint32_t* __restrict__ lab,
                                                   uint64_t* __restrict__ key /* in: vkey */,
                                                   uint8_t* __restrict__ fixedv, uint32_t* __restrict__ oldv,
-                                                  uint32_t* __restrict__ oldt, int packed) {
+                                                  uint32_t* __restrict__ oldt, int packed, int write_keys) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -200,19 +202,27 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
         }
         pos = (uint32_t)__shfl((int)pos, s0);
         l = (uint32_t)__shfl((int)l, s0);
+        // write_keys = 0 (the descent flood): k_descent_init writes every key and fixed flag from
+        // lab, so only lab is written here (and no height is read)
         if (k == kEmptyKey) {
             lab[B.base + i] = 0;
-            fixedv[B.base + i] = 0;
+            if (write_keys) fixedv[B.base + i] = 0;
             continue;  // key stays kEmptyKey == kInfKey
         }
         lab[B.base + i] = l | kFixedBit;
-        key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
-        fixedv[B.base + i] = 1;
-        int z, y, x;
-        inner_to_zyx(i, YX, B.X, z, y, x);
-        if (scan_key(B, z, y, x) == pos) {
-            oldv[B.base + l] = (uint32_t)k;
-            oldt[B.base + l] = (uint32_t)((k >> 32) & 1u);
+        if (write_keys) {
+            key[B.base + i] = ((uint64_t)ordf(h[B.base + i]) << 32) | (packed ? (uint64_t)l : 0ull);
+            fixedv[B.base + i] = 1;
+        }
+        // the value's first voxel in scan order has the smallest x of its x run: a run start, or
+        // a row's first voxel (its memory predecessor ends the previous row; N < 2^31)
+        if (start || (uint32_t)i % (uint32_t)B.X == 0u) {
+            int z, y, x;
+            inner_to_zyx(i, YX, B.X, z, y, x);
+            if (scan_key(B, z, y, x) == pos) {
+                oldv[B.base + l] = (uint32_t)k;
+                oldt[B.base + l] = (uint32_t)((k >> 32) & 1u);
+            }
         }
     }
 }
