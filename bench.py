@@ -724,7 +724,7 @@ def main():
     ap.add_argument('--no-threshcc', action='store_true', help='skip the thresholded-components block leg')
     ap.add_argument('--no-config5', action='store_true',
                     help='skip the config-5 leg (one GPU\'s z-slab of the 2048^3 uint8 two-pass workload)')
-    ap.add_argument('--config5-steps', type=int, default=2)
+    ap.add_argument('--config5-steps', type=int, default=3)
     ap.add_argument('--strong-steps', type=int, default=3)
     ap.add_argument('--e2e-z', type=int, default=None,
                     help='z extent of the end-to-end volume (default: the whole config volume)')
@@ -777,6 +777,29 @@ def main():
     rf = roofline_of(cfg, m)
     value = m['inner_all'] * args.steps / m['dt'] / 1e9
 
+    # ---- config 5 (VERDICT r04 #3): one rank's z-slab of the 2048^3 uint8 masked volume through
+    # the workflow's two-pass schedule (pass 1, the z-halo exchange, pass 2 in the dependency
+    # levels of the sequential loop) -- BASELINE.json's heaviest config, beside the headline
+    c5 = None
+    if not args.no_config5 and args.config != 5:
+        progress('config 5 leg')
+        torch.cuda.empty_cache()
+        s5 = run_workload(5, 'weak', rank, world, dev, args.config5_steps, 2, args.streams)
+        r5 = roofline_of(CONFIGS[5], s5)
+        fl5 = sum(s5['stage_1'].get(p, 0.0) for p in STAGE_PARTS['flood'])
+        c5 = {'value': round(s5['inner_all'] * s5['steps'] / s5['dt'] / 1e9, 4), 'unit': 'Gvoxel/s',
+              'ms_per_step': round(r5['ms_per_step'], 3), 'ms_per_step_ranks': s5['ms_ranks'],
+              'steps': s5['steps'], 'n_gpus': world, 'scaling': 'weak', 'workload': CONFIGS[5]['workload'],
+              'blocks_per_gpu': s5['nblocks'], 'inner_voxels_per_gpu': s5['inner_vox'],
+              'outer_voxels_per_gpu': s5['outer_vox'], 'pass2_outer_voxels': s5['pass2_outer'],
+              'launch_groups': s5['ngroups'],
+              'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(r5['alg_total'] / s5['inner_vox'], 1),
+                                    'achieved': round(r5['pipe'], 1), 'unit': 'GB/s',
+                                    'frac': round(r5['pipe'] / HBM_PEAK_GBS, 4)},
+              'flood_ms_1stream': round(fl5, 3),
+              'flood_frac': round(12 * s5['outer_vox'] / (fl5 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if fl5 > 0 else None,
+              'stage_ms_1stream': {k: round(v, 3) for k, v in s5['stage_1'].items() if v >= 0.05}}
+
     # ---- strong scaling of config 4: the 1024^3 volume in z-slabs over the ranks -------------
     strong = None
     if not args.no_strong and not (args.config == 4 and args.scaling == 'strong'):
@@ -792,29 +815,6 @@ def main():
                   'flood_ms_1stream_rank0': round(sum(s['stage_1'].get(p, 0.0) for p in STAGE_PARTS['flood']), 3),
                   'offset_scan': 'per step: all-gather of the per-block distinct-id counts (%s) + exclusive scan'
                                  % (backend or 'single process')}
-
-    # ---- config 5 (VERDICT r04 #3): one rank's z-slab of the 2048^3 uint8 masked volume through
-    # the workflow's two-pass schedule (pass 1, the z-halo exchange, pass 2 in the dependency
-    # levels of the sequential loop) -- BASELINE.json's heaviest config, beside the headline
-    c5 = None
-    if not args.no_config5 and args.config != 5:
-        progress('config 5 leg')
-        torch.cuda.empty_cache()
-        s5 = run_workload(5, 'weak', rank, world, dev, args.config5_steps, 1, args.streams)
-        r5 = roofline_of(CONFIGS[5], s5)
-        fl5 = sum(s5['stage_1'].get(p, 0.0) for p in STAGE_PARTS['flood'])
-        c5 = {'value': round(s5['inner_all'] * s5['steps'] / s5['dt'] / 1e9, 4), 'unit': 'Gvoxel/s',
-              'ms_per_step': round(r5['ms_per_step'], 3), 'ms_per_step_ranks': s5['ms_ranks'],
-              'steps': s5['steps'], 'n_gpus': world, 'scaling': 'weak', 'workload': CONFIGS[5]['workload'],
-              'blocks_per_gpu': s5['nblocks'], 'inner_voxels_per_gpu': s5['inner_vox'],
-              'outer_voxels_per_gpu': s5['outer_vox'], 'pass2_outer_voxels': s5['pass2_outer'],
-              'launch_groups': s5['ngroups'],
-              'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(r5['alg_total'] / s5['inner_vox'], 1),
-                                    'achieved': round(r5['pipe'], 1), 'unit': 'GB/s',
-                                    'frac': round(r5['pipe'] / HBM_PEAK_GBS, 4)},
-              'flood_ms_1stream': round(fl5, 3),
-              'flood_frac': round(12 * s5['outer_vox'] / (fl5 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if fl5 > 0 else None,
-              'stage_ms_1stream': {k: round(v, 3) for k, v in s5['stage_1'].items() if v >= 0.05}}
 
     # ---- end to end: n5 gzip in -> WatershedWorkflow (GPU jobs) + relabel -> n5 out --------
     e2e = None
