@@ -773,7 +773,7 @@ def main():
     devices = sorted(set(int(x) for x in (sharded_gather_devices(dev_index, dev) if world > 1 else [dev_index])))
 
     m = run_workload(args.config, args.scaling, rank, world, dev, args.steps, args.warmup, args.streams,
-                     host_pass=not args.no_host, keep_block=ref_block[0] if ref_block else None)
+                     host_pass=False, keep_block=ref_block[0] if ref_block else None)
     rf = roofline_of(cfg, m)
     value = m['inner_all'] * args.steps / m['dt'] / 1e9
 
@@ -799,6 +799,15 @@ def main():
               'flood_ms_1stream': round(fl5, 3),
               'flood_frac': round(12 * s5['outer_vox'] / (fl5 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if fl5 > 0 else None,
               'stage_ms_1stream': {k: round(v, 3) for k, v in s5['stage_1'].items() if v >= 0.05}}
+
+    # ---- the host-pointer path (PCIe-inclusive rate) of the main config, after the config-5
+    # leg: run before it, its pinned staging and host pools left that leg's host-bound two-pass
+    # schedule 179 ms per step instead of 157 (profiles/r05/config5/leg_after_host.json)
+    host = None
+    if not args.no_host:
+        progress('host path leg')
+        mh = run_workload(args.config, args.scaling, rank, world, dev, 1, 1, 1, host_pass=True)
+        host = mh['host']
 
     # ---- strong scaling of config 4: the 1024^3 volume in z-slabs over the ranks -------------
     strong = None
@@ -887,7 +896,7 @@ def main():
                                   'frac': round(rf['pipe'] / HBM_PEAK_GBS, 4)},
             'strong_config4': strong,
             'config5': c5,
-            'host_resident': m['host'],
+            'host_resident': host,
             'end_to_end': e2e,
             'thresholded_components': tcc,
             'vi_vs_oracle': vi,
