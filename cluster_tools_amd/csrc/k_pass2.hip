@@ -121,6 +121,19 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
     }
 }
 
+// the 3-D relabel key of voxel i computed where it is used (k_p2_insert / k_p2_label with
+// fused = 1; 3-D keys carry no slice position): the k_p2_values rule without the per-voxel key
+// array in HBM (its write and two reads)
+__device__ __forceinline__ uint64_t p2_value3(const BlockDesc& B, int64_t i, const uint32_t* PF,
+                                              const uint64_t* sbits) {
+    const uint64_t u = gbl(B.init)[i];
+    if (u != 0) return (uint32_t)u != 0 ? (uint64_t)(uint32_t)u : kEmptyKey;
+    if (B.mask && !gbl(B.mask)[i]) return kEmptyKey;
+    const uint32_t gl = bit_of(sbits, B, i) ? cc_label(PF, PF[i]) : 0u;
+    const uint32_t v = gl ? gl + (uint32_t)B.id_offset : 0u;  // wraps to 0: background
+    return v ? (uint64_t)v : kEmptyKey;
+}
+
 // insert the keys of the voxels none of whose backward neighbours along the scan axes (3-D:
 // z - 1, y - 1, x - 1; 2-D: y - 1, x - 1 in the slice) holds the same key: a voxel with such a
 // neighbour has a smaller scan key with its value, so it cannot be the first appearance, and
@@ -129,21 +142,24 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
 // table keeps the smallest scan key per value.
 __global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__ D, BlockStat* S,
                                                    const uint64_t* __restrict__ vkey, uint64_t* __restrict__ hkey,
-                                                   uint32_t* __restrict__ hpos) {
+                                                   uint32_t* __restrict__ hpos, const uint32_t* __restrict__ PFg,
+                                                   const uint64_t* __restrict__ sbits, int fused) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
     uint64_t* hk = hkey + B.hbase;
     uint32_t* hp = hpos + B.hbase;
     const int64_t cap = B.hcap;
+    const uint32_t* PF = PFg + B.base;
+    auto value = [&](int64_t j) { return fused ? p2_value3(B, j, PF, sbits) : vkey[B.base + j]; };
     BLOCK_LOOP(i, B) {
-        const uint64_t k = vkey[B.base + i];
+        const uint64_t k = value(i);
         if (k == kEmptyKey) continue;
         int z, y, x;
         inner_to_zyx(i, YX, B.X, z, y, x);
-        if (B.nd_ws == 3 && z > 0 && vkey[B.base + i - YX] == k) continue;
-        if (y > 0 && vkey[B.base + i - B.X] == k) continue;
-        if (x > 0 && vkey[B.base + i - 1] == k) continue;
+        if (B.nd_ws == 3 && z > 0 && value(i - YX) == k) continue;
+        if (y > 0 && value(i - B.X) == k) continue;
+        if (x > 0 && value(i - 1) == k) continue;
         const uint32_t f = scan_key(B, z, y, x);
         int64_t s = (int64_t)(mix64(k) & (uint64_t)(cap - 1));
         bool done = false;
@@ -181,15 +197,18 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
                                                   const float* __restrict__ h, uint32_t* __restrict__ lab,
                                                   uint64_t* __restrict__ key /* in: vkey */,
                                                   uint8_t* __restrict__ fixedv, uint32_t* __restrict__ oldv,
-                                                  uint32_t* __restrict__ oldt, int packed, int write_keys) {
+                                                  uint32_t* __restrict__ oldt, int packed, int write_keys,
+                                                  const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ sbits,
+                                                  int fused) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
     const int lane = threadIdx.x & 63;
+    const uint32_t* PF = PFg + B.base;
     BLOCK_LOOP(i, B) {
         // a wave holds 64 consecutive voxels (only trailing lanes can be past the block's end):
         // keys come in runs, and the first lane of each run looks its key up for the run
-        const uint64_t k = key[B.base + i];
+        const uint64_t k = fused ? p2_value3(B, i, PF, sbits) : key[B.base + i];
         const uint64_t kp = shfl_u64(k, (lane + 63) & 63);
         const bool start = lane == 0 || kp != k;
         const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
