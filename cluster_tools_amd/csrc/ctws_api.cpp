@@ -1281,12 +1281,14 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     const uint32_t* cc = cc_seeds ? w.PF : nullptr;
     if (pl.pass2) {
         k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
-        k_p2_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
-                                              (uint32_t*)w.Bf, (uint32_t*)w.sm, packed ? 1 : 0, descent ? 0 : 1, w.PF,
-                                              w.fseed, pl.nd_ws == 3 ? 1 : 0);
         excl = (uint8_t*)w.fin;  // free after the hmap
         k_p2_excl_zero<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, excl);
-        k_p2_excl<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, excl);
+        // 3-D: k_p2_label marks the exclusions from the initial values it reads anyway
+        const int fused3 = pl.nd_ws == 3 ? 1 : 0;
+        k_p2_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
+                                              (uint32_t*)w.Bf, (uint32_t*)w.sm, packed ? 1 : 0, descent ? 0 : 1, w.PF,
+                                              w.fseed, fused3, fused3 ? excl : nullptr);
+        if (!fused3) k_p2_excl<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, excl);
     } else if (pl.from_seeds) {
         // labels, keys and seed flags in the packed / wide key form (fs_seeds counted them)
         k_fs_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.hm, w.lab, w.key, w.cls, packed ? 1 : 0);

@@ -125,8 +125,9 @@ __global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__
 // fused = 1; 3-D keys carry no slice position): the k_p2_values rule without the per-voxel key
 // array in HBM (its write and two reads)
 __device__ __forceinline__ uint64_t p2_value3(const BlockDesc& B, int64_t i, const uint32_t* PF,
-                                              const uint64_t* sbits) {
+                                              const uint64_t* sbits, uint64_t* init_out = nullptr) {
     const uint64_t u = gbl(B.init)[i];
+    if (init_out) *init_out = u;
     if (u != 0) return (uint32_t)u != 0 ? (uint64_t)(uint32_t)u : kEmptyKey;
     if (B.mask && !gbl(B.mask)[i]) return kEmptyKey;
     const uint32_t gl = bit_of(sbits, B, i) ? cc_label(PF, PF[i]) : 0u;
@@ -199,16 +200,21 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
                                                   uint8_t* __restrict__ fixedv, uint32_t* __restrict__ oldv,
                                                   uint32_t* __restrict__ oldt, int packed, int write_keys,
                                                   const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ sbits,
-                                                  int fused) {
+                                                  int fused, uint8_t* __restrict__ excl) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
     const int lane = threadIdx.x & 63;
     const uint32_t* PF = PFg + B.base;
+    const uint32_t nl = S[blockIdx.y].n_seeds;
     BLOCK_LOOP(i, B) {
         // a wave holds 64 consecutive voxels (only trailing lanes can be past the block's end):
         // keys come in runs, and the first lane of each run looks its key up for the run
-        const uint64_t k = fused ? p2_value3(B, i, PF, sbits) : key[B.base + i];
+        uint64_t u = 0;
+        const uint64_t k = fused ? p2_value3(B, i, PF, sbits, &u) : key[B.base + i];
+        // fused (3-D) with excl: k_p2_excl's marks from the initial value read here (zeroed
+        // beforehand by k_p2_excl_zero)
+        if (excl && u != 0 && u <= nl && !excl[B.base + u]) excl[B.base + u] = 1;
         const uint64_t kp = shfl_u64(k, (lane + 63) & 63);
         const bool start = lane == 0 || kp != k;
         const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
