@@ -1240,16 +1240,14 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     k_root_label<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.Wp);
     if (pl.pass2) {
         // _apply_watershed_with_seeds: shifted seeds + initial seeds, relabelConsecutive
-        k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.sb);
+        // the slices' seed bases of the seed CC into w.soff (free until k_slice_offsets): the
+        // relabel keys of 2-D blocks need them after w.sb is rewritten for the new ids
+        k_slice_seed_base<<<gsb, 256, 0, h->stream>>>(w.desc, w.stat, w.W, w.Wp, w.soff);
         HIPCHK(hipMemsetAsync(w.hkey, 0xFF, sizeof(uint64_t) * (size_t)TH, h->stream));
         HIPCHK(hipMemsetAsync(w.hpos, 0xFF, sizeof(uint32_t) * (size_t)TH, h->stream));
-        // 3-D: the relabel key computed where it is read (p2_value3), no key array in HBM; 2-D
-        // keys hold the slice and the seed base of this point (sb is rewritten below)
-        const int p2_fused = pl.nd_ws == 3 ? 1 : 0;
-        if (!p2_fused)
-            k_p2_values<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.PF, w.fseed, w.sb,
-                                                   (const uint32_t*)h->p2_hint_dev.p, w.key);
-        k_p2_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.hkey, w.hpos, w.PF, w.fseed, p2_fused);
+        // the relabel key of a voxel is computed where it is read (p2_value), no key array in HBM
+        k_p2_insert<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.PF, w.fseed, w.soff,
+                                               (const uint32_t*)h->p2_hint_dev.p);
         HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
         const dim3 hg((unsigned)std::min<int64_t>((maxH + 255) / 256, 4096), nb);
         k_p2_roots<<<hg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W);
@@ -1287,7 +1285,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const int fused3 = pl.nd_ws == 3 ? 1 : 0;
         k_p2_label<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.hpos, w.W, w.Wp, w.hm, w.lab, w.key, w.cls,
                                               (uint32_t*)w.Bf, (uint32_t*)w.sm, packed ? 1 : 0, descent ? 0 : 1, w.PF,
-                                              w.fseed, fused3, fused3 ? excl : nullptr);
+                                              w.fseed, w.soff, (const uint32_t*)h->p2_hint_dev.p,
+                                              fused3 ? excl : nullptr);
         if (!fused3) k_p2_excl<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, excl);
     } else if (pl.from_seeds) {
         // labels, keys and seed flags in the packed / wide key form (fs_seeds counted them)

@@ -231,14 +231,12 @@ __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t
 
 // k_pass2.hip (two-pass watershed, pass 2)
 __global__ void k_p2_zero_dt(const BlockDesc*, const BlockStat*, float*);
-__global__ void k_p2_values(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
-                            const uint32_t*, uint64_t*);
-__global__ void k_p2_insert(const BlockDesc*, BlockStat*, const uint64_t*, uint64_t*, uint32_t*, const uint32_t*,
-                            const uint64_t*, int);
+__global__ void k_p2_insert(const BlockDesc*, BlockStat*, uint64_t*, uint32_t*, const uint32_t*, const uint64_t*,
+                            const uint32_t*, const uint32_t*);
 __global__ void k_p2_roots(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, uint64_t*);
 __global__ void k_p2_label(const BlockDesc*, const BlockStat*, const uint64_t*, const uint32_t*, const uint64_t*,
                            const uint32_t*, const float*, uint32_t*, uint64_t*, uint8_t*, uint32_t*, uint32_t*, int, int,
-                           const uint32_t*, const uint64_t*, int, uint8_t*);
+                           const uint32_t*, const uint64_t*, const uint32_t*, const uint32_t*, uint8_t*);
 __global__ void k_p2_excl_zero(const BlockDesc*, const BlockStat*, uint8_t*);
 __global__ void k_p2_excl(const BlockDesc*, const BlockStat*, const uint32_t*, uint8_t*);
 __global__ void k_p2_check(const BlockDesc*, BlockStat*, const uint64_t*, const uint32_t*);

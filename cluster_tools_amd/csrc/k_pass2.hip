@@ -85,54 +85,35 @@ __global__ void __launch_bounds__(256) k_p2_zero_dt(const BlockDesc* __restrict_
     }
 }
 
-// per-voxel relabel key (kEmptyKey: unlabelled); written into `vkey`.  `hint` (2-D, blocks with
-// B.p2hint >= 0): the slice offsets of the previous run, new seeds keyed by their uint32 value
-__global__ void __launch_bounds__(256) k_p2_values(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                   const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ sbits,
-                                                   const uint32_t* __restrict__ sb,
-                                                   const uint32_t* __restrict__ hint, uint64_t* __restrict__ vkey) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
-    const int64_t YX = (int64_t)B.Y * B.X;
-    const uint32_t* PF = PFg + B.base;
-    BLOCK_LOOP(i, B) {
-        // the slice (2-D ws only: 3-D keys carry no position)
-        const int z = B.nd_ws == 3 ? 0 : (int)((uint32_t)i / (uint32_t)YX);
-        const uint64_t u = gbl(B.init)[i];
-        uint64_t k = kEmptyKey;
-        if (u != 0) {
-            // (uint32)u == 0: the setitem truncation makes the voxel background
-            if ((uint32_t)u != 0)
-                k = (B.nd_ws == 3) ? (uint64_t)(uint32_t)u : (((uint64_t)z << 33) | kInitTag | (uint32_t)u);
-        } else if (!B.mask || gbl(B.mask)[i]) {
-            const uint32_t gl = bit_of(sbits, B, i) ? cc_label(PF, PF[i]) : 0u;  // seed label (0: background)
-            if (gl) {
-                if (B.nd_ws == 3) {
-                    const uint32_t v = gl + (uint32_t)B.id_offset;  // wraps to 0: background
-                    if (v) k = v;
-                } else if (B.p2hint >= 0) {
-                    // seeds[seeds != 0] += offset in uint32: a value that wraps to 0 is background
-                    const uint32_t v = (gl - sb[B.sbase + z]) + (uint32_t)B.id_offset + hint[B.p2hint + z];
-                    if (v) k = ((uint64_t)z << 33) | kInitTag | v;
-                } else k = ((uint64_t)z << 33) | (uint64_t)(gl - sb[B.sbase + z]);
-            }
-        }
-        vkey[B.base + i] = k;
-    }
-}
-
-// the 3-D relabel key of voxel i computed where it is used (k_p2_insert / k_p2_label with
-// fused = 1; 3-D keys carry no slice position): the k_p2_values rule without the per-voxel key
-// array in HBM (its write and two reads)
-__device__ __forceinline__ uint64_t p2_value3(const BlockDesc& B, int64_t i, const uint32_t* PF,
-                                              const uint64_t* sbits, uint64_t* init_out = nullptr) {
+// the relabel key of voxel i (kEmptyKey: unlabelled) computed where it is used (k_p2_insert,
+// k_p2_label) instead of a per-voxel key array in HBM (its write and two reads): 3-D keys are the
+// seed values; 2-D keys carry the slice and tag the initial seeds.  sb0 (2-D): the slices' seed
+// bases of the seed CC (k_slice_seed_base before the relabel rewrites w.sb); hint (2-D, blocks
+// with B.p2hint >= 0): the slice offsets of the previous run, new seeds keyed by their uint32 value
+__device__ __forceinline__ uint64_t p2_value(const BlockDesc& B, int64_t i, const uint32_t* PF, const uint64_t* sbits,
+                                             const uint32_t* sb0, const uint32_t* hint, uint64_t* init_out = nullptr) {
     const uint64_t u = gbl(B.init)[i];
     if (init_out) *init_out = u;
-    if (u != 0) return (uint32_t)u != 0 ? (uint64_t)(uint32_t)u : kEmptyKey;
+    // the slice (2-D ws only: 3-D keys carry no position; a block holds fewer than 2^31 voxels)
+    const int z = B.nd_ws == 3 ? 0 : (int)((uint32_t)i / (uint32_t)((int64_t)B.Y * B.X));
+    if (u != 0) {
+        // (uint32)u == 0: the setitem truncation makes the voxel background
+        if ((uint32_t)u == 0) return kEmptyKey;
+        return (B.nd_ws == 3) ? (uint64_t)(uint32_t)u : (((uint64_t)z << 33) | kInitTag | (uint32_t)u);
+    }
     if (B.mask && !gbl(B.mask)[i]) return kEmptyKey;
-    const uint32_t gl = bit_of(sbits, B, i) ? cc_label(PF, PF[i]) : 0u;
-    const uint32_t v = gl ? gl + (uint32_t)B.id_offset : 0u;  // wraps to 0: background
-    return v ? (uint64_t)v : kEmptyKey;
+    const uint32_t gl = bit_of(sbits, B, i) ? cc_label(PF, PF[i]) : 0u;  // seed label (0: background)
+    if (!gl) return kEmptyKey;
+    if (B.nd_ws == 3) {
+        const uint32_t v = gl + (uint32_t)B.id_offset;  // wraps to 0: background
+        return v ? (uint64_t)v : kEmptyKey;
+    }
+    if (B.p2hint >= 0) {
+        // seeds[seeds != 0] += offset in uint32: a value that wraps to 0 is background
+        const uint32_t v = (gl - sb0[B.sbase + z]) + (uint32_t)B.id_offset + hint[B.p2hint + z];
+        return v ? (((uint64_t)z << 33) | kInitTag | v) : kEmptyKey;
+    }
+    return ((uint64_t)z << 33) | (uint64_t)(gl - sb0[B.sbase + z]);
 }
 
 // insert the keys of the voxels none of whose backward neighbours along the scan axes (3-D:
@@ -142,9 +123,9 @@ __device__ __forceinline__ uint64_t p2_value3(const BlockDesc& B, int64_t i, con
 // a smaller key along some axis).  Only a few corner voxels per segment reach the atomics; the
 // table keeps the smallest scan key per value.
 __global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__ D, BlockStat* S,
-                                                   const uint64_t* __restrict__ vkey, uint64_t* __restrict__ hkey,
-                                                   uint32_t* __restrict__ hpos, const uint32_t* __restrict__ PFg,
-                                                   const uint64_t* __restrict__ sbits, int fused) {
+                                                   uint64_t* __restrict__ hkey, uint32_t* __restrict__ hpos,
+                                                   const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ sbits,
+                                                   const uint32_t* __restrict__ sb0, const uint32_t* __restrict__ hint) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -152,7 +133,7 @@ __global__ void __launch_bounds__(256) k_p2_insert(const BlockDesc* __restrict__
     uint32_t* hp = hpos + B.hbase;
     const int64_t cap = B.hcap;
     const uint32_t* PF = PFg + B.base;
-    auto value = [&](int64_t j) { return fused ? p2_value3(B, j, PF, sbits) : vkey[B.base + j]; };
+    auto value = [&](int64_t j) { return p2_value(B, j, PF, sbits, sb0, hint); };
     BLOCK_LOOP(i, B) {
         const uint64_t k = value(i);
         if (k == kEmptyKey) continue;
@@ -196,11 +177,12 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
                                                   const uint64_t* __restrict__ hkey, const uint32_t* __restrict__ hpos,
                                                   const uint64_t* __restrict__ Wg, const uint32_t* __restrict__ Wpg,
                                                   const float* __restrict__ h, uint32_t* __restrict__ lab,
-                                                  uint64_t* __restrict__ key /* in: vkey */,
+                                                  uint64_t* __restrict__ key,
                                                   uint8_t* __restrict__ fixedv, uint32_t* __restrict__ oldv,
                                                   uint32_t* __restrict__ oldt, int packed, int write_keys,
                                                   const uint32_t* __restrict__ PFg, const uint64_t* __restrict__ sbits,
-                                                  int fused, uint8_t* __restrict__ excl) {
+                                                  const uint32_t* __restrict__ sb0, const uint32_t* __restrict__ hint,
+                                                  uint8_t* __restrict__ excl) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -211,9 +193,9 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
         // a wave holds 64 consecutive voxels (only trailing lanes can be past the block's end):
         // keys come in runs, and the first lane of each run looks its key up for the run
         uint64_t u = 0;
-        const uint64_t k = fused ? p2_value3(B, i, PF, sbits, &u) : key[B.base + i];
-        // fused (3-D) with excl: k_p2_excl's marks from the initial value read here (zeroed
-        // beforehand by k_p2_excl_zero)
+        const uint64_t k = p2_value(B, i, PF, sbits, sb0, hint, &u);
+        // excl (3-D): k_p2_excl's marks from the initial value read here (zeroed beforehand by
+        // k_p2_excl_zero)
         if (excl && u != 0 && u <= nl && !excl[B.base + u]) excl[B.base + u] = 1;
         const uint64_t kp = shfl_u64(k, (lane + 63) & 63);
         const bool start = lane == 0 || kp != k;
