@@ -1409,8 +1409,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK) return r;
     }
     // the histogram, the filter and (pass 1) the final labels read the packed keys directly
-    const bool unpack_final = packed && pl.pass2;
-    if (packed && (h->stop_after == CTWS_STOP_FLOOD || (cfg->size_filter <= 0 && unpack_final)))
+    // (pass 2 reads its final labels from the packed keys too: k_slice_max, k_p2_output)
+    if (packed && h->stop_after == CTWS_STOP_FLOOD)
         k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     mark("flood");
     if (h->stop_after == CTWS_STOP_FLOOD) {
@@ -1509,17 +1509,16 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 return r;
             HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
         }
-        if (unpack_final) k_unpack_labels<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.key, w.lab);
     }
     mark("size_filter");
-    const int keys_final = (packed && !unpack_final) ? 1 : 0;  // final labels still in the keys
+    const int keys_final = packed ? 1 : 0;  // final labels still in the keys
 
     // ---- pass 2: per-slice offsets, takeDict, uncropped inner write --------------------------
     const int ssplit = 4;  // workgroups per slice of the per-slice reductions
     if (pl.pass2) {
         if (pl.nd_ws == 2) {
-            k_slice_max<<<dim3((unsigned)maxZ * ssplit, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, 0,
-                                                                                  w.sb, w.slmax, ssplit, 1);
+            k_slice_max<<<dim3((unsigned)maxZ * ssplit, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key,
+                                                                                  keys_final, w.sb, w.slmax, ssplit, 1);
             k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
             k_p2_check<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.soff);
         }
@@ -1527,8 +1526,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_slice_inmask<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.smin);
         mark("finalize");
         mark("crop_cc");
-        k_p2_output<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, (const uint32_t*)w.Bf, (const uint32_t*)w.sm,
-                                               w.soff);
+        k_p2_output<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, (const uint32_t*)w.Bf,
+                                               (const uint32_t*)w.sm, w.soff);
         LAUNCHCHK();
         mark("output");
     } else if (pl.from_seeds) {

@@ -240,8 +240,8 @@ __global__ void k_p2_label(const BlockDesc*, const BlockStat*, const uint64_t*, 
 __global__ void k_p2_excl_zero(const BlockDesc*, const BlockStat*, uint8_t*);
 __global__ void k_p2_excl(const BlockDesc*, const BlockStat*, const uint32_t*, uint8_t*);
 __global__ void k_p2_check(const BlockDesc*, BlockStat*, const uint64_t*, const uint32_t*);
-__global__ void k_p2_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint32_t*, const uint32_t*,
-                            const uint32_t*);
+__global__ void k_p2_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
+                            const uint32_t*, const uint32_t*);
 __global__ void k_slice_inmask(const BlockDesc*, const BlockStat*, uint32_t*);
 
 // k_relabel.hip (RelabelWorkflow: sorted uniques, assignment-table lookup)

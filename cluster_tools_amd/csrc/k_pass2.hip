@@ -292,7 +292,8 @@ __global__ void __launch_bounds__(256) k_p2_check(const BlockDesc* __restrict__ 
 // uint64 output of the inner block: takeDict(new_to_old), outside mask -> 0, no CC relabel,
 // no offset (two_pass_watershed.py:171-173, 203-206, 252)
 __global__ void __launch_bounds__(256) k_p2_output(const BlockDesc* __restrict__ D, BlockStat* S,
-                                                   const uint32_t* __restrict__ lab, const uint32_t* __restrict__ oldv,
+                                                   const uint32_t* __restrict__ lab, const uint64_t* __restrict__ key,
+                                                   int keys_final, const uint32_t* __restrict__ oldv,
                                                    const uint32_t* __restrict__ oldt, const uint32_t* __restrict__ soff) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;  // dt is None: nothing is written (:240-242)
@@ -303,7 +304,9 @@ __global__ void __launch_bounds__(256) k_p2_output(const BlockDesc* __restrict__
         const int rem = (int)(i - z * yx);
         const int y = rem / B.IX, x = rem - (rem / B.IX) * B.IX;
         const int64_t o = ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0);
-        const uint32_t l = lab[B.base + o] & ~kFixedBit;
+        // the final label: from the packed keys (keys_final: no unpack pass over the outer
+        // block for the inner voxels read here) or from lab
+        const uint32_t l = flood_label(lab, key, keys_final, B.base + o);
         uint32_t v = 0;
         if (l && (!B.mask || gbl(B.mask)[o])) {
             v = oldv[B.base + l];
