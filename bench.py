@@ -499,7 +499,7 @@ def launch_check():
 
 
 def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req, host_pass=False,
-                 keep_block=None):
+                 keep_block=None, keep_volume=False):
     """Stage one workload in HBM, run `warmup` + timed `steps` steps, and measure it.
 
     A step = the `_ws_block` (and `_ws_pass2`) of every block of the rank's share, then the RCCL
@@ -509,7 +509,6 @@ def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req,
     from cluster_tools_amd import ctws
     from cluster_tools_amd.synthetic import boundary_map_torch, ellipsoid_mask_torch
     from cluster_tools_amd.watershed import sharded
-    from cluster_tools_amd.watershed.watershed import pass2_levels
     import torch.distributed as dist
     cfg = CONFIGS[cfg_id]
     two_pass = cfg.get('two_pass', False)
@@ -562,15 +561,31 @@ def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req,
             b['initial_seeds'] = torch.empty(tuple(b['input'].shape[-3:]), dtype=torch.int64, device=dev)
             pass2_outer += int(b['input'].numel())
         # pass 2 in the workflow's schedule (watershed.make_batches): dependency levels of the
-        # sequential loop, each level reading ds_out after the levels before it wrote
-        lv = pass2_levels([(b['osl'], b['isl']) for b in p2])
-        groups = [(0, p1)] + [(1, [b for b, l in zip(p2, lv) if l == k]) for k in range(max(lv) + 1 if lv else 0)]
+        # sequential loop over the pass-2 blocks of ALL ranks (the ones that write: non-empty
+        # inner mask), each level reading ds_out after the levels before it wrote -- on this rank
+        # or, through the z halos, on a neighbour.  The z halos are exchanged before level 0 (the
+        # pass-1 labels) and after every level that wrote rows another rank's halo reads
+        # (sharded.pass2_rank_schedule)
+        writers = set(sharded.all_gather_ints([b['block_id'] for b in p2], device=dev)) if world > 1 else \
+            set(b['block_id'] for b in p2)
+        geos = [volume_geometry(cfg, r, world, scaling) for r in range(world)] if world > 1 else [geo]
+        slabs = [(g['z0'], g['z0'] + g['gshape'][0] - g['lo'] - g['hi']) for g in geos]
+
+        def gsl(g, beg, end):
+            return sl([beg[0] + g['g0']] + list(beg[1:]), [end[0] + g['g0']] + list(end[1:]))
+        glist = sorted((b['block_id'], r, gsl(g, b['obeg'], b['oend']), gsl(g, b['beg'], b['end']))
+                       for r, g in enumerate(geos) for b in g['blocks'] if b['block_id'] in writers)
+        lv, exch = sharded.pass2_rank_schedule([x[1:] for x in glist], slabs, cfg['halo'][0])
+        level = {x[0]: l for x, l in zip(glist, lv)}
+        groups = [(0, p1, False)] + [(1, [b for b in p2 if level[b['block_id']] == k], exch[k])
+                                     for k in range(len(exch))]
     else:
-        groups = [(0, list(blocks.values()))]
-    groups = [(pid, g) for pid, g in groups if g]
+        groups = [(0, list(blocks.values()), False)]
+    # (empty pass-2 levels stay: every rank exchanges at the same levels)
+    groups = [(pid, g, x) for pid, g, x in groups if g or x]
     torch.cuda.synchronize()
 
-    nstreams = max(1, min(nstreams_req, max(len(g) for _, g in groups)))
+    nstreams = max(1, min(nstreams_req, max(len(g) for _, g, _ in groups)))
     handles = [ctws.Handle(dev.index) for _ in range(nstreams)]
     pool = ThreadPoolExecutor(nstreams) if nstreams > 1 else None
     stage_ms = {}
@@ -580,15 +595,15 @@ def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req,
         ns = nstreams if ns is None else ns
         into = stage_ms if into is None else into
         res = []
-        exchanged = False
-        for pid, gblocks in groups:
+        for pid, gblocks, exch in groups:
             if pid == 1:
-                if not exchanged:
-                    # the neighbour slabs' pass-1 labels in the z halos (point-to-point)
+                if exch:
+                    # the neighbour slabs' labels in the z halos (point-to-point)
                     sharded.exchange_z_halos(out_vol, geo['lo'], geo['hi'])
-                    exchanged = True
                 for b in gblocks:  # initial_seeds = ds_out[input_bb] (two_pass_watershed.py:228)
                     b['initial_seeds'].copy_(out_vol[b['osl']])
+            if not gblocks:
+                continue
             nsg = max(1, min(ns, len(gblocks)))
             # contiguous shares of the group's blocks, one per handle (stream)
             parts = [gblocks[len(gblocks) * i // nsg:len(gblocks) * (i + 1) // nsg] for i in range(nsg)]
@@ -668,11 +683,19 @@ def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req,
                 'path': 'ctws_ws_blocks: host numpy input -> pinned staging -> HBM -> uint32 local labels -> '
                         'pinned -> widened with the block id offset into the host numpy uint64 output, one handle',
                 'h2d_bytes': h2d, 'd2h_bytes': int(inner_vox * 4), 'host_output_bytes': int(inner_vox * 8),
-                'phases_ms': phases, 'pcie': pcie_rates(dev), 'matches_device_path': bool(same)}
+                'phases_ms': phases, 'pcie': pcie_rates(dev), 'matches_device_path': bool(same),
+                'method': 'its own leg after the config-5 leg (round 5 on): the best of %d calls of '
+                          'ctws_ws_blocks over the whole workload on one handle (one stream), after one '
+                          'warm-up call; not comparable with the round-4 field, which came from the '
+                          'headline run' % len(ths), 'calls': len(ths), 'streams': 1}
         del hb
     kept = None
     if keep_block is not None and keep_block in blocks:
         kept = blocks[keep_block]['output'].cpu().numpy().view(np.uint64)
+    kept_volume = None
+    if keep_volume and two_pass:
+        # the rank's own slab rows of the labels (tests/test_bench_two_pass_ranks.py)
+        kept_volume = out_vol[geo['lo']:geo['gshape'][0] - geo['hi']].cpu().numpy().view(np.uint64)
     for hh in handles:
         hh.close()
     if pool:
@@ -680,7 +703,8 @@ def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req,
     out = dict(cfg_id=cfg_id, geo=geo, full=full, dt=dt, ms_ranks=ms_ranks, steps=steps,
                inner_vox=inner_vox, outer_vox=outer_vox, pass2_outer=pass2_outer, inner_all=inner_all,
                nblocks=len(blocks), npass=2 if two_pass else 1, ngroups=len(groups), nstreams=nstreams,
-               stage_ms=stage_ms, stage_1=stage_1, n_ids=offsets.get('n_ids'), host=host, kept=kept)
+               stage_ms=stage_ms, stage_1=stage_1, n_ids=offsets.get('n_ids'), host=host, kept=kept,
+               kept_volume=kept_volume, n_exchanges=sum(1 for pid, _, x in groups if pid == 1 and x))
     del blocks, groups, out_vol, mvol
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -792,7 +816,7 @@ def main():
               'steps': s5['steps'], 'n_gpus': world, 'scaling': 'weak', 'workload': CONFIGS[5]['workload'],
               'blocks_per_gpu': s5['nblocks'], 'inner_voxels_per_gpu': s5['inner_vox'],
               'outer_voxels_per_gpu': s5['outer_vox'], 'pass2_outer_voxels': s5['pass2_outer'],
-              'launch_groups': s5['ngroups'],
+              'launch_groups': s5['ngroups'], 'z_halo_exchanges': s5['n_exchanges'],
               'pipeline_roofline': {'alg_bytes_per_inner_voxel': round(r5['alg_total'] / s5['inner_vox'], 1),
                                     'achieved': round(r5['pipe'], 1), 'unit': 'GB/s',
                                     'frac': round(r5['pipe'] / HBM_PEAK_GBS, 4)},

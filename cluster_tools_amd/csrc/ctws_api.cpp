@@ -131,6 +131,10 @@ struct ctws_handle {
     int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
     int no_descent = 0;  // CTWS_NO_DESCENT=1: flood from the seeds alone (test hook)
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
+    // CTWS_FORCE_WIDE=1: every flood on the wide keys (k_flood, 32-bit d; tests).  wide_rerun:
+    // run_batch is re-running blocks whose packed flood reported a saturated d (dsat)
+    int force_wide = 0;
+    int wide_rerun = 0;
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
@@ -413,6 +417,19 @@ int make_plan(ctws_handle* h, const ctws_cfg* cfg, Plan& p) {
 }
 
 int col_width(int L) { return L <= 512 ? 32 : (L <= 1024 ? 16 : 8); }
+
+// dynamic LDS above 64 KiB needs the kernel's opt-in (gfx950: up to 160 KiB per workgroup)
+constexpr size_t kMaxLds = 160 * 1024;
+template <class K>
+void lds_optin(K kern, size_t lds) {
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+// The largest outer block extents the LDS line kernels take: a whole row in LDS (k_prep_edt_x:
+// 16 B per voxel; k_gauss_row: 16 B per voxel + 1 KiB) and whole y / z columns 8 wide (k_edt_col<8>,
+// k_gauss_col<8>: 32 B per position + 1 KiB).  Round 6: the former caps X <= 4096, Y, Z <= 2048
+// were the 64 KiB default, not the hardware.
+constexpr int kMaxRowX = (int)((kMaxLds - 1024) / 16);    // 10176
+constexpr int kMaxColLen = (int)((kMaxLds - 1024) / 32);  // 5088
 // EDT columns: 16 x positions (64-B row segments) beat 32 — half the LDS per tile, twice the
 // tiles per CU, and the bounded search's per-lane trip counts vary less per wave (r01 sweep:
 // y+z passes 1.60 ms at 32, 1.44 at 16, 1.77 at 8 for config 2)
@@ -522,6 +539,7 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
                 dim3 g((unsigned)((int64_t)other * ((maxX + W - 1) / W)), nb);
                 const size_t lds = (size_t)Lm * W * 4;
                 auto kern = W == 32 ? kGaussColR32[r] : (W == 16 ? kGaussColR16[r] : kGaussColR8[r]);
+                lds_optin(kern, lds);
                 hipLaunchKernelGGL(kern, g, dim3(256), lds, h->stream, w.desc, w.stat, gp, hp, (const double*)dtaps,
                                    in, (const float*)w.dt, (const uint32_t*)w.smin, (const uint32_t*)w.smax, out);
             }
@@ -537,6 +555,9 @@ int run_gauss(ctws_handle* h, const Plan& pl, const double* sig, bool hmap_src, 
             const int W = col_width(Lm);
             dim3 g((unsigned)((int64_t)other * ((maxX + W - 1) / W)), nb);
             const size_t lds = 2 * 128 * 4 + (size_t)Lm * W * 4;
+            if (W == 32) lds_optin(k_gauss_col<32>, lds);
+            else if (W == 16) lds_optin(k_gauss_col<16>, lds);
+            else lds_optin(k_gauss_col<8>, lds);
             if (W == 32)
                 k_gauss_col<32><<<g, 256, lds, h->stream>>>(w.desc, w.stat, gp, hp, dtaps, in, w.dt, w.smin, w.smax,
                                                             out);
@@ -913,8 +934,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         maxIRows = std::max(maxIRows, (int64_t)d.IZ * d.IY);
         // validation against what the kernels assume (run_blocks already failed such blocks
         // individually, block_refusal)
-        if (d.X > 4096 || d.Y > 2048 || d.Z > 2048 || d.N >= (1ll << 31)) {
-            h->err = "outer block too large for the kernels (X <= 4096, Y, Z <= 2048, N < 2^31)";
+        if (d.X > kMaxRowX || d.Y > kMaxColLen || d.Z > kMaxColLen || d.N >= (1ll << 31)) {
+            h->err = "outer block too large for the kernels (X <= 10176, Y, Z <= 5088, N < 2^31)";
             return CTWS_EUNSUPPORTED;
         }
         if (d.iz0 < 0 || d.iy0 < 0 || d.ix0 < 0 || d.iz0 + d.IZ > d.Z || d.iy0 + d.IY > d.Y || d.ix0 + d.IX > d.X ||
@@ -1078,8 +1099,10 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             launch_co(std::integral_constant<int, 8>());
         else if (typed && maxX <= 1024)
             launch_co(std::integral_constant<int, 16>());
-        else
+        else {
+            lds_optin(k_prep_edt_x, 4 * (size_t)maxX * 4);
             k_prep_edt_x<<<gx, 256, 4 * (size_t)maxX * 4, h->stream>>>(w.desc, w.stat, pp, fin_out, (uint32_t*)w.A);
+        }
         LAUNCHCHK();
         if (pl.from_seeds) k_fs_active<<<(nb + 255) / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb);
         else k_set_active<<<(nb + 255) / 256, 256, 0, h->stream>>>(w.desc, w.stat, nb);
@@ -1267,6 +1290,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             if (ns >= (1u << 20) - 1u) packed = false;
             max_seeds = std::max(max_seeds, ns);
         }
+        if (h->force_wide || h->wide_rerun) packed = false;
         if (!packed) {
             set_tiles(false);
             HIPCHK(hipMemcpyAsync(w.desc, desc.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, h->stream));
@@ -1408,6 +1432,26 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         mark("flood_descent");
         if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, false, &rounds1, &fk1)) != CTWS_OK) return r;
     }
+    // test hooks that stop after the flood read the workspace: a batch with a saturated packed
+    // key (note_dsat) is run again whole on the wide keys, so they see the unbounded fixpoint too
+    bool rerun_done = false;
+    auto stop_dsat = [&]() -> int {
+        if (!packed) return CTWS_OK;
+        std::vector<BlockStat> sd(nb);
+        HIPCHK(hipMemcpyAsync(sd.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        bool any = false;
+        for (auto& x : sd) any |= x.active && x.dsat;
+        if (!any) return CTWS_OK;
+        ++h->wide_rerun;
+        const int rr = run_batch(h, cfg, pl, blocks, io, nb);
+        --h->wide_rerun;
+        rerun_done = true;
+        return rr;
+    };
+    if (h->stop_after == CTWS_STOP_FLOOD) {
+        if ((r = stop_dsat()) != CTWS_OK || rerun_done) return r;
+    }
     // the histogram, the filter and (pass 1) the final labels read the packed keys directly
     // (pass 2 reads its final labels from the packed keys too: k_slice_max, k_p2_output)
     if (packed && h->stop_after == CTWS_STOP_FLOOD)
@@ -1475,7 +1519,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 2);
                 k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
                 k_auto_seed_set<<<ag, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.surv, w.W, w.Wp, w.sb, w.key,
-                                                           w.cls, w.fopen, w.front0);
+                                                           w.cls, w.fopen, w.front0, nullptr);
                 LAUNCHCHK();
             }
             if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2)) !=
@@ -1505,9 +1549,32 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_size_filter<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, fp, counts, excl, w.hm, w.lab, w.key, w.cls,
                                                      w.surv, packed ? 1 : 0);
             LAUNCHCHK();
+            HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
+            std::vector<BlockStat> s3(nb);
+            HIPCHK(hipMemcpyAsync(s3.data(), w.stat, sizeof(BlockStat) * nb, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            for (int i = 0; i < nb; ++i) {
+                if (!s3[i].active) continue;
+                const int ns = pl.nd_ws == 2 ? desc[i].Z : 1;
+                bool need = false;
+                for (int z = 0; z < ns; ++z) need |= !surv[desc[i].sbase + z];
+                n_auto_blocks += need;
+            }
+            if (n_auto_blocks) {
+                // vigra's auto-seeding (above) on the wide keys: the strict minima as fixed seeds
+                // with their labels in lab (any width); their tiles were freed, so they are active
+                HIPCHK(hipMemsetAsync(w.W, 0, sizeof(uint64_t) * (size_t)TW, h->stream));
+                const dim3 ag((unsigned)std::min<int64_t>(maxRows, 65535), nb);
+                k_auto_minima<<<ag, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.surv, w.W);
+                k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
+                k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 2);
+                k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
+                k_auto_seed_set<<<ag, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.surv, w.W, w.Wp, w.sb, w.key,
+                                                           w.cls, nullptr, nullptr, w.lab);
+                LAUNCHCHK();
+            }
             if ((r = run_flood(h, pl.nd_ws, packed, nb, max_tiles, TT, w.hm, true, &rounds2, &fk2)) != CTWS_OK)
                 return r;
-            HIPCHK(hipMemcpyAsync(surv.data(), w.surv, sizeof(uint32_t) * TS, hipMemcpyDeviceToHost, h->stream));
         }
     }
     mark("size_filter");
@@ -1552,6 +1619,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
         }
         if (stop_ws) {
+            if ((r = stop_dsat()) != CTWS_OK || rerun_done) return r;
             // test hook: the final uint32 ws of the outer block in `lab`
             k_finalize_ws<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.sb, w.soff, w.key, keys_final, w.lab);
             LAUNCHCHK();
@@ -1642,13 +1710,21 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     add_timing(h, "flood_local_iters", (float)h->flood_iters);
     add_timing(h, "flood_lines_swept", (float)h->flood_lines);
     add_timing(h, "size_filter_kernel_ms", fk2);
+    // blocks whose packed flood wrote a key with d at kDMax (note_dsat): the 12-bit hop distance
+    // may have saturated, so they are flooded again on the wide keys (32-bit d) below, never
+    // returned with a possibly different fixpoint
+    std::vector<int> wide;
+    if (packed)
+        for (int i = 0; i < nb; ++i)
+            if (st[i].active && st[i].dsat) wide.push_back(i);
+    auto in_wide = [&](int i) { return std::find(wide.begin(), wide.end(), i) != wide.end(); };
     // pass 2 (2-D): blocks whose relabel needs the wrapped-id merge (k_p2_check) or whose offsets
     // differ from the hint they ran with run again with their offsets as the hint
     std::vector<int> redo;
     std::vector<std::vector<uint32_t>> redo_hint;
     if (pl.pass2 && pl.nd_ws == 2) {
         for (int i = 0; i < nb; ++i) {
-            if (!st[i].active) continue;
+            if (!st[i].active || in_wide(i)) continue;
             std::vector<uint32_t> so(soffh.begin() + desc[i].sbase, soffh.begin() + desc[i].sbase + desc[i].Z);
             const bool again = desc[i].p2hint < 0 ? (st[i].err & kErrCollision) != 0 : so != h->p2_hints[i];
             if (!again || (st[i].err & ~kErrCollision)) continue;  // (other failures stay failures)
@@ -1671,6 +1747,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         blocks[i].n_ids = (pl.pass2 || pl.from_seeds) ? -1 : (int32_t)((st[i].active ? st[i].n_cc : 0u) + bare);
         if (!st[i].active) continue;
         if (std::find(redo.begin(), redo.end(), i) != redo.end()) continue;  // filled by the re-run below
+        if (in_wide(i)) continue;  // filled by the wide re-run below
         uint32_t err = st[i].err | (regrow_bad ? kErrVerify : 0u);
         if (desc[i].p2hint >= 0 && !soffh.empty() &&
             !std::equal(h->p2_hints[i].begin(), h->p2_hints[i].end(), soffh.begin() + desc[i].sbase))
@@ -1686,9 +1763,6 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 if (!nl && (pl.nd_ws == 3 || inmask[s0])) err |= kErrTakeDict;
             }
         }
-        if (cfg->size_filter > 0 && !packed)
-            for (int z = 0; z < ns; ++z)
-                if (!surv[desc[i].sbase + z]) err |= kErrUnsupported;
         if (err) {
             blocks[i].status = CTWS_BLOCK_FAILED;
             char msg[256];
@@ -1732,6 +1806,32 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         h->last_desc.clear();
         add_timing(h, "p2_merge_reruns", (float)redo.size());
     }
+    if (!wide.empty()) {
+        std::vector<ctws_block> rb;
+        std::vector<BlockIO> rio;
+        std::vector<std::vector<uint32_t>> rh;
+        const bool hints = h->p2_hints.size() == (size_t)nb;
+        for (int i : wide) {
+            rb.push_back(blocks[i]);
+            rio.push_back(io[i]);
+            if (hints) rh.push_back(h->p2_hints[i]);
+        }
+        auto saved = std::move(h->p2_hints);
+        h->p2_hints = std::move(rh);
+        ++h->wide_rerun;
+        const int rr = run_batch(h, cfg, pl, rb.data(), rio.data(), (int)rb.size());
+        --h->wide_rerun;
+        h->p2_hints = std::move(saved);
+        if (rr != CTWS_OK) return rr;
+        for (size_t k = 0; k < wide.size(); ++k) {
+            blocks[wide[k]].status = rb[k].status;
+            blocks[wide[k]].max_label = rb[k].max_label;
+            blocks[wide[k]].n_ids = rb[k].n_ids;
+            if (k < h->last_bare.size()) bare[wide[k]] = h->last_bare[k];
+        }
+        h->last_desc.clear();
+        add_timing(h, "flood_wide_reruns", (float)wide.size());
+    }
     h->last_bare = std::move(bare);
     return CTWS_OK;
 }
@@ -1741,8 +1841,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 // while the other blocks of the call run.
 const char* block_refusal(const Plan& pl, const ctws_block& b) {
     const int64_t Z = b.outer_shape[0], Y = b.outer_shape[1], X = b.outer_shape[2];
-    if (X > 4096 || Y > 2048 || Z > 2048 || Z * Y * X >= (1ll << 31))
-        return "outer block too large for the kernels (X <= 4096, Y, Z <= 2048, fewer than 2^31 voxels)";
+    if (X > kMaxRowX || Y > kMaxColLen || Z > kMaxColLen || Z * Y * X >= (1ll << 31))
+        return "outer block too large for the kernels (X <= 10176, Y, Z <= 5088, fewer than 2^31 voxels)";
     // vigra's convolveLine: "kernel longer than line" (the reference raises at this block)
     auto too_short = [&](const double* sg, bool en) -> bool {
         if (!en) return false;
@@ -2228,6 +2328,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_TRACE")) h->trace = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_DESCENT")) h->no_descent = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_FORCE_WIDE")) h->force_wide = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))

@@ -58,6 +58,8 @@ struct BlockStat {
     uint32_t err;             // kErr* bits: the block cannot be finished (per-block failure)
     uint32_t n_auto;          // auto-seeded regrow: strict hmap minima of the seedless slices
     uint32_t _p[4];
+    uint32_t dsat;            // packed flood: a key's hop distance d reached kDMax (note_dsat)
+    uint32_t _q[3];
 };
 
 // BlockStat::err bits (a failed block does not fail its batch; the caller sees the status)
@@ -393,6 +395,18 @@ constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
 // cycle of voxels keep a stale label, and the GPU converged to such a fixpoint (round 4,
 // config-1 2-D test config: VI 0.029 against the model's 0) -- not adopted.
 constexpr uint32_t kDMax = 4095;
+
+// A packed key whose d field is at kDMax: the hop distance may have saturated, so the packed
+// fixpoint may differ from the unbounded (C, d, label) one (a cycle of equal saturated keys can
+// keep a stale label).  Every kernel that writes a relaxed packed key reports such a write in
+// BlockStat::dsat; run_batch then floods those blocks again with the wide keys (k_flood: d is
+// 32 bits there and never saturates).  Writes with d < kDMax cannot differ from the unbounded
+// flood, so a batch without a report is exact.
+__device__ __forceinline__ bool key_dsat(uint64_t k) { return (k & kDMask) == kDMask && k != kPackInf; }
+__device__ __forceinline__ void note_dsat(const BlockStat* S, int b) {
+    uint32_t* p = const_cast<uint32_t*>(&S[b].dsat);
+    if (!*(volatile uint32_t*)p) atomicOr(p, 1u);
+}
 
 // K(q) = f_q(min over the neighbours): a neighbour key `best` pushed into voxel q of height hb
 __device__ __forceinline__ uint64_t f_packed(uint32_t hb, uint64_t best) {

@@ -224,7 +224,7 @@ __global__ void k_regrow_init(const BlockDesc*, const BlockStat*, uint32_t, cons
                               const float*, uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*);
 __global__ void k_auto_minima(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*);
 __global__ void k_auto_seed_set(const BlockDesc*, BlockStat*, const float*, const uint32_t*, const uint64_t*,
-                                const uint32_t*, const uint32_t*, uint64_t*, uint8_t*, uint64_t*, uint64_t*);
+                                const uint32_t*, const uint32_t*, uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*);
 __global__ void k_slice_offsets(const BlockDesc*, const BlockStat*, const uint32_t*, uint32_t*);
 __global__ void k_finalize_ws(const BlockDesc*, const BlockStat*, const uint32_t*, const uint32_t*, const uint64_t*, int,
                               uint32_t*);

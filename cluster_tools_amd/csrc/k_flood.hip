@@ -45,10 +45,13 @@ __device__ __forceinline__ void take_min(uint64_t nk, uint32_t nl, uint64_t& bk,
     }
 }
 
+// (C, d + 1): d is 32 bits here and never saturates (a hop distance is < N < 2^31), so this
+// kernel computes the unbounded (C, d, label) fixpoint -- the one the packed flood equals when
+// none of its keys reached kDMax, and the one run_batch falls back to when one did (dsat)
 __device__ __forceinline__ uint64_t f_key(uint32_t hb, uint64_t bk) {
     const uint32_t c = (uint32_t)(bk >> 32);
     if (hb > c) return (uint64_t)hb << 32;
-    return (uint32_t)bk >= kDMax ? bk : bk + 1ull;  // (C, min(d + 1, kDMax)), as f_packed
+    return bk + 1ull;
 }
 
 template <int ND>
@@ -460,7 +463,9 @@ __global__ void __launch_bounds__(PTile<ND>::THREADS, 2) k_flood_packed(const Bl
         if (!(sf[c] & 2)) continue;
         const int lx = c % TX, ly = (c / TX) % TY, lz = c / (TX * TY);
         const int gz = z0 + lz, gy = y0 + ly, gx = x0 + lx;
-        key[gb + gz * YX + (int64_t)gy * B.X + gx] = sk[((lz + ZOFF) * HY + (ly + 1)) * HX + (lx + 1)];
+        const uint64_t kw = sk[((lz + ZOFF) * HY + (ly + 1)) * HX + (lx + 1)];
+        key[gb + gz * YX + (int64_t)gy * B.X + gx] = kw;
+        if (key_dsat(kw)) note_dsat(S, blockIdx.y);
         auto fl = [&](int f, int line) { atomicOr(&sfl[f][line >> 5], 1u << (line & 31)); };
         if (ND == 3) {
             if (lz == 0) fl(0, ly * TX + lx);
@@ -1149,6 +1154,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                     const uint64_t k = f_packed(ordf(hv[u]), m);
                     if (k == own[u]) continue;
                     kb[iv[u]] = k;
+                    if (key_dsat(k)) note_dsat(S, bi);
                     atomicOr((unsigned long long*)&schg[wv][jv[u]], 1ull << bv[u]);
                     if (dirf) {
                         // nb[] order: -z, +z, -y, +y, -x, +x (outside the block: INF, its bit is

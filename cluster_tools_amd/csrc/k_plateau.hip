@@ -27,7 +27,8 @@
 
 namespace ctws {
 
-// n more hops inside the plateau: d + n, saturating at kDMax as f_packed does; INF stays INF
+// n more hops inside the plateau: d + n, saturating at kDMax as f_packed does (a saturated key
+// written is reported, note_dsat); INF stays INF
 __device__ __forceinline__ uint64_t key_hops(uint64_t k, uint32_t n) {
     if (k == kPackInf) return k;
     const uint32_t d = (uint32_t)((k & kDMask) >> kLabelBits);
@@ -77,7 +78,11 @@ __global__ void __launch_bounds__(256) k_plat_entry(const BlockDesc* __restrict_
             if (y + 1 < B.Y) m = min(m, kb[i + B.X]);
             if (x > 0) m = min(m, kb[i - 1]);
             if (x + 1 < B.X) m = min(m, kb[i + 1]);
-            if (m != kPackInf) kb[i] = f_packed(ordf(h[B.base + i]), m);
+            if (m != kPackInf) {
+                const uint64_t k = f_packed(ordf(h[B.base + i]), m);
+                kb[i] = k;
+                if (key_dsat(k)) note_dsat(S, blockIdx.y);
+            }
         }
     })
 }
@@ -129,7 +134,10 @@ __global__ void __launch_bounds__(256) k_plat_scan_x(const BlockDesc* __restrict
                 const uint64_t v0 = inp ? kb[i] : kPackInf;
                 uint64_t v = plat_word_scan(v0, pw, carry, lane);
                 if (!inp) v = kPackInf;
-                if (inp && v != v0) kb[i] = v;
+                if (inp && v != v0) {
+                    kb[i] = v;
+                    if (key_dsat(v)) note_dsat(S, blockIdx.y);
+                }
                 carry = shfl_u64(v, 63);  // kPackInf when the run does not reach the word's end
             }
         }
@@ -183,7 +191,10 @@ __global__ void __launch_bounds__(256) k_plat_scan_col(const BlockDesc* __restri
                         continue;
                     }
                     const uint64_t nv = min(kv[u], key_hops(run, 1u));
-                    if (nv != kv[u]) kb[vi[u]] = nv;
+                    if (nv != kv[u]) {
+                        kb[vi[u]] = nv;
+                        if (key_dsat(nv)) note_dsat(S, blockIdx.y);
+                    }
                     run = nv;
                 }
             }

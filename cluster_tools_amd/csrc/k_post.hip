@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(256) k_auto_seed_set(const BlockDesc* __restri
                                                        const uint64_t* __restrict__ W, const uint32_t* __restrict__ Wp,
                                                        const uint32_t* __restrict__ sb, uint64_t* __restrict__ key,
                                                        uint8_t* __restrict__ fixedv, uint64_t* __restrict__ open,
-                                                       uint64_t* __restrict__ chg) {
+                                                       uint64_t* __restrict__ chg, uint32_t* __restrict__ lab) {
     const BlockDesc& B = D[blockIdx.y];
     BlockStat& st = S[blockIdx.y];
     if (!st.active) return;
@@ -338,11 +338,19 @@ __global__ void __launch_bounds__(256) k_auto_seed_set(const BlockDesc* __restri
             } else if (B.pass2 && l > st.n_seeds) {
                 err |= kErrTakeDict;
             }
+            const int64_t gi = B.base + row * B.X + x;
+            if (lab) {
+                // wide keys (k_flood): the label apart, any width; the minimum's tile is active
+                // already (every voxel of the slice / block was freed by k_size_filter)
+                lab[gi] = l | kFixedBit;
+                key[gi] = (uint64_t)ordf(h[gi]) << 32;
+                fixedv[gi] = 1;
+                continue;
+            }
             if (l >= (1u << 20) - 1u) {
                 err |= kErrLabelBits;
                 continue;
             }
-            const int64_t gi = B.base + row * B.X + x;
             key[gi] = ((uint64_t)ordf(h[gi]) << 32) | (uint64_t)l;
             fixedv[gi] = 1;
             const int64_t wi = B.fbase + row * wpr + (x >> 6);

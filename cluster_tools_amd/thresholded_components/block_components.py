@@ -141,18 +141,23 @@ def _read_block(blocking, block_id, ds_in, mask, channel):
     return b
 
 
-def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config, keep=None, started=None):
+def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config, keep=None, started=None,
+                         spill=False):
     """`_cc_block[_with_mask]` for every block of the job -> {block_id: offset}.  keep (a list):
     the blocks' labels are collected there as (block_id, bb, labels or None, count) instead of
-    written (the in-job merge writes the final ids).  started: called once the first read is
-    under way (the merge's process group starts there, its torch import overlapping the read)."""
+    written (the in-job merge writes the final ids): uint32 (a block has < 2^32 voxels, ctws
+    refuses larger ones), or with spill=True written to ds_out as they are and re-read by the
+    merge (merge_in_job.SpilledBlock) when the job's labels would not fit its share of host
+    memory.  started: called once the first read is under way (the merge's process group starts
+    there, its torch import overlapping the read)."""
+    from cluster_tools_amd.thresholded_components.merge_in_job import SpilledBlock
     from cluster_tools_amd import ctws
     sigma = float(config.get('sigma_prefilter', 0) or 0)
     threshold, mode = config['threshold'], config['threshold_mode']
     channel = config.get('channel', None)
     offsets = {}
-    # chunk inflate / deflate on a pool (libdeflate releases the GIL)
-    ds_in.n_threads = ds_out.n_threads = max(4, int(config.get('threads_per_job', 1)))
+    # chunk inflate / deflate on a pool of the job's threads (libdeflate releases the GIL)
+    ds_in.n_threads = ds_out.n_threads = max(1, int(config.get('threads_per_job', 1)))
     with futures.ThreadPoolExecutor(1) as io, contextlib.ExitStack() as stack:
         nxt = io.submit(_read_block, blocking, block_list[0], ds_in, mask, channel) if block_list else None
         if started is not None:
@@ -178,7 +183,13 @@ def run_component_blocks(blocking, block_list, ds_in, ds_out, mask, config, keep
                                                sigma=sigma)
             offsets[block_id] = n + 1 if n else 0
             if keep is not None:
-                keep.append((block_id, b['bb'], labels if n else None, offsets[block_id]))
+                lab = None
+                if n and spill:
+                    ds_out[b['bb']] = labels
+                    lab = SpilledBlock(ds_out, b['bb'])
+                elif n:
+                    lab = labels.astype(np.uint32)
+                keep.append((block_id, b['bb'], lab, offsets[block_id]))
                 continue
             if n:
                 ds_out[b['bb']] = labels
@@ -215,8 +226,23 @@ def block_components(job_id, config_path):
     fu.log_job_success(job_id)
 
 
+def spill_labels(blocking, block_list, n_jobs, config):
+    """Whether this job writes its blocks' labels as it goes and re-reads them in the merge
+    (config 'merge_spill': true / false; default: when the job's uint32 labels plus the largest
+    block's uint64 write buffer exceed its share -- the local jobs of the task on this node -- of
+    half the available host memory)."""
+    force = config.get('merge_spill')
+    if force is not None:
+        return bool(force)
+    import psutil
+    vox = [int(np.prod([s.stop - s.start for s in vu.block_to_bb(blocking.getBlock(b))])) for b in block_list]
+    need = 4 * sum(vox) + 8 * max(vox, default=0)
+    return need > psutil.virtual_memory().available // (2 * max(1, n_jobs))
+
+
 def _run_blocks_merge(job_id, blocking, ds_in, ds_out, mask, config):
     """The job's blocks, then the merge tail over the jobs' process group (merge_in_job.py)."""
+    import torch.distributed as dist
     from cluster_tools_amd.thresholded_components.merge_in_job import merge_in_job
     from cluster_tools_amd.watershed import job_relabel
     from cluster_tools_amd.cluster_tasks import split_blocks
@@ -226,29 +252,38 @@ def _run_blocks_merge(job_id, blocking, ds_in, ds_out, mask, config):
     for j, blocks in enumerate(split_blocks(block_list, m['n_jobs'], consecutive=True)):
         for b in blocks:
             owner[b] = j
-    group = []
+    group, init_err = [], []
 
     def start_group():
-        job_relabel.init_group(job_id, m['n_jobs'], m['rendezvous'], m['backend'], device=_device())
+        try:
+            job_relabel.init_group(job_id, m['n_jobs'], m['rendezvous'], m['backend'], device=_device())
+        except Exception as e:  # recorded: a second rendezvous would only wait out the timeout again
+            init_err.append(e)
+            raise
         group.append(True)
 
     failed = None
     keep = []
+    spill = spill_labels(blocking, config['block_list'], m['n_jobs'], config)
+    if spill:
+        fu.log("labels of this job's blocks written as they are and re-read by the merge (host memory)")
     try:
         try:
             run_component_blocks(blocking, config['block_list'], ds_in, ds_out, mask, config, keep=keep,
-                                 started=start_group)
+                                 started=start_group, spill=spill)
         except Exception as e:  # still take part in the exchange: every job then raises
             import traceback
             traceback.print_exc()
             failed = e
+        if init_err:
+            raise init_err[0]
         if not group:   # (failed before its first read)
             start_group()
         merge_in_job(job_id, [] if failed else keep, blocking, block_list, owner, dict(m, tmp_folder=config['tmp_folder']),
                      ds_out, log=fu.log, device=_device(), failed=failed is not None)
     finally:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+        if dist.is_initialized():
+            dist.destroy_process_group()
     if failed is not None:
         raise failed
 

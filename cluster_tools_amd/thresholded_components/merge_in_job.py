@@ -30,6 +30,26 @@ import numpy as np
 from cluster_tools_amd.thresholded_components.merge_offsets import scan_block_counts
 
 
+class SpilledBlock:
+    """A block's labels written to ds_out as they are (uint64) instead of kept in host memory
+    (block_components.spill_labels); the merge reads its face planes and, for the final write,
+    the whole block back."""
+
+    def __init__(self, ds, bb):
+        self.ds, self.bb = ds, tuple(bb)
+
+    def plane(self, axis, index):
+        bb = list(self.bb)
+        bb[axis] = slice(self.bb[axis].start + index, self.bb[axis].start + index + 1)
+        return np.ascontiguousarray(np.asarray(self.ds[tuple(bb)]).squeeze(axis))
+
+    def extent(self, axis):
+        return self.bb[axis].stop - self.bb[axis].start
+
+    def read(self):
+        return np.asarray(self.ds[self.bb])
+
+
 def lower_plane(labels, axis):
     """The block's first plane along `axis` (the face its lower neighbour pairs with)."""
     return np.ascontiguousarray(np.take(labels, 0, axis=axis))
@@ -110,9 +130,30 @@ def merge_in_job(job_id, results, blocking, block_list, owner, config, ds_out, l
     from cluster_tools_amd import ctws
     from cluster_tools_amd.utils import volume_utils as vu
     from cluster_tools_amd.watershed.job_relabel import _agree
-    to_numpy = to_numpy or (lambda a: a if isinstance(a, np.ndarray) else a.cpu().numpy())
+    to_numpy = to_numpy or (lambda a: a if isinstance(a, np.ndarray) else
+                            a.read() if isinstance(a, SpilledBlock) else a.cpu().numpy())
     comm_dev = device if dist.get_backend() == 'nccl' else None
     tmp = config['tmp_folder']
+    try:
+        return _merge(job_id, results, blocking, block_list, owner, config, ds_out, log, device, failed, to_numpy,
+                      dist, ctws, vu, _agree, comm_dev, tmp)
+    finally:
+        # job 0 removes the run's files whether the merge ended or failed (every job leaves the
+        # merge at the same _agree, so no peer reads them any more)
+        if job_id == 0:
+            _remove_run_files(tmp, dist.get_world_size(), block_list)
+
+
+def _remove_run_files(tmp, world, block_list):
+    paths = [_pairs_file(tmp, j) for j in range(world)] + [_assignments_file(tmp)]
+    paths += [_plane_file(tmp, bid, axis) for bid in block_list for axis in range(3)]
+    for p in paths:
+        if os.path.exists(p):
+            os.remove(p)
+
+
+def _merge(job_id, results, blocking, block_list, owner, config, ds_out, log, device, failed, to_numpy,
+           dist, ctws, vu, _agree, comm_dev, tmp):
     rows = [[-1, 0, int(failed)]] + [[bid, int(cnt), 0] for bid, _, _, cnt in results]
     allr = _gather_counts(rows, comm_dev)
     if allr[:, 2].any():
@@ -217,26 +258,22 @@ def merge_in_job(job_id, results, blocking, block_list, owner, config, ds_out, l
     except Exception as e:  # noqa: BLE001
         err = e
     _agree(err, comm_dev, 'writing its blocks')
-    if job_id == 0:
-        for j in range(dist.get_world_size()):
-            os.remove(_pairs_file(tmp, j))
-        os.remove(_assignments_file(tmp))
-        for bid in block_list:
-            for axis in range(3):
-                p = _plane_file(tmp, bid, axis)
-                if os.path.exists(p):
-                    os.remove(p)
     return n_labels
 
 
 def lower_plane_any(lab, axis):
-    """lower_plane on a numpy array or a torch tensor (the plane only crosses PCIe)."""
+    """lower_plane on a numpy array, a spilled block (one plane read back) or a torch tensor
+    (the plane only crosses PCIe)."""
     if isinstance(lab, np.ndarray):
         return lower_plane(lab, axis)
+    if isinstance(lab, SpilledBlock):
+        return lab.plane(axis, 0)
     return lab.select(axis, 0).contiguous()
 
 
 def upper_plane_any(lab, axis):
     if isinstance(lab, np.ndarray):
         return upper_plane(lab, axis)
+    if isinstance(lab, SpilledBlock):
+        return lab.plane(axis, lab.extent(axis) - 1)
     return lab.select(axis, lab.shape[axis] - 1).contiguous()

@@ -162,3 +162,36 @@ def exchange_z_halos(vol, lo, hi):
     if recv_hi is not None:
         vol[lo + Z:] = recv_hi
     return vol
+
+
+def all_gather_ints(values, device=None):
+    """Every rank's list of ints, concatenated in rank order."""
+    return [int(v) for v in gather_counts(values, device=device)]
+
+
+def pass2_rank_schedule(p2_blocks, slabs, hz):
+    """The two-pass watershed's sequential schedule over z-slab ranks.
+
+    p2_blocks: the pass-2 blocks of the whole job that write something, in the sequential list
+    order (two_pass_watershed.py:296-299), as (owner rank, input_bb, output_bb) with global
+    bounding boxes; slabs: [(z0, z1)] per rank; hz: the z halo.  Returns (levels, exchange):
+    levels[k] = the level of block k (watershed.pass2_levels over the global list, so a block
+    reads after every earlier block it overlaps wrote, on whichever rank that one ran);
+    exchange[l] = whether the z-halo rows must be exchanged before level l: before level 0
+    (the pass-1 labels) and after every level with a block whose output rows lie within hz of
+    its slab's boundary to a neighbouring rank (another rank's halo reads them).  Every rank
+    computes the same schedule, so all of them exchange at the same levels."""
+    from cluster_tools_amd.watershed.watershed import pass2_levels
+    levels = pass2_levels([(ib, ob) for _, ib, ob in p2_blocks])
+    n_levels = max(levels) + 1 if levels else 0
+    exchange = [False] * n_levels
+    if n_levels:
+        exchange[0] = True
+    world = len(slabs)
+    for (r, _, ob), lv in zip(p2_blocks, levels):
+        z0, z1 = slabs[r]
+        b0, b1 = ob[0].start, ob[0].stop
+        near = (r > 0 and b0 < z0 + hz) or (r + 1 < world and b1 > z1 - hz)
+        if near and lv + 1 < n_levels:
+            exchange[lv + 1] = True
+    return levels, exchange

@@ -254,8 +254,8 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
     # keep (in-job relabel): small batches, so that the GPU runs a batch while the next is read
     batch_blocks = batch_blocks or int(config.get('gpu_batch_blocks') or (4 if keep is not None else 16))
     batches = make_batches(blocking, block_list, config, pass_id, batch_blocks)
-    n_io = max(1, int(config.get('threads_per_job', 1)))
-    ds_in.n_threads = ds_out.n_threads = max(n_io, 4)
+    # chunk inflate / deflate on a pool of the job's threads_per_job (not more)
+    ds_in.n_threads = ds_out.n_threads = max(1, int(config.get('threads_per_job', 1)))
     if hasattr(ds_in, 'cache_bytes'):
         # inflate each input chunk once for the job's blocks with halos (n5 / zarr reader)
         ds_in.cache_bytes = int(float(config.get('read_cache_gb', 2.0)) * (1 << 30))
@@ -303,6 +303,7 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
                 nxt = io.submit(read_batch, batches[bi + 1]) if bi + 1 < len(batches) else None
             for b in blocks:
                 fu.log("start processing block %i" % b['block_id'])
+            _test_fail_once(blocks)
             todo = [b for b in blocks if not b.get('skip')]
             if not todo:
                 res = []
@@ -326,6 +327,20 @@ def run_blocks(blocking, block_list, ds_in, ds_out, mask, config, pass_id=0, bat
                 nxt = io.submit(read_batch, batches[bi + 1]) if bi + 1 < len(batches) else None
         if pending_write is not None:
             pending_write.result()
+
+
+def _test_fail_once(blocks):
+    """Test hook of the retry test (tests/test_workflow_gpu.py, as the reference's
+    test/retry/failing_task.py): with CTWS_TEST_FAIL_ONCE=<folder>, the first attempt at a block
+    with id % 4 == 1 raises (a marker file in the folder records it), the retry succeeds."""
+    folder = os.environ.get('CTWS_TEST_FAIL_ONCE')
+    if not folder:
+        return
+    for b in blocks:
+        marker = os.path.join(folder, 'failed_block_%i' % b['block_id'])
+        if b['block_id'] % 4 == 1 and not os.path.exists(marker):
+            open(marker, 'w').close()
+            raise RuntimeError("injected failure of block %i (CTWS_TEST_FAIL_ONCE)" % b['block_id'])
 
 
 def _keep_on_device(blocking, block_list, config):
@@ -391,10 +406,14 @@ def _run_blocks_relabel(job_id, blocking, ds_in, ds_out, mask, config, rel):
     # the group as soon as the first read is under way: all jobs start together, so the
     # rendezvous is immediate; a job that dies later breaks its peers' pending collective (gloo /
     # RCCL report the lost peer) instead of leaving them waiting out the timeout
-    group = []
+    group, init_err = [], []
 
     def start_group():
-        job_relabel.init_group(job_id, rel['n_jobs'], rel['rendezvous'], rel['backend'], device=_device())
+        try:
+            job_relabel.init_group(job_id, rel['n_jobs'], rel['rendezvous'], rel['backend'], device=_device())
+        except Exception as e:  # recorded: a second rendezvous would only wait out the timeout again
+            init_err.append(e)
+            raise
         group.append(True)
 
     keep, failed = [], None
@@ -406,6 +425,8 @@ def _run_blocks_relabel(job_id, blocking, ds_in, ds_out, mask, config, rel):
             import traceback
             traceback.print_exc()
             failed = e
+        if init_err:
+            raise init_err[0]
         if not group:   # (run_blocks failed before its first read)
             start_group()
         if failed is None:
@@ -424,8 +445,8 @@ def _run_blocks_relabel(job_id, blocking, ds_in, ds_out, mask, config, rel):
             job_relabel.relabel_in_job(job_id, [], ds_out, rel['tmp_folder'], rel['assignment_path'],
                                        rel['assignment_key'], None, failed=True, log=fu.log, device=_device())
     finally:
-        if group:
-            import torch.distributed as dist
+        import torch.distributed as dist
+        if dist.is_initialized():
             dist.destroy_process_group()
     if failed is not None:
         raise failed

@@ -442,7 +442,7 @@ struct PQCompare {
 // ---------------------------------------------------------------------------------------
 int g_flood_model = 0;
 // tie orders for the tie-order experiment (scripts/tie_order_experiment.py): the GPU's
-// order is 1 (kDMax = 4095 in cluster_tools_amd/csrc/ctws_dev.h).  Orders 2 and 6 have no
+// order is 1 (unbounded d; the packed key's 12-bit field reports kDMax, cluster_tools_amd/csrc/ctws_dev.h).  Orders 2 and 6 have no
 // unique fixpoint (equal keys along plateau paths), so no parallel relaxation can promise them.  2: (C, label), no hop distance; 3: (C, d, -label); 4: (C, d, push count) = FIFO
 // inside an equal-(C, d) front; 5: (C, push count) = FIFO on a plateau; 6: (C, min(d, 1), label);
 // 7: (C, label, d) -- the label before the hop distance; the fixpoint is unique, but a parallel
@@ -504,8 +504,10 @@ uint32_t watersheds_model(const float* h, const Dims& d, uint32_t* labels) {
                 labels[j] = e.label;
                 const uint32_t hb = ordf(h[j]);
                 const uint32_t cc = (uint32_t)(e.key >> 32);
-                // d saturates at 4095 (12-bit field of the GPU's packed key)
-                const uint64_t dcap = g_tie_order == 6 ? 1ull : 4095ull;
+                // d is unbounded (32 bits) in the GPU's order: the packed 12-bit d reports a
+                // saturation and the GPU floods such a block again on wide keys (round 6);
+                // order 6 caps it at 1
+                const uint64_t dcap = g_tie_order == 6 ? 1ull : 0xFFFFFFFFull;
                 const uint64_t k = hb > cc ? ((uint64_t)hb << 32)
                                            : (!use_d || (e.key & 0xFFFFFFFFull) >= dcap ? e.key : e.key + 1ull);
                 pq.push({k, e.label, j, seq++});

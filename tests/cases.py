@@ -47,6 +47,11 @@ def make_cases():
     # 4096-voxel rows with a larger x radius than y: the x pass is the separate row kernel, whose
     # 1 KiB + 16 B per voxel of LDS is above 64 KiB (the opt-in launch)
     xw4096_3d = _x(seed=18, shape=(4, 12, 4096))
+    # outer blocks beyond the round-5 caps (X <= 4096, Y, Z <= 2048): rows and
+    # columns held whole in LDS above the 64 KiB default (the kernels' opt-in, up to 160 KiB)
+    xw4200 = _x(seed=19, shape=(1, 64, 4200))
+    xt2200 = _x(seed=20, shape=(1, 2200, 64))
+    xd2200 = _x(seed=21, shape=(2200, 8, 32))
     # a mask of random blobs: the masked region is a non-convex plateau with holes, so the
     # plateau fill's run scans (k_plateau.hip) miss paths that the frontier has to correct
     rs = np.random.RandomState(17)
@@ -60,6 +65,9 @@ def make_cases():
         '3d_wide1100': (dict(D3), dict(input=xw1100)),
         '3d_wide4096_aniso': (dict(D3, sigma_seeds=(1., 1., 3.), sigma_weights=(1., 1., 3.)), dict(input=xw4096_3d)),
         '2d_sigma22': (dict(sigma_seeds=22.0), dict(input=x)),
+        '2d_wide4200': ({}, dict(input=xw4200)),
+        '2d_tall2200': (dict(sigma_weights=5.0), dict(input=xt2200)),
+        '3d_deep2200': (dict(D3), dict(input=xd2200)),
         '3d_sparse_fg': (dict(D3), dict(input=xs)),
         '2d_sparse_fg': ({}, dict(input=xs)),
         '3d_sizefilter_all': (dict(D3, size_filter=10 ** 9), dict(input=x)),

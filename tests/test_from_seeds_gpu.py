@@ -56,11 +56,12 @@ def _cases():
     c['no_seeds'] = (dict(size_filter=0), dict(input=x, seeds=np.zeros(SHAPE, np.uint64)))
     c['filter_all'] = (dict(size_filter=10 ** 9), dict(input=x, seeds=_seeds(SHAPE, 30, rng)))
     c['raw_plateaus'] = (dict(size_filter=25), dict(input=raw, seeds=_seeds(SHAPE, 80, rng, blob=3)))
-    # one flat plateau 64 x 4096 wide: hop distances up to 4158 > kDMax = 4095 (the 12-bit d
-    # saturates near the far corner)
+    # one flat plateau 64 x 4096 with three seeds: hop distances to the nearest seed up to 1,099
+    # (tie order on a wide plateau; the floods that meet past kDMax = 4095 hops are the corridor
+    # cases, tests/test_corridor_gpu.py)
     dp = np.zeros((1, 64, 4096), np.uint64)
     dp[0, 0, 0], dp[0, 63, 4095], dp[0, 40, 2000] = 9, 4, 7
-    c['deep_plateau'] = (dict(size_filter=0), dict(input=np.full((1, 64, 4096), .5, np.float32), seeds=dp))
+    c['wide_plateau'] = (dict(size_filter=0), dict(input=np.full((1, 64, 4096), .5, np.float32), seeds=dp))
     return c
 
 
@@ -71,7 +72,7 @@ CASES = _cases()
 # schedule reproduces.  There the GPU must equal the flood model exactly and the whole VI gap to
 # the heap order must be the model's tie order (gaps measured with the oracle: 4d_max 0.012,
 # uint8 0.54, raw_plateaus 1.78; other tie orders: profiles/r05/tie_order_experiment.json).
-TIE_GAP = {'4d_max': 0.02, 'uint8': 0.7, 'raw_plateaus': 2.0, 'deep_plateau': 1.8}  # deep_plateau: 1.774
+TIE_GAP = {'4d_max': 0.02, 'uint8': 0.7, 'raw_plateaus': 2.0, 'wide_plateau': 1.8}  # wide_plateau: 1.774
 
 
 @pytest.mark.parametrize('name', sorted(CASES))

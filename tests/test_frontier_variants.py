@@ -2,7 +2,8 @@
 
 The flood's fixpoint (K = f(min of the neighbours' keys), k_flood.hip) is unique, so every
 chunk brick (CTWS_FRONTIER_CHUNK2D / _3D), a one-sweep limit (CTWS_FRONTIER_REPS=1: every changed chunk hits the limit, so the
-non-converged re-queue path runs), and the masked-plateau fill switched off (CTWS_PLATEAU_FILL=0) must reproduce the oracle's flood model bit for bit on every
+non-converged re-queue path runs), the masked-plateau fill switched off (CTWS_PLATEAU_FILL=0) and the wide keys
+(CTWS_FORCE_WIDE=1) must reproduce the oracle's flood model bit for bit on every
 parity case, as the default schedule does (test_gpu_parity.py::test_flood_matches_model_exactly).
 The knobs are read when a handle is opened.
 """
@@ -26,6 +27,9 @@ VARIANTS = {
     'no_plateau_fill': {'CTWS_PLATEAU_FILL': '0'},
     # cropped blocks' uint64 output through the word-tiled k_output instead of k_output_crop
     'output_words': {'CTWS_OUTPUT_TILE': '0'},
+    # every flood on the wide keys (k_flood, labels apart, 32-bit d): the path run_batch re-runs a
+    # block on when its packed flood saturated d (tests/test_corridor_gpu.py)
+    'wide_keys': {'CTWS_FORCE_WIDE': '1'},
 }
 
 

@@ -1,0 +1,117 @@
+"""The multi-rank two-pass schedule (sharded.pass2_rank_schedule, bench.py's config-5 leg) is the
+reference's sequential loop (two_pass_watershed.py:296-299), VERDICT r05 #8.
+
+A toy pass 2 -- each block's output is a hash of everything its input_bb reads -- run
+(a) sequentially over the whole volume in list order, and (b) on z-slab ranks that each hold
+their slab plus z halos, running the global dependency levels with the z-halo exchanges the
+schedule asks for, must write identical volumes.  The round-5 harness (one exchange, before
+pass 2) is shown to differ on the same geometry, so the test sees the dependency it guards."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import blocking  # noqa: E402
+from cluster_tools_amd.watershed.sharded import pass2_rank_schedule  # noqa: E402
+
+
+def _sl(beg, end):
+    return tuple(slice(a, b) for a, b in zip(beg, end))
+
+
+def _setup(shape, block_shape, halo, world):
+    blocks = blocking(shape, block_shape, halo)
+    grid = [(s + b - 1) // b for s, b in zip(shape, block_shape)]
+    nzb = grid[0]
+    slabs = []
+    for r in range(world):
+        r0, r1 = nzb * r // world, nzb * (r + 1) // world
+        slabs.append((r0 * block_shape[0], min(shape[0], r1 * block_shape[0])))
+
+    def owner(b):
+        return next(r for r, (z0, z1) in enumerate(slabs) if z0 <= b['beg'][0] < z1)
+
+    def colour(b):
+        return sum(bb // s for bb, s in zip(b['beg'], block_shape)) % 2
+    p1 = [b for b in blocks if colour(b) == 0]
+    p2 = [b for b in blocks if colour(b) == 1]
+    return blocks, slabs, owner, p1, p2
+
+
+def _value(read, bid):
+    return np.uint64((int(read.astype(np.uint64).sum()) * 1000003 + bid * 7919) % (1 << 40) + 1)
+
+
+def _sequential(shape, p1, p2):
+    vol = np.zeros(shape, np.uint64)
+    for b in p1:
+        vol[_sl(b['beg'], b['end'])] = b['block_id'] + 1
+    for b in p2:
+        v = _value(vol[_sl(b['obeg'], b['oend'])], b['block_id'])
+        vol[_sl(b['beg'], b['end'])] = v
+    return vol
+
+
+def _sharded(shape, halo, slabs, owner, p1, p2, all_exchanges=True):
+    world = len(slabs)
+    hz = halo[0]
+    reg = [(max(0, z0 - hz), min(shape[0], z1 + hz)) for z0, z1 in slabs]
+    loc = [np.zeros((g1 - g0,) + tuple(shape[1:]), np.uint64) for g0, g1 in reg]
+
+    def local(r, beg, end):
+        return _sl([beg[0] - reg[r][0]] + list(beg[1:]), [end[0] - reg[r][0]] + list(end[1:]))
+
+    def exchange():
+        # every rank's own rows next to a boundary into its neighbours' halo rows
+        for r in range(world):
+            z0, z1 = slabs[r]
+            for n in (r - 1, r + 1):
+                if 0 <= n < world:
+                    a, b = max(z0, reg[n][0]), min(z1, reg[n][1])
+                    if a < b:
+                        loc[n][a - reg[n][0]:b - reg[n][0]] = loc[r][a - reg[r][0]:b - reg[r][0]]
+    for b in p1:
+        r = owner(b)
+        loc[r][local(r, b['beg'], b['end'])] = b['block_id'] + 1
+    glist = [(owner(b), _sl(b['obeg'], b['oend']), _sl(b['beg'], b['end'])) for b in p2]
+    levels, exch = pass2_rank_schedule(glist, slabs, hz)
+    if not all_exchanges:
+        exch = [k == 0 for k in range(len(exch))]
+    for lv in range(len(exch)):
+        if exch[lv]:
+            exchange()
+        todo = [b for b, l in zip(p2, levels) if l == lv]
+        vals = [_value(loc[owner(b)][local(owner(b), b['obeg'], b['oend'])], b['block_id']) for b in todo]
+        for b, v in zip(todo, vals):
+            r = owner(b)
+            loc[r][local(r, b['beg'], b['end'])] = v
+    vol = np.zeros(shape, np.uint64)
+    for r, (z0, z1) in enumerate(slabs):
+        vol[z0:z1] = loc[r][z0 - reg[r][0]:z1 - reg[r][0]]
+    return vol, exch
+
+
+@pytest.mark.parametrize('world', [1, 2, 3, 4])
+@pytest.mark.parametrize('geom', [((64, 32, 32), (8, 16, 16), (2, 4, 4)),
+                                  ((96, 48, 40), (16, 16, 16), (8, 8, 8)),
+                                  ((64, 64, 64), (8, 32, 32), (4, 8, 8))])
+def test_rank_schedule_is_sequential(world, geom):
+    shape, bs, halo = geom
+    _, slabs, owner, p1, p2 = _setup(shape, bs, halo, world)
+    ref = _sequential(shape, p1, p2)
+    got, exch = _sharded(shape, halo, slabs, owner, p1, p2)
+    np.testing.assert_array_equal(got, ref)
+    if world == 1:
+        assert sum(exch) == 1  # only the pass-1 labels
+
+
+def test_single_exchange_is_not_sequential():
+    """The round-5 harness (z halos exchanged once, before pass 2) differs from the sequential
+    loop where a pass-2 block's halo holds a neighbour rank's earlier pass-2 output."""
+    shape, bs, halo = (64, 32, 32), (8, 16, 16), (2, 4, 4)
+    _, slabs, owner, p1, p2 = _setup(shape, bs, halo, 2)
+    ref = _sequential(shape, p1, p2)
+    got, exch = _sharded(shape, halo, slabs, owner, p1, p2, all_exchanges=False)
+    assert sum(exch) == 1 and not np.array_equal(got, ref)

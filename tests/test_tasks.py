@@ -267,3 +267,23 @@ def test_split_blocks_consecutive_keeps_block_ids():
     assert runs == [[3, 4, 7], [8, 11], [12, 30]]
     assert sum(runs, []) == bl
     assert split_blocks(bl, 3) == [[3, 8, 30], [4, 11], [7, 12]]
+
+
+@pytest.mark.parametrize('retries', [0, 1])
+def test_workflow_keeps_retry_with_max_num_retries(tmp_path, retries):
+    """the in-job relabel numbers all blocks at once and cannot re-run one, so
+    with max_num_retries > 0 WatershedWorkflow runs watershed + RelabelWorkflow, whose watershed
+    task retries failed blocks as the reference's does (cluster_tasks.py:127-142)."""
+    from cluster_tools_amd.watershed import WatershedWorkflow
+    from cluster_tools_amd.relabel import RelabelWorkflow
+    cfg = _configs(tmp_path, (16, 32, 32))
+    g = json.load(open(os.path.join(cfg, 'global.config')))
+    g['max_num_retries'] = retries
+    json.dump(g, open(os.path.join(cfg, 'global.config'), 'w'))
+    wf = WatershedWorkflow(input_path='in.n5', input_key='raw', output_path='ws.n5', output_key='ws',
+                           config_dir=cfg, tmp_folder=str(tmp_path / 'tmp'), target='local', max_jobs=2)
+    dep = wf.requires()
+    if retries:
+        assert isinstance(dep, RelabelWorkflow)
+    else:
+        assert not isinstance(dep, RelabelWorkflow) and dep.assignment_key == 'relabel_watershed'

@@ -9,6 +9,7 @@
   composition (oracle threshcc -> orc_ws_from_seeds per block).
 """
 import json
+import os
 import sys
 
 import numpy as np
@@ -78,14 +79,24 @@ def _configs(tmp_path, block_shape, task_configs=None):
     return str(cfg_dir)
 
 
-@pytest.mark.parametrize('merge_in_job', [True, False])
+@pytest.mark.parametrize('merge_in_job', [True, False, 'spill'])
 @pytest.mark.parametrize('masked,max_jobs', [(False, 1), (False, 3), (True, 2)])
 def test_thresholded_components_workflow_matches_oracle(tmp_path, masked, max_jobs, merge_in_job):
     """merge_in_job: the merge tail in the BlockComponents jobs (merge_in_job.py), else the
     reference's five-task chain; with max_jobs > 1 BlockFaces has several jobs (one of them
-    without any pair makes the reference's merge the identity -- both modes must agree)."""
+    without any pair makes the reference's merge the identity -- both modes must agree).
+    'spill': the in-job merge with the labels written as they come and re-read by the merge
+    (block_components.spill_labels, the path a job takes when its labels would not fit its
+    share of host memory)."""
     from conftest import luigi_build
     from cluster_tools_amd.thresholded_components import ThresholdedComponentsWorkflow
+    from cluster_tools_amd.thresholded_components.block_components import BlockComponentsLocal
+    task_configs = None
+    if merge_in_job == 'spill':
+        bc = BlockComponentsLocal.default_task_config()
+        bc['merge_spill'] = True
+        task_configs = {'block_components': bc}
+        merge_in_job = True
     shape, bs = (32, 96, 160), (16, 32, 64)
     x = _volume(shape, 7)
     path = str(tmp_path / 'data.n5')
@@ -99,12 +110,15 @@ def test_thresholded_components_workflow_matches_oracle(tmp_path, masked, max_jo
             f.create_dataset('mask', data=mask, chunks=(8, 16, 32))
     wf = ThresholdedComponentsWorkflow(input_path=path, input_key='x', output_path=path, output_key='cc',
                                        assignment_key='ass', threshold=.55, tmp_folder=str(tmp_path / 'tmp'),
-                                       config_dir=_configs(tmp_path, bs), max_jobs=max_jobs, target='local',
-                                       mask_path=path if masked else '', mask_key='mask' if masked else '',
-                                       merge_in_job=merge_in_job)
+                                       config_dir=_configs(tmp_path, bs, task_configs), max_jobs=max_jobs,
+                                       target='local', mask_path=path if masked else '',
+                                       mask_key='mask' if masked else '', merge_in_job=merge_in_job)
     luigi_build(wf, tmp_path / 'tmp')
     ref_seg, ref_ass, ref_off = T.thresholded_components(x, Blocking([0, 0, 0], list(shape), list(bs)), .55,
                                                          'greater', mask=mask, faces_jobs=max_jobs)
+    # the merge removes its per-run files (face planes, pair files, merged assignments)
+    left = [n for n in os.listdir(str(tmp_path / 'tmp')) if n.startswith(('cc_face_', 'cc_block_pairs_', 'cc_assign'))]
+    assert not left, left
     with vu.file_reader(path, 'r') as f:
         seg, ass = f['cc'][:], f['ass'][:]
         max_id = f['cc'].attrs['maxId']
