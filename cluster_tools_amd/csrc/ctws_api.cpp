@@ -117,6 +117,7 @@ struct ctws_handle {
     int64_t rl_ntable = 0;  // entries of the resident assignment table (rl_keys / rl_vals)
     // EDT: counters (64 B) + columns queued for the lower-envelope pass (k_edt_col_fh)
     DevBuf edt_fh;
+    DevBuf xface;  // crop CC: the tiles' x columns (CcArgs::xface)
     DevBuf edt_scratch;  // k_edt_real_line: per-thread parabola stacks
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
@@ -305,7 +306,7 @@ int ensure_workspace(ctws_handle* h, int64_t vox, int64_t words, int64_t chunks,
     if (!w.fflags) ALLOC(fflags, kFrontierBatch);
     if (!w.wlcnt) ALLOC(wlcnt, kFrontierMaxItersCap + 2);
     if (blocks > w.cap_fstat) {
-        ALLOC(fstat, 2 * blocks);
+        ALLOC(fstat, 3 * blocks);
         ALLOC(plev, blocks);
         w.cap_fstat = blocks;
     }
@@ -710,6 +711,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
         k_frontier<ND, CW, CY, CZ><<<fg, 256, 0, h->stream>>>(                                                      \
             w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
+            fst ? fst + 2 * nb : nullptr,                                                                             \
             h->frontier_reps, h->frontier_dir);                                                                     \
         break;
             switch (fkind) {
@@ -987,6 +989,17 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             max_tiles = std::max(max_tiles, d.tz * d.ty * d.tx);
         }
     };
+    // crop CC: each cropped block's tiles get 2 x columns of (root, label) entries (k_tile_cc)
+    int64_t TXF = 0;
+    {
+        const int ctz = pl.nd_ws == 3 ? CcTile<3>::TZ : CcTile<2>::TZ;
+        const int cty = pl.nd_ws == 3 ? CcTile<3>::TY : CcTile<2>::TY;
+        const int ctx = pl.nd_ws == 3 ? CcTile<3>::TX : CcTile<2>::TX;
+        for (auto& d : desc) {
+            d.xcbase = TXF;
+            if (d.crop) TXF += (int64_t)cdiv(d.IZ, ctz) * cdiv(d.IY, cty) * cdiv(d.IX, ctx) * 2 * ctz * cty;
+        }
+    }
     h->last_bare.assign(nb, 1);  // (a run stopped early by a test hook writes no labels)
     h->cur_max[0] = maxZ;
     h->cur_max[1] = maxY;
@@ -998,6 +1011,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     set_tiles(true);
     int r;
     if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb, TH, TF)) != CTWS_OK) return r;
+    if (TXF && (r = grow(h, h->xface, sizeof(uint64_t) * (size_t)TXF)) != CTWS_OK) return r;
     if (pl.pass2 && pl.nd_ws == 2 && (int)h->p2_hints.size() == nb) {
         std::vector<uint32_t> flat;
         for (int i = 0; i < nb; ++i) {
@@ -1234,7 +1248,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
         // the seed CC's member bitmap (CcArgs::troot for SEED): its parents are members-only
         HIPCHK(hipMemsetAsync(w.fseed, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed};
+        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed, nullptr};
         if (pl.nd_ws == 3) {
             using T = CcTileM<3, CC_SEED>;  // (= the plateau tile)
             const dim3 tg(tiles8(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
@@ -1340,8 +1354,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     uint32_t* fst = h->trace ? w.fstat : nullptr;
     if (descent) {
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
-        // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
-        const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
+        // tile-local descent + pointer jumping (8 x 8 x 64 / 1 x 64 x 64 tiles)
+        const int dz = pl.nd_ws == 3 ? 8 : 1, dy = pl.nd_ws == 3 ? 8 : 64, dx = 64;  // DTile
         const dim3 dg(tiles8(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
         {
             if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
@@ -1349,7 +1363,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             LAUNCHCHK();
         }
         mark("descent_tile");
-        if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
+        if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 3 * (size_t)nb, h->stream));
         // masked blocks: their plateau leaves the open set until the rest is flooded (k_plateau.hip);
         // the plateau level comes out of the descent pass
         bool any_mask = false;
@@ -1387,16 +1401,18 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
         mark("flood_relax");
         if (fst) {
-            std::vector<uint32_t> hs(2 * (size_t)nb);
-            HIPCHK(hipMemcpyAsync(hs.data(), fst, sizeof(uint32_t) * 2 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
+            std::vector<uint32_t> hs(3 * (size_t)nb);
+            HIPCHK(hipMemcpyAsync(hs.data(), fst, sizeof(uint32_t) * 3 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
-            double no = 0, nv = 0;
+            double no = 0, nv = 0, nc = 0;
             for (int i = 0; i < nb; ++i) {
                 no += hs[i];
                 nv += hs[nb + i];
+                nc += hs[2 * nb + i];
             }
             add_timing(h, "open_voxels", (float)no);
             add_timing(h, "frontier_visits", (float)nv);
+            add_timing(h, "frontier_key_writes", (float)nc);
         }
         // fixpoint check of every voxel (a guard: the descent argument and the frontier's
         // convergence make a violation impossible); on a violation the batch is flooded again
@@ -1633,7 +1649,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (any_crop) {
             // tile roots of the crop CC marked in the (free) frontier bitmap front0
             HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0};
+            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0, (uint64_t*)h->xface.p};
             const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;

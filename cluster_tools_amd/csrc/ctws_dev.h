@@ -44,6 +44,7 @@ struct BlockDesc {
     int64_t hcap;           // pass 2: hash capacity of this block (power of two)
     int64_t fbase;          // offset into the frontier bitmaps (Z*Y rows of ceil(X/64) words)
     int64_t p2hint;         // pass 2 (2-D): offset of the block's per-slice offset hint (-1: none)
+    int64_t xcbase;         // crop CC: offset of the block's tiles in CcArgs::xface
 };
 
 struct BlockStat {
@@ -67,7 +68,7 @@ constexpr uint32_t kErrHashFull = 1u;    // pass 2: relabel hash table full
 constexpr uint32_t kErrCollision = 2u;   // pass 2 (2-D): wrapped new id == initial id (unresolved)
 constexpr uint32_t kErrLabelBits = 4u;   // auto-seeded regrow: labels beyond the 20-bit key field
 constexpr uint32_t kErrTakeDict = 8u;    // pass 2: auto-seed label without a new_to_old entry
-constexpr uint32_t kErrUnsupported = 16u; // auto-seeded regrow in a block with >= 2^20 seeds (wide keys)
+constexpr uint32_t kErrUnsupported = 16u; // (unused since round 6: the wide keys auto-seed their regrow too)
 constexpr uint32_t kErrVerify = 64u;     // the regrow's fixpoint check failed (CTWS_VERIFY=1): labels not written
 constexpr uint32_t kErrOverflow = 32u;    // WatershedFromSeeds: seed id >= 2^32 - 1 (the reference's assert)
 
@@ -386,10 +387,12 @@ constexpr uint32_t kLabelBits = 20;
 constexpr uint64_t kLabelMask = (1ull << kLabelBits) - 1ull;
 constexpr uint64_t kDOne = 1ull << kLabelBits;
 constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
-// The tie order inside an equal-C plateau: d = hops since the plateau level was entered,
-// saturating at kDMax (the 12-bit field; INF has d = 0xFFF and stays INF).  d must grow along
-// every parent edge: then (C, d) strictly increases from a voxel's argmin neighbour to the voxel,
-// the fixpoint is unique, and any relaxation schedule reaches the sequential model's result.
+// The tie order inside an equal-C plateau: d = hops since the plateau level was entered (the
+// 12-bit field saturates at kDMax; INF has d = 0xFFF and stays INF).  d must grow along every
+// parent edge: then (C, d) strictly increases from a voxel's argmin neighbour to the voxel, the
+// fixpoint is unique, and any relaxation schedule reaches the sequential model's result.  A
+// saturated d breaks that, so a write of d = kDMax is reported (note_dsat below) and the block is
+// flooded again on the wide keys, whose 32-bit d never saturates (round 6).
 // Orders with d capped at 1 or without d measured closer to vigra's heap order on tie-dominated
 // inputs (scripts/tie_order_experiment.py) but lose that: equal keys along a plateau path let a
 // cycle of voxels keep a stale label, and the GPU converged to such a fixpoint (round 4,

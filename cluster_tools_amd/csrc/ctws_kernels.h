@@ -122,6 +122,8 @@ struct CcArgs {
     uint64_t* troot;       // CROP: tile-root bitmap (inner C index, per block at fbase), zeroed;
                            // SEED: the members (seed voxels; outer rows), zeroed.  The seed forest's
                            // parents are written for members only: readers test this bitmap first
+    uint64_t* xface;       // CROP: per tile, its low and high x columns as (root << 32 | label)
+                           // (k_tile_cc writes, k_tile_merge's x face reads; per block at xcbase)
 };
 template <int ND>
 struct CcTile;
@@ -171,7 +173,7 @@ __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*,
 template <int ND, int CW, int CY, int CZ>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
-                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int);
+                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int);
 // k_eval.hip (VI / Rand contingency table)
 __global__ void k_eval_add(const uint64_t*, const uint64_t*, int64_t, int, uint64_t*, unsigned long long*, int64_t,
                            uint64_t*, unsigned long long*, int64_t, uint64_t*, unsigned long long*, int64_t,

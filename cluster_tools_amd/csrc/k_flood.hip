@@ -539,7 +539,7 @@ namespace ctws {
 // flooded again from the seeds alone.
 // =========================================================================================
 
-// Descent inside a tile: tile (3-D 16^3, 2-D 1 x 64 x 64) + 1-voxel halo of heights in LDS;
+// Descent inside a tile: tile (3-D 8 x 8 x 64, 2-D 1 x 64 x 64) + 1-voxel halo of heights in LDS;
 // every tile voxel gets its steepest-descent parent (itself for seeds, local minima and ties),
 // then pointer jumping in LDS runs each chain to its end inside the tile: a root of the tile
 // or the first voxel outside it.  exit[q] = kDescRes | label for a chain ending at a tile root
@@ -561,7 +561,10 @@ template <int ND>
 struct DTile;
 template <>
 struct DTile<3> {
-    static constexpr int TZ = 16, TY = 16, TX = 16, HZ = 18;
+    // 64 wide in x: a halo row of 66 heights is 264 contiguous bytes (3 lines) where a 16^3
+    // tile's 18-height rows each touched 1-2 lines for 72 bytes (the 16^3 tile
+    // read 20 B per outer voxel for the 4 B of h it needs)
+    static constexpr int TZ = 8, TY = 8, TX = 64, HZ = 10;
 };
 template <>
 struct DTile<2> {
@@ -969,7 +972,8 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                                   uint32_t* __restrict__ gnext, int it, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ cnt, uint32_t* __restrict__ list_next,
                                                   uint32_t* __restrict__ cnt_next, uint32_t* __restrict__ qgen,
-                                                  uint32_t* __restrict__ nvisit, int reps, int dirf) {
+                                                  uint32_t* __restrict__ nvisit, uint32_t* __restrict__ nchange,
+                                                  int reps, int dirf) {
     static_assert(ND == 3 || CZ == 1, "2-D ws: slices are independent, chunks are one slice deep");
     __shared__ uint64_t schg[kFrontierWaves][64];
     // dirf: the local sweeps queue only the neighbours a change of p can affect, by the (C, d)
@@ -1071,6 +1075,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
         uint64_t acc = 0ull;  // changed bits of this word over all local sweeps
         bool conv = true;     // the local sweeps ended without a pending change
         uint32_t vis = 0;     // statistics (CTWS_TRACE): voxels visited
+        uint32_t nch = 0;     // statistics (CTWS_TRACE): keys written
         for (int rep = 0;; ++rep) {
             // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list
             // is bit (e - pre[j]) of word j, the last j with pre[j] <= e
@@ -1155,6 +1160,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                     if (k == own[u]) continue;
                     kb[iv[u]] = k;
                     if (key_dsat(k)) note_dsat(S, bi);
+                    ++nch;
                     atomicOr((unsigned long long*)&schg[wv][jv[u]], 1ull << bv[u]);
                     if (dirf) {
                         // nb[] order: -z, +z, -y, +y, -x, +x (outside the block: INF, its bit is
@@ -1208,6 +1214,10 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             f &= opw;
         }
         if (nvisit && lane == 0 && vis) atomicAdd(&nvisit[bi], vis);
+        if (nchange) {
+            for (int o = 32; o > 0; o >>= 1) nch += (uint32_t)__shfl_xor((int)nch, o);
+            if (lane == 0 && nch) atomicAdd(&nchange[bi], nch);
+        }
         if (__ballot(acc != 0ull) == 0ull) continue;
         // the chunk changed: publish its changed words and queue the chunks that hold a
         // neighbour of a change (faces), and itself unless its local sweeps converged
@@ -1242,7 +1252,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
                                                         const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,  \
                                                         uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*,   \
-                                                        uint32_t*, uint32_t*, uint32_t*, int, int);
+                                                        uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int);
 #define CTWS_LIST0_INST(CW, CY, CZ)                                                                             \
     template __global__ void k_frontier_list0<CW, CY, CZ>(const BlockDesc*, const BlockStat*, const uint64_t*, \
                                                           uint32_t*, uint32_t*);

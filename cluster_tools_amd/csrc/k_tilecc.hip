@@ -249,10 +249,10 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             }
             if (!mem) continue;
         }
-        if (z >= nz || y >= ny || x >= nx) continue;
+        const bool ind = z < nz && y < ny && x < nx;
         uint32_t g = kNoParent;
         const int64_t gi = ((int64_t)z * ny + y) * nx + x;
-        if (vv[j] != kLNone) {
+        if (ind && vv[j] != kLNone) {
             const uint32_t r = lds_find(sp, (uint32_t)c);
             const int rx = (int)(r % TX), ry = (int)((r / TX) % TY), rz = (int)(r / (TX * TY));
             g = (uint32_t)(((int64_t)(z0 + rz) * ny + (y0 + ry)) * nx + (x0 + rx));
@@ -260,6 +260,13 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
             if (MODE == CC_CROP && r == (uint32_t)c)
                 atomicOr((unsigned long long*)&a.troot[B.fbase + (gi >> 6)], 1ull << (gi & 63));
         }
+        if (MODE == CC_CROP && (lx == 0 || lx == TX - 1)) {
+            // the x columns for k_tile_merge: its x face reads them contiguously instead of one
+            // cache line per voxel for each of P, key and mask on both sides
+            const int64_t xb = B.xcbase + (int64_t)t * 2 * TZ * TY + (lx == 0 ? 0 : TZ * TY) + lz * TY + ly;
+            a.xface[xb] = ((uint64_t)g << 32) | (uint64_t)(ind ? vv[j] : kLNone);
+        }
+        if (!ind) continue;
         P[gi] = g;
     }
 }
@@ -295,7 +302,20 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
         for (int e0 = 0; e0 < n; e0 += 256) {
             const int e = e0 + (int)threadIdx.x;
             uint32_t ra = kNoParent, rb = kNoParent;
-            if (e < n) {
+            if (MODE == CC_CROP && f == 2) {
+                // x face from the tiles' x columns (k_tile_cc): this tile's low column against
+                // the high column of the tile before it in x, (root << 32 | label) each
+                if (e < n && txi > 0) {
+                    const int64_t tb = B.xcbase + (int64_t)t * 2 * TZ * TY;
+                    const uint64_t own = a.xface[tb + e];
+                    const uint64_t prv = a.xface[tb - 2 * TZ * TY + TZ * TY + e];
+                    const uint32_t lo = (uint32_t)own, lp = (uint32_t)prv;
+                    if (lo != kLNone && lo == lp) {
+                        ra = (uint32_t)(own >> 32);
+                        rb = (uint32_t)(prv >> 32);
+                    }
+                }
+            } else if (e < n) {
                 int lz, ly, lx;
                 if (f == 0) { lz = 0; ly = e / TX; lx = e % TX; }
                 else if (f == 1) { lz = e / TX; ly = 0; lx = e % TX; }

@@ -336,11 +336,14 @@ def _test_fail_once(blocks):
     folder = os.environ.get('CTWS_TEST_FAIL_ONCE')
     if not folder:
         return
+    fail = []
     for b in blocks:
         marker = os.path.join(folder, 'failed_block_%i' % b['block_id'])
         if b['block_id'] % 4 == 1 and not os.path.exists(marker):
             open(marker, 'w').close()
-            raise RuntimeError("injected failure of block %i (CTWS_TEST_FAIL_ONCE)" % b['block_id'])
+            fail.append(b['block_id'])
+    if fail:
+        raise RuntimeError("injected failure of blocks %s (CTWS_TEST_FAIL_ONCE)" % fail)
 
 
 def _keep_on_device(blocking, block_list, config):

@@ -117,7 +117,8 @@ def test_thresholded_components_workflow_matches_oracle(tmp_path, masked, max_jo
     ref_seg, ref_ass, ref_off = T.thresholded_components(x, Blocking([0, 0, 0], list(shape), list(bs)), .55,
                                                          'greater', mask=mask, faces_jobs=max_jobs)
     # the merge removes its per-run files (face planes, pair files, merged assignments)
-    left = [n for n in os.listdir(str(tmp_path / 'tmp')) if n.startswith(('cc_face_', 'cc_block_pairs_', 'cc_assign'))]
+    left = [n for n in os.listdir(str(tmp_path / 'tmp'))
+            if n.startswith(('cc_face_', 'cc_block_pairs_', 'cc_assignments_merged'))]
     assert not left, left
     with vu.file_reader(path, 'r') as f:
         seg, ass = f['cc'][:], f['ass'][:]

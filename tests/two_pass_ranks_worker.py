@@ -12,7 +12,9 @@ import numpy as np  # noqa: E402
 
 import bench  # noqa: E402
 
-bench.CONFIGS['test_two_pass'] = dict(
+TEST_CONFIG = 99  # (bench.py prints config ids with %d)
+
+bench.CONFIGS[TEST_CONFIG] = dict(
     shape=(128, 128, 128), full_shape=(128, 128, 128), block_shape=(32, 64, 64), halo=(8, 16, 16), dtype='uint8',
     mask=True, two_pass=True, seed=5, task=dict(bench.D3, size_filter=25, halo=[8, 16, 16]),
     workload='test: 128^3 uint8 + ellipsoid mask, 32x64x64 blocks, halo [8,16,16], two-pass')
@@ -26,7 +28,7 @@ def main(out_dir):
     dev = torch.device('cuda', 0)
     if world > 1:
         dist.init_process_group('gloo')
-    m = bench.run_workload('test_two_pass', 'strong', rank, world, dev, 1, 0, 1, keep_volume=True)
+    m = bench.run_workload(TEST_CONFIG, 'strong', rank, world, dev, 1, 0, 1, keep_volume=True)
     np.save(os.path.join(out_dir, 'rank%d_of%d.npy' % (rank, world)), m['kept_volume'])
     with open(os.path.join(out_dir, 'rank%d_of%d.json' % (rank, world)), 'w') as f:
         json.dump({'z0': m['geo']['z0'], 'n_exchanges': m['n_exchanges'], 'ngroups': m['ngroups']}, f)
