@@ -118,6 +118,7 @@ struct ctws_handle {
     // EDT: counters (64 B) + columns queued for the lower-envelope pass (k_edt_col_fh)
     DevBuf edt_fh;
     DevBuf xface;  // crop CC: the tiles' x columns (CcArgs::xface)
+    DevBuf ptile;  // plateau CC: per-tile plateau flags (CcArgs::ptile)
     DevBuf edt_scratch;  // k_edt_real_line: per-thread parabola stacks
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
@@ -1000,6 +1001,17 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             if (d.crop) TXF += (int64_t)cdiv(d.IZ, ctz) * cdiv(d.IY, cty) * cdiv(d.IX, ctx) * 2 * ctz * cty;
         }
     }
+    // plateau CC: one flag per tile (k_localmax sets it for the tiles with a plateau voxel)
+    int64_t TPT = 0;
+    {
+        const int ptz = pl.nd_ws == 3 ? CcTileM<3, CC_PLATEAU>::TZ : CcTileM<2, CC_PLATEAU>::TZ;
+        const int pty = pl.nd_ws == 3 ? CcTileM<3, CC_PLATEAU>::TY : CcTileM<2, CC_PLATEAU>::TY;
+        const int ptx = pl.nd_ws == 3 ? CcTileM<3, CC_PLATEAU>::TX : CcTileM<2, CC_PLATEAU>::TX;
+        for (auto& d : desc) {
+            d.ptbase = TPT;
+            TPT += (int64_t)cdiv(d.Z, ptz) * cdiv(d.Y, pty) * cdiv(d.X, ptx);
+        }
+    }
     h->last_bare.assign(nb, 1);  // (a run stopped early by a test hook writes no labels)
     h->cur_max[0] = maxZ;
     h->cur_max[1] = maxY;
@@ -1012,6 +1024,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     int r;
     if ((r = ensure_workspace(h, T, TW, TC, TS, std::max(TT_packed, TT_wide), nb, TH, TF)) != CTWS_OK) return r;
     if (TXF && (r = grow(h, h->xface, sizeof(uint64_t) * (size_t)TXF)) != CTWS_OK) return r;
+    if ((r = grow(h, h->ptile, sizeof(uint32_t) * (size_t)std::max<int64_t>(TPT, 1))) != CTWS_OK) return r;
     if (pl.pass2 && pl.nd_ws == 2 && (int)h->p2_hints.size() == nb) {
         std::vector<uint32_t> flat;
         for (int i = 0; i < nb; ++i) {
@@ -1174,18 +1187,13 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         const unsigned gfh = (unsigned)std::min<int64_t>((ncols + 255) / 256, 1024);
         auto launch_col = [&](int W, dim3 g, size_t lds, EdtColParams p, const uint32_t* gin, uint32_t* gout,
                               uint32_t* cnt) {
-            if (lds > 65536)  // gfx950: up to 160 KiB of LDS per workgroup, above 64 KiB by opt-in
-                (void)hipFuncSetAttribute((const void*)(W == 32 ? k_edt_col<32> : W == 16 ? k_edt_col<16> : k_edt_col<8>),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (W == 32)
-                k_edt_col<32><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list,
-                                                          cnt);
-            else if (W == 16)
-                k_edt_col<16><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list,
-                                                          cnt);
-            else
-                k_edt_col<8><<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list,
-                                                         cnt);
+            auto go = [&](auto kern) {
+                lds_optin(kern, lds);
+                kern<<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list, cnt);
+            };
+            if (W == 32) go(k_edt_col<32>);
+            else if (W == 16) go(k_edt_col<16>);
+            else go(k_edt_col<8>);
             k_edt_col_fh<<<gfh, 256, 0, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list, cnt);
         };
         launch_col(Wy, gy, ldsy, ep, (uint32_t*)w.A, (uint32_t*)w.Bf, fh_cnt);
@@ -1242,13 +1250,14 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
 
     // ---- seeds: local maxima, plateaus, CC, vigra scan-order ids -----------------------------
     {
-        k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.smax);
+        HIPCHK(hipMemsetAsync(h->ptile.p, 0, sizeof(uint32_t) * (size_t)std::max<int64_t>(TPT, 1), h->stream));
+        k_localmax<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, seedmap, w.cls, w.smax, (uint32_t*)h->ptile.p);
         LAUNCHCHK();
         // plateaus (equal-valued maxima candidates) and the seed CC: LDS tile union-find
         // (k_tilecc.hip); blocks without plateau voxels skip the plateau kernels on the device
         // the seed CC's member bitmap (CcArgs::troot for SEED): its parents are members-only
         HIPCHK(hipMemsetAsync(w.fseed, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed, nullptr};
+        CcArgs ca{seedmap, w.cls, w.P, nullptr, nullptr, 0, w.fseed, nullptr, (const uint32_t*)h->ptile.p};
         if (pl.nd_ws == 3) {
             using T = CcTileM<3, CC_SEED>;  // (= the plateau tile)
             const dim3 tg(tiles8(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
@@ -1354,8 +1363,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     uint32_t* fst = h->trace ? w.fstat : nullptr;
     if (descent) {
         // descent pre-pass (k_flood.hip): voxels whose steepest descent reaches a seed are final
-        // tile-local descent + pointer jumping (8 x 8 x 64 / 1 x 64 x 64 tiles)
-        const int dz = pl.nd_ws == 3 ? 8 : 1, dy = pl.nd_ws == 3 ? 8 : 64, dx = 64;  // DTile
+        // tile-local descent + pointer jumping (16^3 / 1 x 64 x 64 tiles)
+        const int dz = pl.nd_ws == 3 ? 16 : 1, dy = pl.nd_ws == 3 ? 16 : 64, dx = pl.nd_ws == 3 ? 16 : 64;  // DTile
         const dim3 dg(tiles8(((maxZ + dz - 1) / dz) * ((maxY + dy - 1) / dy) * ((maxX + dx - 1) / dx)), nb);
         {
             if (pl.nd_ws == 3) k_descent_tile<3><<<dg, 512, 0, h->stream>>>(w.desc, w.stat, w.hm, w.lab, cc, w.fseed, w.P);
@@ -1649,7 +1658,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (any_crop) {
             // tile roots of the crop CC marked in the (free) frontier bitmap front0
             HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
-            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0, (uint64_t*)h->xface.p};
+            CcArgs ca{nullptr, nullptr, nullptr, w.lab, w.key, keys_final, w.front0, (uint64_t*)h->xface.p, nullptr};
             const dim3 wgi((unsigned)((words_of(maxNI) + 255) / 256), nb);
             if (pl.nd_ws == 3) {
                 using T = CcTile<3>;

@@ -45,6 +45,7 @@ struct BlockDesc {
     int64_t fbase;          // offset into the frontier bitmaps (Z*Y rows of ceil(X/64) words)
     int64_t p2hint;         // pass 2 (2-D): offset of the block's per-slice offset hint (-1: none)
     int64_t xcbase;         // crop CC: offset of the block's tiles in CcArgs::xface
+    int64_t ptbase;         // plateau CC: offset of the block's tile flags (CcArgs::ptile)
 };
 
 struct BlockStat {

@@ -79,14 +79,15 @@ __global__ void k_gauss_col_r(const BlockDesc*, const BlockStat*, GaussParams, H
 template <int R>
 __global__ void k_gauss_row_r(const BlockDesc*, const BlockStat*, GaussParams, HmapParams, const double*, const float*,
                               const float*, const uint32_t*, const uint32_t*, float*);
-// fused y + x passes on 2-D tiles: kGaussYxTY rows x (128 - 2R) columns per workgroup
+// fused y + x passes on 2-D tiles: kGaussYxTY rows x (128 - 2R) columns per workgroup (the x pass
+// maps 8 threads to each of the 32 rows)
 constexpr int kGaussYxTY = 32;
 template <int R>
 __global__ void k_gauss_yx(const BlockDesc*, const BlockStat*, int, HmapParams, const double*, const double*,
                            const float*, const float*, const uint32_t*, const uint32_t*, float*);
 
 // k_cc.hip
-__global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, const uint32_t*);
+__global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*, const uint32_t*, uint32_t*);
 __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uint32_t*);
 __global__ void k_flatten_tile_roots(const BlockDesc*, const BlockStat*, uint32_t*, const uint64_t*, uint64_t*);
 __global__ void k_flatten_seeds(const BlockDesc*, const BlockStat*, uint32_t*, const uint64_t*, uint64_t*);
@@ -124,6 +125,8 @@ struct CcArgs {
                            // parents are written for members only: readers test this bitmap first
     uint64_t* xface;       // CROP: per tile, its low and high x columns as (root << 32 | label)
                            // (k_tile_cc writes, k_tile_merge's x face reads; per block at xcbase)
+    const uint32_t* ptile; // PLATEAU: per tile, nonzero if it holds a plateau voxel (k_localmax;
+                           // per block at ptbase)
 };
 template <int ND>
 struct CcTile;

@@ -64,7 +64,8 @@ namespace ctws {
 // huge zero plateau otherwise).  pos: the slice's / block's dt maximum > 0.
 template <int ND>
 __device__ __forceinline__ void localmax_words(const BlockDesc& B, const BlockStat& st, const uint32_t* __restrict__ smax,
-                                               const float* __restrict__ p, uint8_t* __restrict__ cl, uint32_t& nplat) {
+                                               const float* __restrict__ p, uint8_t* __restrict__ cl, uint32_t& nplat,
+                                               uint32_t* __restrict__ ptile) {
     const uint32_t ord0 = 0x80000000u;  // ordf(+0.0f)
     constexpr int U = 8, R = U + 2;
     const int Y = B.Y, X = B.X, Z = B.Z;
@@ -86,6 +87,7 @@ __device__ __forceinline__ void localmax_words(const BlockDesc& B, const BlockSt
         const uint32_t strip = un32 / (uint32_t)ngy;
         const int xw = (int)(strip % (uint32_t)wpr), z = (int)(strip / (uint32_t)wpr);
         const int y0 = gy * U;
+        bool ueq = false;  // a plateau voxel in the unit (this lane)
         const int x = xw * 64 + lane;
         const int xc = min(x, X - 1);
         const int xe = lane == 0 ? max(xc - 1, 0) : min(xc + 1, X - 1);  // lane 0: left, others: right
@@ -164,18 +166,33 @@ __device__ __forceinline__ void localmax_words(const BlockDesc& B, const BlockSt
             const bool valid = y < Y && x < X;
             if (valid) cl[zb + (int64_t)y * X + x] = (uint8_t)((gt ? 1 : 0) | (eq ? 2 : 0));
             nplat += valid && eq;  // plateau parents: k_tile_cc<.., CC_PLATEAU> (k_tilecc.hip)
+            ueq |= valid && eq;
+        }
+        // the plateau CC's tiles that hold a plateau voxel (CcTileM<ND, CC_PLATEAU>: 2-D
+        // 1 x 32 x 64, one word column; 3-D 8 x 16 x 32, two tiles per word): the others are
+        // skipped by k_tile_cc / k_tile_merge without reading cls
+        const uint64_t em = __ballot(ueq);
+        if (em && lane < (ND == 3 ? 2 : 1)) {
+            using PT = CcTileM<ND, CC_PLATEAU>;
+            const int ntx = (X + PT::TX - 1) / PT::TX, nty = (Y + PT::TY - 1) / PT::TY;
+            const uint64_t half = ND == 3 ? ((em >> (32 * lane)) & 0xFFFFFFFFull) : em;
+            const int txi = ND == 3 ? 2 * xw + lane : xw;
+            if (half && txi < ntx) {
+                uint32_t* f = ptile + B.ptbase + ((int64_t)(z / PT::TZ) * nty + y0 / PT::TY) * ntx + txi;
+                if (!*f) *f = 1u;
+            }
         }
     }
 }
 
 __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ D, BlockStat* S,
                                                   const float* __restrict__ v, uint8_t* __restrict__ cls,
-                                                  const uint32_t* __restrict__ smax) {
+                                                  const uint32_t* __restrict__ smax, uint32_t* __restrict__ ptile) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     uint32_t nplat = 0;
-    if (B.nd_ws == 3) localmax_words<3>(B, S[blockIdx.y], smax, v + B.base, cls + B.base, nplat);
-    else localmax_words<2>(B, S[blockIdx.y], smax, v + B.base, cls + B.base, nplat);
+    if (B.nd_ws == 3) localmax_words<3>(B, S[blockIdx.y], smax, v + B.base, cls + B.base, nplat, ptile);
+    else localmax_words<2>(B, S[blockIdx.y], smax, v + B.base, cls + B.base, nplat, ptile);
     nplat = wg_reduce_u32(nplat, OpAdd());
     if (threadIdx.x == 0 && nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
 }

@@ -539,7 +539,7 @@ namespace ctws {
 // flooded again from the seeds alone.
 // =========================================================================================
 
-// Descent inside a tile: tile (3-D 8 x 8 x 64, 2-D 1 x 64 x 64) + 1-voxel halo of heights in LDS;
+// Descent inside a tile: tile (3-D 16^3, 2-D 1 x 64 x 64) + 1-voxel halo of heights in LDS;
 // every tile voxel gets its steepest-descent parent (itself for seeds, local minima and ties),
 // then pointer jumping in LDS runs each chain to its end inside the tile: a root of the tile
 // or the first voxel outside it.  exit[q] = kDescRes | label for a chain ending at a tile root
@@ -561,10 +561,10 @@ template <int ND>
 struct DTile;
 template <>
 struct DTile<3> {
-    // 64 wide in x: a halo row of 66 heights is 264 contiguous bytes (3 lines) where a 16^3
-    // tile's 18-height rows each touched 1-2 lines for 72 bytes (the 16^3 tile
-    // read 20 B per outer voxel for the 4 B of h it needs)
-    static constexpr int TZ = 8, TY = 8, TX = 64, HZ = 10;
+    // (8 x 8 x 64 tiles, whose 66-height halo rows are 3 contiguous lines instead of 1-2 lines
+    // per 18-height row, measured slower in round 6: config 4 descent tile 12.1 -> 12.9 ms and
+    // the cross-tile hops of k_descent_init 8.9 -> 9.6 ms, more chains leave a flat tile)
+    static constexpr int TZ = 16, TY = 16, TX = 16, HZ = 18;
 };
 template <>
 struct DTile<2> {

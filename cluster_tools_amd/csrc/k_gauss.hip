@@ -336,6 +336,7 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
                                                   const float* __restrict__ dt, const uint32_t* smin,
                                                   const uint32_t* smax, float* __restrict__ out) {
     constexpr int TX = gauss_yx_tx(R);
+    static_assert(kYxTY == 32, "the x pass maps 8 threads to each of the 32 tile rows");
     constexpr int NROW = kYxTY + 2 * R;
     constexpr int NL = NROW / 2;  // staged rows per thread
     __shared__ float win_s[NROW * kYxP];
@@ -356,6 +357,15 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
     auto refl = [](int p, int L) { return min(max(reflect_idx(p, L), 0), L - 1); };
     const int64_t sbase = B.base + (int64_t)z * Y * X;
     const int gx = refl(x0 - R + c, X);
+    // window rows and columns all inside the slice (the common case): no reflection, the row
+    // addresses step by 2 X from one base (the reflected index arithmetic was a third of the
+    // kernel's VALU issue, and the kernel is VALU-bound: 806 FP64 mul / add per wave and tile)
+    const bool interior = y0 - R >= 0 && y0 + kYxTY + R <= Y && x0 - R >= 0 && x0 - R + 128 <= X;
+    const int64_t ibase = sbase + (int64_t)(y0 - R + half) * X + (x0 - R + c);
+    const int64_t X2 = 2 * (int64_t)X;
+    auto gidx = [&](int i) -> int64_t {
+        return interior ? ibase + i * X2 : sbase + (int64_t)refl(y0 - R + 2 * i + half, Y) * X + gx;
+    };
     // ---- stage: NL rows per thread, all loads in flight
     if (hmap_src) {
         float mn, mx;
@@ -370,7 +380,7 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
         float vf[NL], vd[NL];
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
-            const int64_t gi = sbase + (int64_t)refl(y0 - R + 2 * i + half, Y) * X + gx;
+            const int64_t gi = gidx(i);
             vf[i] = gbl(in)[gi];
             vd[i] = gbl(dt)[gi];
         }
@@ -386,7 +396,7 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
     } else {
         float v[NL];
 #pragma unroll
-        for (int i = 0; i < NL; ++i) v[i] = gbl(in)[sbase + (int64_t)refl(y0 - R + 2 * i + half, Y) * X + gx];
+        for (int i = 0; i < NL; ++i) v[i] = gbl(in)[gidx(i)];
 #pragma unroll
         for (int i = 0; i < NL; ++i) win_s[(2 * i + half) * kYxP + c] = v[i];
     }
@@ -434,18 +444,16 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
             for (int m = 0; m <= 2 * R; ++m) sum += k[2 * R - m] * w[(i + m) % (2 * R + 1)];
             res[i] = (float)sum;
         }
-        __syncthreads();
+        // ---- stores straight from the registers: row p, columns [xs, xe) of the tile (the
+        // 8 runs of a row are written by 8 neighbouring lanes, so each row's lines fill within
+        // the wave's RUNX store instructions; no LDS round trip, no barriers, no division)
+        if (y0 + p < Y) {
+            gwptr_t<float> o = gblw(out) + sbase + (int64_t)(y0 + p) * X + x0 + xs;
+            const int n = min(xe, X - x0) - xs;
 #pragma unroll
-        for (int i = 0; i < RUNX; ++i)
-            if (xs + i < xe) win_s[p * kYxP + xs + i] = res[i];
-    }
-    __syncthreads();
-    // ---- coalesced stores of the valid part of the tile
-    const int ny = min(kYxTY, Y - y0), nx = min(TX, X - x0);
-    gwptr_t<float> o = gblw(out) + sbase + (int64_t)y0 * X + x0;
-    for (int v = tid; v < kYxTY * TX; v += 256) {
-        const int pp = v / TX, xx = v - pp * TX;
-        if (pp < ny && xx < nx) o[(int64_t)pp * X + xx] = win_s[pp * kYxP + xx];
+            for (int i = 0; i < RUNX; ++i)
+                if (i < n) o[i] = res[i];
+        }
     }
 }
 

@@ -112,6 +112,7 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
     // gridDim.x may be rounded up to a multiple of 8)
     const int t = blockIdx.x;
     if (t >= ntx * nty * ntz) return;
+    if (MODE == CC_PLATEAU && !a.ptile[B.ptbase + t]) return;  // no plateau voxel (k_localmax)
     const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
     const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
     // order key of tile position c: the C index (PLATEAU) or the vigra scan key (SEED, CROP)
@@ -289,6 +290,8 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
     // a workgroup walks several tiles (a face is only a few hundred voxels: one workgroup per
     // tile would make the dispatch of ~10^5 workgroups the cost)
     for (int t = blockIdx.x; t < ntx * nty * ntz; t += gridDim.x) {
+    // a face pair needs a plateau voxel on this tile's side: tiles without one are skipped
+    if (MODE == CC_PLATEAU && !a.ptile[B.ptbase + t]) continue;
     const int txi = t % ntx, tyi = (t / ntx) % nty, tzi = t / (ntx * nty);
     const int z0 = tzi * TZ, y0 = tyi * TY, x0 = txi * TX;
     uint32_t* P = Pg + (MODE == CC_CROP ? B.ibase : B.base);

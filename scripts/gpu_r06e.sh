@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 6: parity of every kernel change (crop x-face buffer, 8x8x64 3-D descent tiles, plateau
+# tile flags), same-box A/B vs the previous build, knob sweep, frontier statistics.
+cd "${GRAFT_REPO_ROOT:-.}"
+O=gpurun_out/r06e
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_config_blocks.py tests/test_corridor_gpu.py tests/test_from_seeds_gpu.py tests/test_gpu_pass2.py tests/test_golden_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; tail -1 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
+for c in 3 4 5; do
+  for k in 1 2; do
+    for v in new old; do
+      if [ $v = old ]; then export CTWS_LIB=$PWD/cluster_tools_amd/libctws_old.so; else unset CTWS_LIB; fi
+      timeout -k 10 200 python -u bench.py --config $c --streams 1 --steps 2 --warmup 1 --no-host --no-cpu-baseline --no-e2e --no-strong --no-threshcc --no-config5 > $O/c${c}_${v}_$k.json 2> $O/c${c}_${v}_$k.err || { tail -5 $O/c${c}_${v}_$k.err; exit 1; }
+      python3 -c "import json; d=json.loads(open('$O/c${c}_${v}_$k.json').read().strip().splitlines()[-1]); s=d['stage_ms_1stream']; print('c$c $v', d['ms_per_step'], {k: round(v, 2) for k, v in s.items() if k in ('descent_tile', 'flood_descent', 'flood_relax', 'crop_cc', 'seeds', 'edt_yz', 'smooth_seeds', 'hmap')})"
+    done
+  done
+done
+unset CTWS_LIB
+VARIANTS="base CTWS_GAUSS_YX_TY=16 CTWS_GAUSS_YX_TY=64 CTWS_EDT_U=16" CONFIGS="3 4" TAG=e bash scripts/gpu_r06_sweep.sh &&
+bash scripts/gpu_r06_fstats.sh
