@@ -575,9 +575,12 @@ def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req,
             return sl([beg[0] + g['g0']] + list(beg[1:]), [end[0] + g['g0']] + list(end[1:]))
         glist = sorted((b['block_id'], r, gsl(g, b['obeg'], b['oend']), gsl(g, b['beg'], b['end']))
                        for r, g in enumerate(geos) for b in g['blocks'] if b['block_id'] in writers)
-        lv, exch = sharded.pass2_rank_schedule([x[1:] for x in glist], slabs, cfg['halo'][0])
+        lv, exch, xboxes = sharded.pass2_rank_schedule([x[1:] for x in glist], slabs, cfg['halo'][0], boxes=True)
         level = {x[0]: l for x, l in zip(glist, lv)}
-        groups = [(0, p1, False)] + [(1, [b for b in p2 if level[b['block_id']] == k], exch[k])
+        # level 0: the whole halo rows (pass 1 wrote everywhere); later levels: only the (y, x)
+        # footprints of the blocks that wrote next to a slab boundary since
+        groups = [(0, p1, False)] + [(1, [b for b in p2 if level[b['block_id']] == k],
+                                      True if k == 0 else (xboxes[k] if exch[k] else False))
                                      for k in range(len(exch))]
     else:
         groups = [(0, list(blocks.values()), False)]
@@ -597,9 +600,13 @@ def run_workload(cfg_id, scaling, rank, world, dev, steps, warmup, nstreams_req,
         res = []
         for pid, gblocks, exch in groups:
             if pid == 1:
-                if exch:
+                if exch is True:
                     # the neighbour slabs' labels in the z halos (point-to-point)
                     sharded.exchange_z_halos(out_vol, geo['lo'], geo['hi'])
+                elif exch:
+                    sharded.exchange_z_halo_boxes(out_vol, geo['lo'], geo['hi'], exch.get((rank, 'lo'), []),
+                                                  exch.get((rank, 'hi'), []), exch.get((rank - 1, 'hi'), []),
+                                                  exch.get((rank + 1, 'lo'), []))
                 for b in gblocks:  # initial_seeds = ds_out[input_bb] (two_pass_watershed.py:228)
                     b['initial_seeds'].copy_(out_vol[b['osl']])
             if not gblocks:

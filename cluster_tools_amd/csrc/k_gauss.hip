@@ -358,14 +358,14 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
     const int64_t sbase = B.base + (int64_t)z * Y * X;
     const int gx = refl(x0 - R + c, X);
     // window rows and columns all inside the slice (the common case): no reflection, the row
-    // addresses step by 2 X from one base (the reflected index arithmetic was a third of the
-    // kernel's VALU issue, and the kernel is VALU-bound: 806 FP64 mul / add per wave and tile)
+    // addresses step by 2 X from one base (the kernel is VALU-bound: 806 FP64 mul / add per wave
+    // and tile, and the reflected index arithmetic of the staging adds ~10 instructions per load).
+    // A tile-uniform branch, so each path is one straight unrolled loop.
     const bool interior = y0 - R >= 0 && y0 + kYxTY + R <= Y && x0 - R >= 0 && x0 - R + 128 <= X;
     const int64_t ibase = sbase + (int64_t)(y0 - R + half) * X + (x0 - R + c);
     const int64_t X2 = 2 * (int64_t)X;
-    auto gidx = [&](int i) -> int64_t {
-        return interior ? ibase + i * X2 : sbase + (int64_t)refl(y0 - R + 2 * i + half, Y) * X + gx;
-    };
+    auto gidx_in = [&](int i) -> int64_t { return ibase + i * X2; };
+    auto gidx_refl = [&](int i) -> int64_t { return sbase + (int64_t)refl(y0 - R + 2 * i + half, Y) * X + gx; };
     // ---- stage: NL rows per thread, all loads in flight
     if (hmap_src) {
         float mn, mx;
@@ -378,12 +378,16 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
         }
         const float den = mx - mn;
         float vf[NL], vd[NL];
+        auto load2 = [&](auto gidx) {
 #pragma unroll
-        for (int i = 0; i < NL; ++i) {
-            const int64_t gi = gidx(i);
-            vf[i] = gbl(in)[gi];
-            vd[i] = gbl(dt)[gi];
-        }
+            for (int i = 0; i < NL; ++i) {
+                const int64_t gi = gidx(i);
+                vf[i] = gbl(in)[gi];
+                vd[i] = gbl(dt)[gi];
+            }
+        };
+        if (interior) load2(gidx_in);
+        else load2(gidx_refl);
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
             float d = vd[i] - mn;
@@ -395,8 +399,12 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
         }
     } else {
         float v[NL];
+        auto load1 = [&](auto gidx) {
 #pragma unroll
-        for (int i = 0; i < NL; ++i) v[i] = gbl(in)[gidx(i)];
+            for (int i = 0; i < NL; ++i) v[i] = gbl(in)[gidx(i)];
+        };
+        if (interior) load1(gidx_in);
+        else load1(gidx_refl);
 #pragma unroll
         for (int i = 0; i < NL; ++i) win_s[(2 * i + half) * kYxP + c] = v[i];
     }
@@ -444,16 +452,20 @@ __global__ void __launch_bounds__(256) k_gauss_yx(const BlockDesc* __restrict__ 
             for (int m = 0; m <= 2 * R; ++m) sum += k[2 * R - m] * w[(i + m) % (2 * R + 1)];
             res[i] = (float)sum;
         }
-        // ---- stores straight from the registers: row p, columns [xs, xe) of the tile (the
-        // 8 runs of a row are written by 8 neighbouring lanes, so each row's lines fill within
-        // the wave's RUNX store instructions; no LDS round trip, no barriers, no division)
-        if (y0 + p < Y) {
-            gwptr_t<float> o = gblw(out) + sbase + (int64_t)(y0 + p) * X + x0 + xs;
-            const int n = min(xe, X - x0) - xs;
+        __syncthreads();
 #pragma unroll
-            for (int i = 0; i < RUNX; ++i)
-                if (i < n) o[i] = res[i];
-        }
+        for (int i = 0; i < RUNX; ++i)
+            if (xs + i < xe) win_s[p * kYxP + xs + i] = res[i];
+    }
+    __syncthreads();
+    // ---- coalesced stores of the valid part of the tile (through LDS: storing each thread's
+    // run from its registers measured 3.7 -> 6.1 ms per call on config 3 -- 64 lanes 14.5
+    // voxels apart write partial lines)
+    const int ny = min(kYxTY, Y - y0), nx = min(TX, X - x0);
+    gwptr_t<float> o = gblw(out) + sbase + (int64_t)y0 * X + x0;
+    for (int v = tid; v < kYxTY * TX; v += 256) {
+        const int pp = v / TX, xx = v - pp * TX;
+        if (pp < ny && xx < nx) o[(int64_t)pp * X + xx] = win_s[pp * kYxP + xx];
     }
 }
 

@@ -164,12 +164,66 @@ def exchange_z_halos(vol, lo, hi):
     return vol
 
 
+def exchange_z_halo_boxes(vol, lo, hi, send_lo, send_hi, recv_lo, recv_hi):
+    """exchange_z_halos restricted to (y0, y1, x0, x1) boxes of the halo rows: the rank sends
+    its first lo own rows inside the `send_lo` boxes to rank - 1 and its last hi own rows inside
+    `send_hi` to rank + 1, and fills its lower / upper halo rows inside `recv_lo` / `recv_hi`
+    (the boxes the neighbour sends, in the same order).  Every rank derives the boxes from the
+    same schedule (pass2_rank_schedule), so sends and receives pair up; an empty list skips that
+    transfer on both sides.  Point-to-point, concatenated boxes per neighbour."""
+    dist = _dist()
+    if dist is None or dist.get_world_size() == 1:
+        return vol
+    rank, world = dist.get_rank(), dist.get_world_size()
+    Z = vol.shape[0] - lo - hi
+    host = comm_device(vol.device) is None and vol.device.type != 'cpu'
+
+    def pack(z0, z1, boxes):
+        parts = [vol[z0:z1, y0:y1, x0:x1].reshape(-1) for y0, y1, x0, x1 in boxes]
+        t = parts[0].new_empty(0) if not parts else (parts[0] if len(parts) == 1 else torch.cat(parts))
+        return t.cpu() if host else t.contiguous()
+
+    def nvals(n, boxes):
+        return n * sum((y1 - y0) * (x1 - x0) for y0, y1, x0, x1 in boxes)
+
+    def unpack(buf, z0, z1, boxes):
+        buf = buf.to(vol.device) if host else buf
+        o = 0
+        for y0, y1, x0, x1 in boxes:
+            m = (z1 - z0) * (y1 - y0) * (x1 - x0)
+            vol[z0:z1, y0:y1, x0:x1] = buf[o:o + m].view(z1 - z0, y1 - y0, x1 - x0)
+            o += m
+    import torch
+    ops, rl, rh = [], None, None
+    dev = 'cpu' if host else vol.device
+    if rank > 0 and lo:
+        if send_lo:
+            ops.append(dist.P2POp(dist.isend, pack(lo, 2 * lo, send_lo), rank - 1))
+        if recv_lo:
+            rl = torch.empty(nvals(lo, recv_lo), dtype=vol.dtype, device=dev)
+            ops.append(dist.P2POp(dist.irecv, rl, rank - 1))
+    if rank + 1 < world and hi:
+        if send_hi:
+            ops.append(dist.P2POp(dist.isend, pack(lo + Z - hi, lo + Z, send_hi), rank + 1))
+        if recv_hi:
+            rh = torch.empty(nvals(hi, recv_hi), dtype=vol.dtype, device=dev)
+            ops.append(dist.P2POp(dist.irecv, rh, rank + 1))
+    if ops:
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    if rl is not None:
+        unpack(rl, 0, lo, recv_lo)
+    if rh is not None:
+        unpack(rh, lo + Z, lo + Z + hi, recv_hi)
+    return vol
+
+
 def all_gather_ints(values, device=None):
     """Every rank's list of ints, concatenated in rank order."""
     return [int(v) for v in gather_counts(values, device=device)]
 
 
-def pass2_rank_schedule(p2_blocks, slabs, hz):
+def pass2_rank_schedule(p2_blocks, slabs, hz, boxes=False):
     """The two-pass watershed's sequential schedule over z-slab ranks.
 
     p2_blocks: the pass-2 blocks of the whole job that write something, in the sequential list
@@ -180,7 +234,10 @@ def pass2_rank_schedule(p2_blocks, slabs, hz):
     exchange[l] = whether the z-halo rows must be exchanged before level l: before level 0
     (the pass-1 labels) and after every level with a block whose output rows lie within hz of
     its slab's boundary to a neighbouring rank (another rank's halo reads them).  Every rank
-    computes the same schedule, so all of them exchange at the same levels."""
+    computes the same schedule, so all of them exchange at the same levels.
+    With boxes=True also returns, per level l >= 1, {(owner, 'lo' | 'hi'): [(y0, y1, x0, x1)]}:
+    the (y, x) footprints of the level-(l - 1) blocks each rank must send down ('lo', to
+    owner - 1) or up ('hi', to owner + 1) -- only those rows changed since the last exchange."""
     from cluster_tools_amd.watershed.watershed import pass2_levels
     levels = pass2_levels([(ib, ob) for _, ib, ob in p2_blocks])
     n_levels = max(levels) + 1 if levels else 0
@@ -188,10 +245,19 @@ def pass2_rank_schedule(p2_blocks, slabs, hz):
     if n_levels:
         exchange[0] = True
     world = len(slabs)
+    bx = [dict() for _ in range(n_levels)]
     for (r, _, ob), lv in zip(p2_blocks, levels):
         z0, z1 = slabs[r]
         b0, b1 = ob[0].start, ob[0].stop
-        near = (r > 0 and b0 < z0 + hz) or (r + 1 < world and b1 > z1 - hz)
-        if near and lv + 1 < n_levels:
+        dn = r > 0 and b0 < z0 + hz
+        up = r + 1 < world and b1 > z1 - hz
+        if (dn or up) and lv + 1 < n_levels:
             exchange[lv + 1] = True
+            fp = (ob[1].start, ob[1].stop, ob[2].start, ob[2].stop)
+            if dn:
+                bx[lv + 1].setdefault((r, 'lo'), []).append(fp)
+            if up:
+                bx[lv + 1].setdefault((r, 'hi'), []).append(fp)
+    if boxes:
+        return levels, exchange, bx
     return levels, exchange

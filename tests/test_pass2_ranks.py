@@ -54,7 +54,9 @@ def _sequential(shape, p1, p2):
     return vol
 
 
-def _sharded(shape, halo, slabs, owner, p1, p2, all_exchanges=True):
+def _sharded(shape, halo, slabs, owner, p1, p2, mode='boxes'):
+    """mode: 'boxes' (the bench: whole halo rows before level 0, then only the schedule's
+    footprints), 'full' (whole halo rows at every flagged level), 'once' (round 5)."""
     world = len(slabs)
     hz = halo[0]
     reg = [(max(0, z0 - hz), min(shape[0], z1 + hz)) for z0, z1 in slabs]
@@ -63,25 +65,30 @@ def _sharded(shape, halo, slabs, owner, p1, p2, all_exchanges=True):
     def local(r, beg, end):
         return _sl([beg[0] - reg[r][0]] + list(beg[1:]), [end[0] - reg[r][0]] + list(end[1:]))
 
-    def exchange():
-        # every rank's own rows next to a boundary into its neighbours' halo rows
+    def exchange(boxes=None):
+        # every rank's own rows next to a boundary into its neighbours' halo rows (boxes: only
+        # the (y, x) footprints the schedule lists per sender and direction)
         for r in range(world):
             z0, z1 = slabs[r]
-            for n in (r - 1, r + 1):
+            for n, side in ((r - 1, 'lo'), (r + 1, 'hi')):
                 if 0 <= n < world:
                     a, b = max(z0, reg[n][0]), min(z1, reg[n][1])
-                    if a < b:
-                        loc[n][a - reg[n][0]:b - reg[n][0]] = loc[r][a - reg[r][0]:b - reg[r][0]]
+                    if a >= b:
+                        continue
+                    fps = [(0, shape[1], 0, shape[2])] if boxes is None else boxes.get((r, side), [])
+                    for y0, y1, x0, x1 in fps:
+                        loc[n][a - reg[n][0]:b - reg[n][0], y0:y1, x0:x1] = \
+                            loc[r][a - reg[r][0]:b - reg[r][0], y0:y1, x0:x1]
     for b in p1:
         r = owner(b)
         loc[r][local(r, b['beg'], b['end'])] = b['block_id'] + 1
     glist = [(owner(b), _sl(b['obeg'], b['oend']), _sl(b['beg'], b['end'])) for b in p2]
-    levels, exch = pass2_rank_schedule(glist, slabs, hz)
-    if not all_exchanges:
+    levels, exch, boxes = pass2_rank_schedule(glist, slabs, hz, boxes=True)
+    if mode == 'once':
         exch = [k == 0 for k in range(len(exch))]
     for lv in range(len(exch)):
         if exch[lv]:
-            exchange()
+            exchange(boxes[lv] if mode == 'boxes' and lv > 0 else None)
         todo = [b for b, l in zip(p2, levels) if l == lv]
         vals = [_value(loc[owner(b)][local(owner(b), b['obeg'], b['oend'])], b['block_id']) for b in todo]
         for b, v in zip(todo, vals):
@@ -93,15 +100,16 @@ def _sharded(shape, halo, slabs, owner, p1, p2, all_exchanges=True):
     return vol, exch
 
 
+@pytest.mark.parametrize('mode', ['boxes', 'full'])
 @pytest.mark.parametrize('world', [1, 2, 3, 4])
 @pytest.mark.parametrize('geom', [((64, 32, 32), (8, 16, 16), (2, 4, 4)),
                                   ((96, 48, 40), (16, 16, 16), (8, 8, 8)),
                                   ((64, 64, 64), (8, 32, 32), (4, 8, 8))])
-def test_rank_schedule_is_sequential(world, geom):
+def test_rank_schedule_is_sequential(world, geom, mode):
     shape, bs, halo = geom
     _, slabs, owner, p1, p2 = _setup(shape, bs, halo, world)
     ref = _sequential(shape, p1, p2)
-    got, exch = _sharded(shape, halo, slabs, owner, p1, p2)
+    got, exch = _sharded(shape, halo, slabs, owner, p1, p2, mode)
     np.testing.assert_array_equal(got, ref)
     if world == 1:
         assert sum(exch) == 1  # only the pass-1 labels
@@ -113,5 +121,5 @@ def test_single_exchange_is_not_sequential():
     shape, bs, halo = (64, 32, 32), (8, 16, 16), (2, 4, 4)
     _, slabs, owner, p1, p2 = _setup(shape, bs, halo, 2)
     ref = _sequential(shape, p1, p2)
-    got, exch = _sharded(shape, halo, slabs, owner, p1, p2, all_exchanges=False)
+    got, exch = _sharded(shape, halo, slabs, owner, p1, p2, 'once')
     assert sum(exch) == 1 and not np.array_equal(got, ref)

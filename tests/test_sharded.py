@@ -141,3 +141,42 @@ def test_strong_scaling_partition(cfg_id, world):
             assert geo['lo'] <= b['beg'][0] < geo['gshape'][0] - geo['hi']
         seen += [b['block_id'] for b in geo['blocks']]
     assert sorted(seen) == sorted(every)
+
+
+def _boxes_worker(rank, world, port, outdir):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        hz, Z = 2, 5
+        vol = torch.full((Z + 2 * hz, 6, 8), -1, dtype=torch.int64)
+        for z in range(Z):
+            vol[hz + z] = (100 * rank + z) * 1000 + torch.arange(48).view(6, 8)
+        # every rank sends box A down and box B up; receives the neighbours' opposite boxes
+        a, b = [(0, 2, 1, 4)], [(3, 6, 0, 2), (1, 2, 6, 8)]
+        sharded.exchange_z_halo_boxes(vol, hz, hz, a, b, b, a)
+        np.save(os.path.join(outdir, 'boxes_%d.npy' % rank), vol.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_gloo_halo_exchange_boxes(tmp_path):
+    """exchange_z_halo_boxes (the bench's two-pass levels after the first): only the listed
+    (y, x) boxes of the halo rows change, with the neighbour's own rows there."""
+    world, hz, Z = 3, 2, 5
+    tmp.spawn(_boxes_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    own = lambda r, z: ((100 * r + z) * 1000 + np.arange(48).reshape(6, 8))  # noqa: E731
+    for r in range(world):
+        v = np.load(os.path.join(str(tmp_path), 'boxes_%d.npy' % r))
+        exp = np.full(v.shape, -1, np.int64)
+        for z in range(Z):
+            exp[hz + z] = own(r, z)
+        if r > 0:   # lower halo: rank r-1's last hz own rows, in the boxes r-1 sends up
+            for y0, y1, x0, x1 in [(3, 6, 0, 2), (1, 2, 6, 8)]:
+                for k in range(hz):
+                    exp[k, y0:y1, x0:x1] = own(r - 1, Z - hz + k)[y0:y1, x0:x1]
+        if r + 1 < world:   # upper halo: rank r+1's first hz own rows, in the box it sends down
+            for y0, y1, x0, x1 in [(0, 2, 1, 4)]:
+                for k in range(hz):
+                    exp[hz + Z + k, y0:y1, x0:x1] = own(r + 1, k)[y0:y1, x0:x1]
+        np.testing.assert_array_equal(v, exp)
