@@ -137,6 +137,7 @@ struct ctws_handle {
     // run_batch is re-running blocks whose packed flood reported a saturated d (dsat)
     int force_wide = 0;
     int wide_rerun = 0;
+    int sf_sparse = 1;  // CTWS_SF_SPARSE=0: the size filter's regrow initialisation scans every block
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
     int plateau_fill = 1;  // CTWS_PLATEAU_FILL=0: masked blocks' plateaus relaxed hop by hop (k_plateau.hip)
@@ -668,7 +669,7 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 // it has not converged after frontier_max_iters iterations (very long equal-height paths) the
 // tile flood finishes from the current keys.
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
-                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out) {
+                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out, bool regrow = false) {
     Workspace& w = h->ws;
     const int64_t nch = (TF >> kChunkShift) + 1;
     uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
@@ -751,6 +752,9 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
         HIPCHK(hipMemsetAsync(w.act0, 0, sizeof(uint32_t) * (size_t)TT, h->stream));
         k_frontier_tiles<<<dim3((unsigned)std::min<int64_t>((TF / nb + 255) / 256 + 1, 4096), nb), 256, 0,
                            h->stream>>>(w.desc, w.stat, w.fopen, w.act0, TZ, TY, TX);
+        // a sparse regrow (k_sf_sparse) left the survivors' seed flags as the first flood had
+        // them: the tile flood needs every survivor fixed
+        if (regrow) k_fixed_from_open<<<dim3(2048, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.fopen, w.cls);
         LAUNCHCHK();
         int rounds = 0;
         float kms = 0.f;
@@ -1283,7 +1287,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
-    k_root_label<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.Wp);
+    // (pass 1: the roots' positions per label for the sparse size filter, in w.Bf -- free after
+    // the hmap; pass 2 relabels the seeds, so its size filter scans)
+    k_root_label<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.Wp, pl.pass2 ? nullptr : (uint32_t*)w.Bf);
     if (pl.pass2) {
         // _apply_watershed_with_seeds: shifted seeds + initial seeds, relabelConsecutive
         // the slices' seed bases of the seed CC into w.soff (free until k_slice_offsets): the
@@ -1515,8 +1521,21 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (packed) {
             // survivors -> regrow seeds, removed voxels -> open; then the frontier relaxation
             std::vector<BlockStat> s3(nb);
+            // pass 1 with a small size filter: the removed segments walked from their seeds
+            // (k_sf_plan decides per block; CTWS_SF_SPARSE=0 scans every block)
+            const bool sparse_ok = h->sf_sparse && !pl.pass2 && !pl.from_seeds && cfg->size_filter <= 64;
             auto regrow_init = [&]() -> int {
                 HIPCHK(hipMemsetAsync(w.surv, 0, sizeof(uint32_t) * TS, h->stream));
+                if (sparse_ok) {
+                    k_sf_plan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts, w.sb,
+                                                         w.surv);
+                    HIPCHK(hipMemsetAsync(w.fopen, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+                    HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
+                    k_sf_sparse<<<dim3((unsigned)std::max<uint32_t>((max_seeds + 255) / 256, 1u), nb), 256, 0,
+                                   h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts,
+                                                (const uint32_t*)w.Bf, w.hm, w.key, w.cls, w.fopen, w.front0);
+                    LAUNCHCHK();
+                }
                 // 4 words per wave step (8: +1.2 ms on config 3, +2.2 ms on config 4)
                 k_regrow_init<4><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts,
                                                             excl, w.hm, w.key, w.cls, w.fopen, w.front0, w.surv);
@@ -1547,7 +1566,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                                                            w.cls, w.fopen, w.front0, nullptr);
                 LAUNCHCHK();
             }
-            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2)) !=
+            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2, true)) !=
                 CTWS_OK)
                 return r;
             if (h->verify) {
@@ -1676,7 +1695,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_bitmap_csum<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum);
             k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.csum, 1);
             k_word_prefix<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.W, w.csum, w.Wp);
-            k_root_label<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp);
+            k_root_label<<<wgi, 256, 0, h->stream>>>(w.desc, w.stat, 1, w.PF, w.W, w.Wp, nullptr);
             LAUNCHCHK();
         }
         mark("crop_cc");
@@ -2354,6 +2373,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_NO_DESCENT")) h->no_descent = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FORCE_WIDE")) h->force_wide = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_SF_SPARSE")) h->sf_sparse = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))

@@ -61,7 +61,9 @@ struct BlockStat {
     uint32_t n_auto;          // auto-seeded regrow: strict hmap minima of the seedless slices
     uint32_t _p[4];
     uint32_t dsat;            // packed flood: a key's hop distance d reached kDMax (note_dsat)
-    uint32_t _q[3];
+    uint32_t unreached;       // 2-D size filter: voxels the flood did not reach (k_hist2d)
+    uint32_t sf_sparse;       // size filter: the removed segments are walked, not scanned (k_sf_plan)
+    uint32_t _q;
 };
 
 // BlockStat::err bits (a failed block does not fail its batch; the caller sees the status)

@@ -104,7 +104,8 @@ __global__ void k_plat_restore(const BlockDesc*, const BlockStat*, uint64_t*, co
 __global__ void k_bitmap_csum(const BlockDesc*, const BlockStat*, int, const uint64_t*, uint32_t*);
 __global__ void k_chunk_scan(const BlockDesc*, BlockStat*, int, uint32_t*, int);
 __global__ void k_word_prefix(const BlockDesc*, const BlockStat*, int, const uint64_t*, const uint32_t*, uint32_t*);
-__global__ void k_root_label(const BlockDesc*, const BlockStat*, int, uint32_t*, const uint64_t*, const uint32_t*);
+__global__ void k_root_label(const BlockDesc*, const BlockStat*, int, uint32_t*, const uint64_t*, const uint32_t*,
+                             uint32_t*);
 __global__ void k_seed_label(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const float*,
                              uint32_t*, uint64_t*, uint8_t*, int);
 __global__ void k_output(const BlockDesc*, BlockStat*, const uint32_t*, const uint64_t*, int, const uint32_t*,
@@ -224,6 +225,10 @@ __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*,
 template <int PACKED>
 __global__ void k_hist2d(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
                          uint32_t*, int);
+__global__ void k_sf_plan(const BlockDesc*, BlockStat*, uint32_t, const uint32_t*, const uint32_t*, uint32_t*);
+__global__ void k_sf_sparse(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*, const uint32_t*, const float*,
+                            uint64_t*, uint8_t*, uint64_t*, uint64_t*);
+__global__ void k_fixed_from_open(const BlockDesc*, const BlockStat*, const uint64_t*, uint8_t*);
 template <int U>
 __global__ void k_regrow_init(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*, const uint8_t*,
                               const float*, uint64_t*, uint8_t*, uint64_t*, uint64_t*, uint32_t*);

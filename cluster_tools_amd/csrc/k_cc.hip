@@ -308,9 +308,11 @@ __global__ void __launch_bounds__(256) k_word_prefix(const BlockDesc* __restrict
 
 // roots: slot <- (1 + rank of the root's scan key) | kRootBit, walking the set bits of the
 // root bitmap (roots are few: no pass over the voxels)
+// rootpos (seed CC, nullable): rootpos[base + label] = the root's block C index (the sparse
+// size-filter initialisation starts its walk over a small segment there: a seed keeps its label)
 __global__ void __launch_bounds__(256) k_root_label(const BlockDesc* __restrict__ D, const BlockStat* S, int inner,
                                                     uint32_t* __restrict__ PFg, const uint64_t* __restrict__ Wg,
-                                                    const uint32_t* __restrict__ Wpg) {
+                                                    const uint32_t* __restrict__ Wpg, uint32_t* __restrict__ rootpos) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || (inner && !B.crop)) return;
     uint32_t* P = PFg + (inner ? B.ibase : B.base);
@@ -337,7 +339,9 @@ __global__ void __launch_bounds__(256) k_root_label(const BlockDesc* __restrict_
                 y = (int)(rem % ny);
                 x = (int)(rem / ny);
             }
-            P[((int64_t)z * ny + y) * nx + x] = (++rank) | kRootBit;
+            const int64_t ci = ((int64_t)z * ny + y) * nx + x;
+            P[ci] = (++rank) | kRootBit;
+            if (rootpos) rootpos[B.base + rank] = (uint32_t)ci;
         }
     }
 }

@@ -132,6 +132,7 @@ __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D,
     const int64_t i0 = (int64_t)z * YX + YX * s / splits, i1 = (int64_t)z * YX + YX * (s + 1) / splits;
     uint32_t* c = counts + B.base + b0 + 1;
     const int lane = threadIdx.x & 63;
+    uint32_t nzero = 0;
     constexpr int U = 8;
     for (int64_t ib = i0; ib < i1; ib += 256 * U) {
         uint32_t lv[U];
@@ -149,23 +150,149 @@ __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t i = ib + u * 256 + threadIdx.x;
-            lv[u] = (i < i1 && !(lv[u] & 0x80000000u)) ? lv[u] : 0u;
+            lv[u] = i < i1 ? ((lv[u] & 0x80000000u) ? 0u : lv[u]) : 0xFFFFFFFFu;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t l = lv[u];
-            // 0 (unreached) is not counted: a run of its own, dropped
+            // 0 (unreached) is not counted, only tallied for the size filter's plan (k_sf_plan)
             count_label_runs(l, l != 0xFFFFFFFFu, lane, [&](uint32_t lb, uint32_t n) {
+                if (lb == 0) {
+                    nzero += n;
+                    return;
+                }
                 if (lb <= b0 || lb > b1) return;
                 if (use_lds) atomicAdd(&sh[lb - b0 - 1], n);
                 else atomicAdd(&c[lb - b0 - 1], n);
             });
         }
     }
+    nzero = wg_reduce_u32(nzero, OpAdd());
+    if (threadIdx.x == 0 && nzero) atomicAdd(const_cast<uint32_t*>(&S[blockIdx.y].unreached), nzero);
     if (!use_lds) return;
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += 256)
         if (sh[j]) atomicAdd(&c[j], sh[j]);
+}
+
+// ---- sparse size-filter initialisation ---------------------------------------------------
+// With a small size filter the removed segments are a few voxels each, yet k_regrow_init reads
+// every voxel's key and seed flag.  A watershed segment is connected and contains its seed (the
+// seed CC root of its label keeps it), so each removed segment can be walked from its seed
+// instead: k_sf_plan decides per block (pass 1, packed keys: labels are seed CC ranks whose roots
+// k_root_label recorded), k_sf_sparse walks each removed segment, and k_regrow_init skips the
+// sparse blocks.  The walk writes what k_regrow_init would write where the regrow reads it: the
+// removed voxels' keys (INF), seed flags and open bits, and the surviving neighbours' changed bits
+// and seed keys (h, 0, label) -- survivors elsewhere are never read by the regrow.
+constexpr uint32_t kSfSparseMax = 64;  // the largest size filter walked (a segment below it fits the queue)
+
+__global__ void __launch_bounds__(256) k_sf_plan(const BlockDesc* __restrict__ D, BlockStat* S, uint32_t size_filter,
+                                                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ sb,
+                                                 uint32_t* __restrict__ survivors) {
+    const BlockDesc& B = D[blockIdx.x];
+    BlockStat& st = S[blockIdx.x];
+    if (!st.active) return;
+    const uint32_t ns = st.n_seeds;
+    const uint32_t* c = counts + B.base;
+    uint32_t nsmall = 0;
+    for (uint32_t l = 1 + threadIdx.x; l <= ns; l += 256) nsmall += c[l] < size_filter ? 1u : 0u;
+    nsmall = wg_reduce_u32(nsmall, OpAdd());
+    // every slice (2-D) / the block (3-D) keeps a segment: no auto-seeded regrow
+    uint32_t bare = 0;
+    if (B.nd_ws == 2) {
+        for (int z = threadIdx.x; z < B.Z; z += 256) {
+            const uint32_t l0 = sb[B.sbase + z], l1 = z + 1 < B.Z ? sb[B.sbase + z + 1] : ns;
+            bool any = false;
+            for (uint32_t l = l0 + 1; l <= l1 && !any; ++l) any = c[l] >= size_filter;
+            bare += any ? 0u : 1u;
+        }
+    } else {
+        bare = threadIdx.x == 0 && nsmall == ns ? 1u : 0u;
+    }
+    bare = wg_reduce_u32(bare, OpAdd());
+    const uint32_t unreached = B.nd_ws == 2 ? st.unreached : c[0];
+    const bool sparse = size_filter <= kSfSparseMax && !unreached && !bare &&
+                        (uint64_t)nsmall * size_filter <= (uint64_t)B.N / 8;
+    if (threadIdx.x == 0) st.sf_sparse = sparse ? 1u : 0u;
+    if (sparse)
+        for (int z = threadIdx.x; z < (B.nd_ws == 2 ? B.Z : 1); z += 256) survivors[B.sbase + z] = 1u;
+}
+
+// one thread per label of the block: a removed segment (count < size_filter) is walked from its
+// seed (breadth first, in-plane 4-neighbourhood in 2-D ws mode, 6 in 3-D)
+__global__ void __launch_bounds__(256) k_sf_sparse(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                   uint32_t size_filter, const uint32_t* __restrict__ counts,
+                                                   const uint32_t* __restrict__ rootpos, const float* __restrict__ h,
+                                                   uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
+                                                   uint64_t* __restrict__ open, uint64_t* __restrict__ chg) {
+    const BlockDesc& B = D[blockIdx.y];
+    const BlockStat& st = S[blockIdx.y];
+    if (!st.active || !st.sf_sparse) return;
+    const uint32_t l = 1u + blockIdx.x * blockDim.x + threadIdx.x;
+    if (l > st.n_seeds) return;
+    const uint32_t* c = counts + B.base;
+    if (c[l] >= size_filter) return;
+    uint64_t* kb = key + B.base;
+    const int wpr = (B.X + 63) >> 6;
+    const int64_t YX = (int64_t)B.Y * B.X;
+    auto setbit = [&](uint64_t* bm, int64_t i) {
+        const int64_t row = i / B.X;
+        const int x = (int)(i - row * B.X);
+        atomicOr((unsigned long long*)&bm[B.fbase + row * wpr + (x >> 6)], 1ull << (x & 63));
+    };
+    uint32_t q[kSfSparseMax];
+    int qh = 0, qt = 0;
+    auto claim = [&](int64_t i) {
+        kb[i] = kPackInf;
+        fixedv[B.base + i] = 0;
+        setbit(open, i);
+        q[qt++] = (uint32_t)i;
+    };
+    claim((int64_t)rootpos[B.base + l]);
+    while (qh < qt) {
+        const int64_t v = q[qh++];
+        const int z = (int)(v / YX);
+        const int64_t r = v - (int64_t)z * YX;
+        const int y = (int)(r / B.X), x = (int)(r - (int64_t)y * B.X);
+        int64_t nbr[6];
+        int nn = 0;
+        if (x > 0) nbr[nn++] = v - 1;
+        if (x + 1 < B.X) nbr[nn++] = v + 1;
+        if (y > 0) nbr[nn++] = v - B.X;
+        if (y + 1 < B.Y) nbr[nn++] = v + B.X;
+        if (B.nd_ws == 3) {
+            if (z > 0) nbr[nn++] = v - YX;
+            if (z + 1 < B.Z) nbr[nn++] = v + YX;
+        }
+        for (int k = 0; k < nn; ++k) {
+            const int64_t u = nbr[k];
+            const uint64_t ku = kb[u];
+            if (ku == kPackInf) continue;  // removed already (this segment or another)
+            const uint32_t lu = (uint32_t)(ku & kLabelMask);
+            if (lu == l) {
+                if (qt < (int)kSfSparseMax) claim(u);
+                continue;
+            }
+            if (c[lu] < size_filter) continue;  // another removed segment (its own thread)
+            // a survivor next to the removed segment: a regrow seed, read by the frontier
+            setbit(chg, u);
+            if (ku & kDMask) {
+                kb[u] = ((uint64_t)ordf(h[B.base + u]) << 32) | (uint64_t)lu;
+                fixedv[B.base + u] = 1;
+            }
+        }
+    }
+}
+
+// seed flags from the open bitmap (the fallback tile flood of a sparse regrow: every voxel that
+// is not open is a survivor, a seed of the regrow)
+__global__ void __launch_bounds__(256) k_fixed_from_open(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                         const uint64_t* __restrict__ open, uint8_t* __restrict__ fixedv) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active || !S[blockIdx.y].sf_sparse) return;
+    WORD_TILES(B.Z, B.Y, B.X, {
+        if (valid) fixedv[B.base + i] = ((open[B.fbase + w_] >> lane) & 1ull) ? 0 : 1;
+    })
 }
 
 // Size filter + regrow initialisation for the frontier relaxation (packed keys).  The regrow
@@ -182,7 +309,7 @@ __global__ void __launch_bounds__(256) k_regrow_init(const BlockDesc* __restrict
                                                      uint64_t* __restrict__ open, uint64_t* __restrict__ chg,
                                                      uint32_t* __restrict__ survivors) {
     const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
+    if (!S[blockIdx.y].active || S[blockIdx.y].sf_sparse) return;  // (walked by k_sf_sparse)
     constexpr uint64_t kLab = (1ull << 20) - 1ull;
     // word tiles (a wave's ballot is exactly one word of the open / changed bitmaps), U words per
     // step: the loads of the U words, then their dependent count loads, in flight together

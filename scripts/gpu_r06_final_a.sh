@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 6 final (1/2): the whole GPU suite as the driver runs it, smoke(), then the default bench line.
+cd "${GRAFT_REPO_ROOT:-.}"
+O=gpurun_out/r06_final
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+tail -1 $O/bench.json | cut -c1-600

@@ -30,6 +30,9 @@ VARIANTS = {
     # every flood on the wide keys (k_flood, labels apart, 32-bit d): the path run_batch re-runs a
     # block on when its packed flood saturated d (tests/test_corridor_gpu.py)
     'wide_keys': {'CTWS_FORCE_WIDE': '1'},
+    # the size filter's regrow initialised by the scan of every voxel instead of the walk over
+    # the removed segments (k_sf_sparse, the default for pass 1 with size_filter <= 64)
+    'sf_scan': {'CTWS_SF_SPARSE': '0'},
 }
 
 
