@@ -119,6 +119,7 @@ struct ctws_handle {
     DevBuf edt_fh;
     DevBuf xface;  // crop CC: the tiles' x columns (CcArgs::xface)
     DevBuf ptile;  // plateau CC: per-tile plateau flags (CcArgs::ptile)
+    DevBuf ctrue;  // experiment (CTWS_CTRUE_EXP): final C per voxel
     DevBuf edt_scratch;  // k_edt_real_line: per-thread parabola stacks
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
@@ -137,6 +138,7 @@ struct ctws_handle {
     // run_batch is re-running blocks whose packed flood reported a saturated d (dsat)
     int force_wide = 0;
     int wide_rerun = 0;
+    int ctrue_exp = 0;  // CTWS_CTRUE_EXP=1 (with CTWS_TRACE): re-run the frontier filtered by the final C
     int sf_sparse = 1;  // CTWS_SF_SPARSE=0: the size filter's regrow initialisation scans every block
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
@@ -669,7 +671,8 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 // it has not converged after frontier_max_iters iterations (very long equal-height paths) the
 // tile flood finishes from the current keys.
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
-                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out, bool regrow = false) {
+                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out, bool regrow = false,
+                 const uint32_t* ctrue = nullptr) {
     Workspace& w = h->ws;
     const int64_t nch = (TF >> kChunkShift) + 1;
     uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
@@ -714,7 +717,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
             w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
             fst ? fst + 2 * nb : nullptr,                                                                             \
-            h->frontier_reps, h->frontier_dir);                                                                     \
+            h->frontier_reps, h->frontier_dir, ctrue);                                                              \
         break;
             switch (fkind) {
                 CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
@@ -1288,7 +1291,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
     k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
     // (pass 1: the roots' positions per label for the sparse size filter, in w.Bf -- free after
-    // the hmap; pass 2 relabels the seeds, so its size filter scans)
+    // the hmap; pass 2 relabels the seeds and records its ids' first positions below)
     k_root_label<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.PF, w.W, w.Wp, pl.pass2 ? nullptr : (uint32_t*)w.Bf);
     if (pl.pass2) {
         // _apply_watershed_with_seeds: shifted seeds + initial seeds, relabelConsecutive
@@ -1306,6 +1309,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         k_bitmap_csum<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum);
         k_chunk_scan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.csum, 0);
         k_word_prefix<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, w.W, w.csum, w.Wp);
+        // the first position of each new id (a seed: it keeps the id) for the sparse size
+        // filter, in w.dt (free after the seed CC)
+        k_root_label<<<wg, 256, 0, h->stream>>>(w.desc, w.stat, 0, nullptr, w.W, w.Wp, (uint32_t*)w.dt);
         LAUNCHCHK();
     }
     }  // !from_seeds
@@ -1415,6 +1421,45 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 return r;
         }
         mark("flood_relax");
+        if (fst && h->ctrue_exp && !plat_fill) {
+            // experiment: the frontier again from the descent, each write filtered by the final C
+            std::vector<uint32_t> hs(3 * (size_t)nb);
+            HIPCHK(hipMemcpyAsync(hs.data(), fst, sizeof(uint32_t) * 3 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
+            if ((r = grow(h, h->ctrue, sizeof(uint32_t) * (size_t)T)) != CTWS_OK) return r;
+            k_ctrue_copy<<<dim3(4096, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.key, (uint32_t*)h->ctrue.p);
+            HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 3 * (size_t)nb, h->stream));
+            k_descent_init<8><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
+                                                         w.front0, fst, nullptr);
+            hipEvent_t e0, e1;
+            hipEventCreate(&e0);
+            hipEventCreate(&e1);
+            hipEventRecord(e0, h->stream);
+            int it2 = 0;
+            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &it2, &rounds1, &fk1, false,
+                                  (const uint32_t*)h->ctrue.p)) != CTWS_OK)
+                return r;
+            hipEventRecord(e1, h->stream);
+            std::vector<uint32_t> hs2(3 * (size_t)nb);
+            HIPCHK(hipMemcpyAsync(hs2.data(), fst, sizeof(uint32_t) * 3 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            float ms = 0.f;
+            hipEventElapsedTime(&ms, e0, e1);
+            hipEventDestroy(e0);
+            hipEventDestroy(e1);
+            double v1 = 0, c1 = 0, v2 = 0, c2 = 0;
+            for (int i = 0; i < nb; ++i) {
+                v1 += hs[nb + i];
+                c1 += hs[2 * nb + i];
+                v2 += hs2[nb + i];
+                c2 += hs2[2 * nb + i];
+            }
+            add_timing(h, "exp_ctrue_ms", ms);
+            add_timing(h, "exp_ctrue_iters", (float)it2);
+            add_timing(h, "exp_ctrue_visits", (float)v2);
+            add_timing(h, "exp_ctrue_writes", (float)c2);
+            std::fprintf(stderr, "[ctws] ctrue exp: visits %.0f -> %.0f, writes %.0f -> %.0f, %d iters, %.3f ms\n", v1,
+                         v2, c1, c2, it2, ms);
+        }
         if (fst) {
             std::vector<uint32_t> hs(3 * (size_t)nb);
             HIPCHK(hipMemcpyAsync(hs.data(), fst, sizeof(uint32_t) * 3 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
@@ -1521,19 +1566,21 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         if (packed) {
             // survivors -> regrow seeds, removed voxels -> open; then the frontier relaxation
             std::vector<BlockStat> s3(nb);
-            // pass 1 with a small size filter: the removed segments walked from their seeds
-            // (k_sf_plan decides per block; CTWS_SF_SPARSE=0 scans every block)
-            const bool sparse_ok = h->sf_sparse && !pl.pass2 && !pl.from_seeds && cfg->size_filter <= 64;
+            // a small size filter: the removed segments walked from their seeds (k_sf_plan decides
+            // per block; CTWS_SF_SPARSE=0 scans every block).  WatershedFromSeeds numbers its
+            // labels by seed value, without first positions: it scans
+            const bool sparse_ok = h->sf_sparse && !pl.from_seeds && cfg->size_filter <= 64;
+            const uint32_t* rootpos = pl.pass2 ? (const uint32_t*)w.dt : (const uint32_t*)w.Bf;
             auto regrow_init = [&]() -> int {
                 HIPCHK(hipMemsetAsync(w.surv, 0, sizeof(uint32_t) * TS, h->stream));
                 if (sparse_ok) {
-                    k_sf_plan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts, w.sb,
-                                                         w.surv);
+                    k_sf_plan<<<nb, 256, 0, h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts, excl,
+                                                         w.sb, w.surv);
                     HIPCHK(hipMemsetAsync(w.fopen, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
                     HIPCHK(hipMemsetAsync(w.front0, 0, sizeof(uint64_t) * (size_t)TF, h->stream));
                     k_sf_sparse<<<dim3((unsigned)std::max<uint32_t>((max_seeds + 255) / 256, 1u), nb), 256, 0,
-                                   h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts,
-                                                (const uint32_t*)w.Bf, w.hm, w.key, w.cls, w.fopen, w.front0);
+                                   h->stream>>>(w.desc, w.stat, (uint32_t)cfg->size_filter, counts, excl,
+                                                rootpos, w.hm, w.key, w.cls, w.fopen, w.front0);
                     LAUNCHCHK();
                 }
                 // 4 words per wave step (8: +1.2 ms on config 3, +2.2 ms on config 4)
@@ -2374,6 +2421,7 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FORCE_WIDE")) h->force_wide = std::atoi(t);
     if (const char* t = std::getenv("CTWS_SF_SPARSE")) h->sf_sparse = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_CTRUE_EXP")) h->ctrue_exp = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))

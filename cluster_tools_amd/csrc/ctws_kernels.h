@@ -177,7 +177,9 @@ __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*,
 template <int ND, int CW, int CY, int CZ>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
-                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int);
+                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int,
+                           const uint32_t*);
+__global__ void k_ctrue_copy(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
 // k_eval.hip (VI / Rand contingency table)
 __global__ void k_eval_add(const uint64_t*, const uint64_t*, int64_t, int, uint64_t*, unsigned long long*, int64_t,
                            uint64_t*, unsigned long long*, int64_t, uint64_t*, unsigned long long*, int64_t,
@@ -225,9 +227,10 @@ __global__ void k_slice_max(const BlockDesc*, const BlockStat*, const uint32_t*,
 template <int PACKED>
 __global__ void k_hist2d(const BlockDesc*, const BlockStat*, const uint32_t*, const uint64_t*, const uint32_t*,
                          uint32_t*, int);
-__global__ void k_sf_plan(const BlockDesc*, BlockStat*, uint32_t, const uint32_t*, const uint32_t*, uint32_t*);
-__global__ void k_sf_sparse(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*, const uint32_t*, const float*,
-                            uint64_t*, uint8_t*, uint64_t*, uint64_t*);
+__global__ void k_sf_plan(const BlockDesc*, BlockStat*, uint32_t, const uint32_t*, const uint8_t*, const uint32_t*,
+                          uint32_t*);
+__global__ void k_sf_sparse(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*, const uint8_t*,
+                            const uint32_t*, const float*, uint64_t*, uint8_t*, uint64_t*, uint64_t*);
 __global__ void k_fixed_from_open(const BlockDesc*, const BlockStat*, const uint64_t*, uint8_t*);
 template <int U>
 __global__ void k_regrow_init(const BlockDesc*, const BlockStat*, uint32_t, const uint32_t*, const uint8_t*,

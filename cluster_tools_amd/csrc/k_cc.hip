@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(256) k_root_label(const BlockDesc* __restrict_
                                                     const uint32_t* __restrict__ Wpg, uint32_t* __restrict__ rootpos) {
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active || (inner && !B.crop)) return;
-    uint32_t* P = PFg + (inner ? B.ibase : B.base);
+    uint32_t* P = PFg ? PFg + (inner ? B.ibase : B.base) : nullptr;  // null: rootpos only (pass 2)
     const int64_t n = inner ? B.NI : B.N;
     const int64_t nw = n / 64 + 1;
     const int nz = inner ? B.IZ : B.Z, ny = inner ? B.IY : B.Y, nx = inner ? B.IX : B.X;
@@ -340,7 +340,8 @@ __global__ void __launch_bounds__(256) k_root_label(const BlockDesc* __restrict_
                 x = (int)(rem / ny);
             }
             const int64_t ci = ((int64_t)z * ny + y) * nx + x;
-            P[ci] = (++rank) | kRootBit;
+            ++rank;
+            if (P) P[ci] = rank | kRootBit;
             if (rootpos) rootpos[B.base + rank] = (uint32_t)ci;
         }
     }

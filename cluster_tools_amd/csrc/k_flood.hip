@@ -973,7 +973,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                                   const uint32_t* __restrict__ cnt, uint32_t* __restrict__ list_next,
                                                   uint32_t* __restrict__ cnt_next, uint32_t* __restrict__ qgen,
                                                   uint32_t* __restrict__ nvisit, uint32_t* __restrict__ nchange,
-                                                  int reps, int dirf) {
+                                                  int reps, int dirf, const uint32_t* __restrict__ ctrue) {
     static_assert(ND == 3 || CZ == 1, "2-D ws: slices are independent, chunks are one slice deep");
     __shared__ uint64_t schg[kFrontierWaves][64];
     // dirf: the local sweeps queue only the neighbours a change of p can affect, by the (C, d)
@@ -1158,6 +1158,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                     if (m == kPackInf) continue;
                     const uint64_t k = f_packed(ordf(hv[u]), m);
                     if (k == own[u]) continue;
+                    if (ctrue && (uint32_t)(k >> 32) != ctrue[B.base + iv[u]]) continue;
                     kb[iv[u]] = k;
                     if (key_dsat(k)) note_dsat(S, bi);
                     ++nch;
@@ -1252,7 +1253,8 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
                                                         const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,  \
                                                         uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*,   \
-                                                        uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int);
+                                                        uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int,         \
+                                                        const uint32_t*);
 #define CTWS_LIST0_INST(CW, CY, CZ)                                                                             \
     template __global__ void k_frontier_list0<CW, CY, CZ>(const BlockDesc*, const BlockStat*, const uint64_t*, \
                                                           uint32_t*, uint32_t*);
@@ -1268,6 +1270,15 @@ CTWS_LIST0_INST(8, 8, 1)
 CTWS_LIST0_INST(1, 32, 2)
 #undef CTWS_FRONTIER_INST
 #undef CTWS_LIST0_INST
+
+// experiment (CTWS_CTRUE_EXP, trace): the C part of the final keys
+__global__ void __launch_bounds__(256) k_ctrue_copy(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                    const uint64_t* __restrict__ key, uint32_t* __restrict__ ct) {
+    const BlockDesc& B = D[blockIdx.y];
+    if (!S[blockIdx.y].active) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * 256)
+        ct[B.base + i] = (uint32_t)(key[B.base + i] >> 32);
+}
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,

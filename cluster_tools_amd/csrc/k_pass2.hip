@@ -213,8 +213,13 @@ __global__ void __launch_bounds__(256) k_p2_label(const BlockDesc* __restrict__ 
         // lab, so only lab is written here (and no height is read)
         if (k == kEmptyKey) {
             lab[B.base + i] = 0;
-            if (write_keys) fixedv[B.base + i] = 0;
-            continue;  // key stays kEmptyKey == kInfKey
+            if (write_keys) {
+                // (the wide keys and the descent-less flood start from here: no stale key of an
+                // earlier batch may stay in an unlabelled voxel)
+                key[B.base + i] = kInfKey;
+                fixedv[B.base + i] = 0;
+            }
+            continue;
         }
         lab[B.base + i] = l | kFixedBit;
         if (write_keys) {

@@ -186,16 +186,22 @@ __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D,
 // and seed keys (h, 0, label) -- survivors elsewhere are never read by the regrow.
 constexpr uint32_t kSfSparseMax = 64;  // the largest size filter walked (a segment below it fits the queue)
 
+// a label survives the size filter: count >= size_filter, or (pass 2) an excluded initial id
+__device__ __forceinline__ bool sf_keeps(const uint32_t* c, const uint8_t* ex, uint32_t l, uint32_t size_filter) {
+    return c[l] >= size_filter || (ex && ex[l]);
+}
+
 __global__ void __launch_bounds__(256) k_sf_plan(const BlockDesc* __restrict__ D, BlockStat* S, uint32_t size_filter,
-                                                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ sb,
-                                                 uint32_t* __restrict__ survivors) {
+                                                 const uint32_t* __restrict__ counts, const uint8_t* __restrict__ excl,
+                                                 const uint32_t* __restrict__ sb, uint32_t* __restrict__ survivors) {
     const BlockDesc& B = D[blockIdx.x];
     BlockStat& st = S[blockIdx.x];
     if (!st.active) return;
     const uint32_t ns = st.n_seeds;
     const uint32_t* c = counts + B.base;
+    const uint8_t* ex = excl ? excl + B.base : nullptr;
     uint32_t nsmall = 0;
-    for (uint32_t l = 1 + threadIdx.x; l <= ns; l += 256) nsmall += c[l] < size_filter ? 1u : 0u;
+    for (uint32_t l = 1 + threadIdx.x; l <= ns; l += 256) nsmall += sf_keeps(c, ex, l, size_filter) ? 0u : 1u;
     nsmall = wg_reduce_u32(nsmall, OpAdd());
     // every slice (2-D) / the block (3-D) keeps a segment: no auto-seeded regrow
     uint32_t bare = 0;
@@ -203,7 +209,7 @@ __global__ void __launch_bounds__(256) k_sf_plan(const BlockDesc* __restrict__ D
         for (int z = threadIdx.x; z < B.Z; z += 256) {
             const uint32_t l0 = sb[B.sbase + z], l1 = z + 1 < B.Z ? sb[B.sbase + z + 1] : ns;
             bool any = false;
-            for (uint32_t l = l0 + 1; l <= l1 && !any; ++l) any = c[l] >= size_filter;
+            for (uint32_t l = l0 + 1; l <= l1 && !any; ++l) any = sf_keeps(c, ex, l, size_filter);
             bare += any ? 0u : 1u;
         }
     } else {
@@ -222,6 +228,7 @@ __global__ void __launch_bounds__(256) k_sf_plan(const BlockDesc* __restrict__ D
 // seed (breadth first, in-plane 4-neighbourhood in 2-D ws mode, 6 in 3-D)
 __global__ void __launch_bounds__(256) k_sf_sparse(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                    uint32_t size_filter, const uint32_t* __restrict__ counts,
+                                                   const uint8_t* __restrict__ excl,
                                                    const uint32_t* __restrict__ rootpos, const float* __restrict__ h,
                                                    uint64_t* __restrict__ key, uint8_t* __restrict__ fixedv,
                                                    uint64_t* __restrict__ open, uint64_t* __restrict__ chg) {
@@ -231,7 +238,8 @@ __global__ void __launch_bounds__(256) k_sf_sparse(const BlockDesc* __restrict__
     const uint32_t l = 1u + blockIdx.x * blockDim.x + threadIdx.x;
     if (l > st.n_seeds) return;
     const uint32_t* c = counts + B.base;
-    if (c[l] >= size_filter) return;
+    const uint8_t* ex = excl ? excl + B.base : nullptr;
+    if (sf_keeps(c, ex, l, size_filter)) return;
     uint64_t* kb = key + B.base;
     const int wpr = (B.X + 63) >> 6;
     const int64_t YX = (int64_t)B.Y * B.X;
@@ -273,7 +281,7 @@ __global__ void __launch_bounds__(256) k_sf_sparse(const BlockDesc* __restrict__
                 if (qt < (int)kSfSparseMax) claim(u);
                 continue;
             }
-            if (c[lu] < size_filter) continue;  // another removed segment (its own thread)
+            if (!sf_keeps(c, ex, lu, size_filter)) continue;  // another removed segment (its own thread)
             // a survivor next to the removed segment: a regrow seed, read by the frontier
             setbit(chg, u);
             if (ku & kDMask) {

@@ -31,7 +31,7 @@ VARIANTS = {
     # block on when its packed flood saturated d (tests/test_corridor_gpu.py)
     'wide_keys': {'CTWS_FORCE_WIDE': '1'},
     # the size filter's regrow initialised by the scan of every voxel instead of the walk over
-    # the removed segments (k_sf_sparse, the default for pass 1 with size_filter <= 64)
+    # the removed segments (k_sf_sparse, the default for size_filter <= 64)
     'sf_scan': {'CTWS_SF_SPARSE': '0'},
 }
 
@@ -72,3 +72,21 @@ def test_variant_matches_model(variant_handle, name):
     res = variant_handle.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=3)])[0]
     assert res['status'] == ref['status']
     np.testing.assert_array_equal(res['output'], ref['output'])
+
+
+_REF2 = {}
+
+
+@pytest.mark.parametrize('name', ['2d', '3d', '3d_mask', '2d_collide'])
+def test_variant_pass2_matches_model(variant_handle, name):
+    """_ws_pass2 under every knob: pass 2's size filter keeps the excluded initial ids whatever
+    their size, on the sparse walk (first positions of the relabelled ids) and on the scan."""
+    from pass2_cases import scenario
+    config, block_shape, blocks = scenario(name)
+    if name not in _REF2:
+        with O.flood_model():
+            _REF2[name] = O.ws_blocks(config, block_shape, blocks, pass_id=1)
+    res = variant_handle.ws_blocks(config, block_shape, blocks, pass_id=1)
+    for r, g in zip(_REF2[name], res):
+        assert g['status'] == r['status']
+        np.testing.assert_array_equal(g['output'], r['output'])
