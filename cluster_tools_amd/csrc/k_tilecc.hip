@@ -318,6 +318,25 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
                         rb = (uint32_t)(prv >> 32);
                     }
                 }
+            } else if (MODE == CC_CROP) {
+                // z / y face: one backward neighbour q across it.  Members are exactly the voxels
+                // with a parent (k_tile_cc), so two members connect iff their flood labels match:
+                // both parents and both labels are loaded together (clamped, unconditional), one
+                // round trip instead of parent -> neighbour's parent -> mask and label
+                const int lz = f == 0 ? 0 : e / TX, ly = f == 0 ? e / TX : 0, lx = e % TX;
+                const int z = z0 + lz, y = y0 + ly, x = x0 + lx;
+                const bool ok = e < n && z < nz && y < ny && x < nx && (f == 0 ? z > 0 : y > 0);
+                const int64_t i = ok ? ((int64_t)z * ny + y) * nx + x : 0;
+                const int64_t q = ok ? i - (f == 0 ? (int64_t)ny * nx : (int64_t)nx) : 0;
+                const int64_t o = ok ? ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0) : 0;
+                const int64_t oq = ok ? o - (f == 0 ? (int64_t)B.Y * B.X : (int64_t)B.X) : 0;
+                const uint32_t pi = gbl(P)[i], pq = gbl(P)[q];
+                const uint32_t li = flood_label(a.lab, a.key, a.packed, B.base + o);
+                const uint32_t lq = flood_label(a.lab, a.key, a.packed, B.base + oq);
+                if (ok && pi != kNoParent && pq != kNoParent && li == lq) {
+                    ra = pi;
+                    rb = pq;
+                }
             } else if (e < n) {
                 int lz, ly, lx;
                 if (f == 0) { lz = 0; ly = e / TX; lx = e % TX; }
