@@ -133,6 +133,7 @@ struct ctws_handle {
     int stop_after = 0;
     int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
     int no_descent = 0;  // CTWS_NO_DESCENT=1: flood from the seeds alone (test hook)
+    int seed_tilecc = 0;  // CTWS_SEED_TILECC=1: the 3-D seed CC by tiles (else k_seed_members)
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     // CTWS_FORCE_WIDE=1: every flood on the wide keys (k_flood, 32-bit d; tests).  wide_rerun:
     // run_batch is re-running blocks whose packed flood reported a saturated d (dsat)
@@ -1271,8 +1272,13 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_tile_cc<3, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_tile_merge<3, CC_PLATEAU><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
-            k_tile_cc<3, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
-            k_tile_merge<3, CC_SEED><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            if (h->seed_tilecc) {
+                k_tile_cc<3, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+                k_tile_merge<3, CC_SEED><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            } else {
+                // the seed components are the maximal plateaus and the isolated maxima (k_cc.hip)
+                k_seed_members<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF, w.fseed);
+            }
         } else {
             using T = CcTile<2>;
             const dim3 tg(tiles8(cdiv(maxZ, T::TZ) * cdiv(maxY, T::TY) * cdiv(maxX, T::TX)), nb);
@@ -1680,8 +1686,9 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_slice_offsets<<<nb, 64, 0, h->stream>>>(w.desc, w.stat, w.slmax, w.soff);
             k_p2_check<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.hkey, w.soff);
         }
+        // per slice: an in-mask voxel (2-D only: a seedless 3-D block fails whatever its mask)
         HIPCHK(hipMemsetAsync(w.smin, 0, sizeof(uint32_t) * TS, h->stream));  // free after the hmap
-        k_slice_inmask<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.smin);
+        if (pl.nd_ws == 2) k_slice_inmask<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.smin);
         mark("finalize");
         mark("crop_cc");
         k_p2_output<<<ig, 256, 0, h->stream>>>(w.desc, w.stat, w.lab, w.key, keys_final, (const uint32_t*)w.Bf,
@@ -2418,6 +2425,7 @@ int ctws_open(int device, ctws_handle** out) {
     h->device = device;
     if (const char* t = std::getenv("CTWS_TRACE")) h->trace = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_DESCENT")) h->no_descent = std::atoi(t);
+    if (const char* t = std::getenv("CTWS_SEED_TILECC")) h->seed_tilecc = std::atoi(t);
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FORCE_WIDE")) h->force_wide = std::atoi(t);
     if (const char* t = std::getenv("CTWS_SF_SPARSE")) h->sf_sparse = std::atoi(t);

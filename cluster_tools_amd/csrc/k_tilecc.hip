@@ -12,9 +12,9 @@
 // costs ~100x a streaming pass on large components.  Here a workgroup first solves its tile
 // (CcTileM: 3-D 8x16x32, crop 4x16x32; 2-D 1x32x64) completely in LDS: parents are tile-local positions and a
 // union links the root with the larger *order key* under the smaller (atomicCAS in LDS), so
-// every tile component is rooted at its smallest key.  For SEED/CROP the order key is the local F-order index
+// every tile component is rooted at its smallest key.  For SEED/CROP (and 3-D PLATEAU) the order key is the local F-order index
 // (x most significant, then y, then z — vigra scan order, A.0), so the tile root is the
-// component's first voxel in scan order within the tile; for PLATEAU the C-order index.
+// component's first voxel in scan order within the tile; for 2-D PLATEAU the C-order index.
 // The tile writes each member's global parent = its tile root (C-order block index), non-
 // members get kNoParent.  k_tile_merge then unions the tile roots across the tile faces with
 // the global (scan-key ordered) union-find; only face pairs whose local roots differ from the
@@ -118,7 +118,9 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
     // order key of tile position c: the C index (PLATEAU) or the vigra scan key (SEED, CROP)
     auto ordk = [&](uint32_t c) -> uint32_t {
         const int lx = (int)(c % TX), ly = (int)((c / TX) % TY), lz = (int)(c / (TX * TY));
-        return MODE == CC_PLATEAU ? c : fkey_local<TZ, TY>(lz, ly, lx);
+        // (3-D plateaus are rooted at their first voxel in scan order too: k_seed_members
+        // takes the maximal plateaus' roots as seed-component roots)
+        return (MODE == CC_PLATEAU && ND == 2) ? c : fkey_local<TZ, TY>(lz, ly, lx);
     };
     // load values: every load unconditional (position clamped into the domain, global address
     // space) so that all of a thread's loads are in flight together; non-members and positions
@@ -273,7 +275,7 @@ __global__ void __launch_bounds__(256) k_tile_cc(const BlockDesc* __restrict__ D
 }
 
 // union the tile roots across the tiles' backward faces (global union-find: by C index for
-// PLATEAU, by scan key for SEED / CROP so that roots stay the first voxel in scan order)
+// 2-D PLATEAU, by scan key otherwise so that roots stay the first voxel in scan order)
 template <int ND, int MODE>
 __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict__ D, const BlockStat* S, CcArgs a,
                                                     uint32_t* __restrict__ Pg) {
@@ -383,7 +385,7 @@ __global__ void __launch_bounds__(256) k_tile_merge(const BlockDesc* __restrict_
             const uint32_t pa = (uint32_t)__shfl_up((int)ra, 1), pb = (uint32_t)__shfl_up((int)rb, 1);
             const bool dup = ((threadIdx.x & 63) != 0) && pa == ra && pb == rb;
             if (ra != kNoParent && !dup) {
-                if (MODE == CC_PLATEAU) uf_union(P, ra, rb);
+                if (MODE == CC_PLATEAU && ND == 2) uf_union(P, ra, rb);
                 else uf_union_scan(P, ra, rb, B, inner);
             }
         }
