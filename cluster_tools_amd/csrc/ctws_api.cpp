@@ -119,7 +119,6 @@ struct ctws_handle {
     DevBuf edt_fh;
     DevBuf xface;  // crop CC: the tiles' x columns (CcArgs::xface)
     DevBuf ptile;  // plateau CC: per-tile plateau flags (CcArgs::ptile)
-    DevBuf ctrue;  // experiment (CTWS_CTRUE_EXP): final C per voxel
     DevBuf edt_scratch;  // k_edt_real_line: per-thread parabola stacks
     // WatershedFromSeeds (k_seeded.hip): distinct seed values, sorted values, segment offsets, sort temp
     DevBuf fs_vals, fs_sorted, fs_off, fs_tmp;
@@ -139,7 +138,6 @@ struct ctws_handle {
     // run_batch is re-running blocks whose packed flood reported a saturated d (dsat)
     int force_wide = 0;
     int wide_rerun = 0;
-    int ctrue_exp = 0;  // CTWS_CTRUE_EXP=1 (with CTWS_TRACE): re-run the frontier filtered by the final C
     int sf_sparse = 1;  // CTWS_SF_SPARSE=0: the size filter's regrow initialisation scans every block
     int verify = 1;      // CTWS_VERIFY: 1 (default) check the flood fixpoint + fallback, 2 fail on a violation (tests), 0 off
     int prep_lds = 0;    // CTWS_PREP_LDS=1: LDS row kernel for the x pass at every row length (tests)
@@ -161,7 +159,7 @@ struct ctws_handle {
     int host_batch_blocks = 0;  // CTWS_HOST_BATCH_BLOCKS: cap on blocks per host-path batch (0: voxel cap)
     int64_t host_batch_voxels = (int64_t)256 << 20;  // CTWS_HOST_BATCH_VOXELS: smaller batches pipeline better
     int edt_wz = 0;  // CTWS_EDT_WZ: the same for the z pass alone (3-D DT)
-    int edt_w = 0;  // CTWS_EDT_W (8, 16, 32): x positions per EDT column tile (0: by line length)
+    int edt_w = 0;  // CTWS_EDT_W (8, 16, 32, 64): x positions per EDT column tile (0: by line length)
     // CTWS_FRONTIER_CHUNK2D / _3D "CWxCYxCZ": frontier chunk brick (words x rows x slices, 64 words).
     // 3-D batches with a mask: 1x32x2 was their default until round 5 (a masked region is one
     // flat plateau the flood crosses hop by hop, and wider bricks in y cut the launches: config 5
@@ -672,8 +670,7 @@ int run_flood(ctws_handle* h, int nd, bool packed, int nb, int max_tiles, int64_
 // it has not converged after frontier_max_iters iterations (very long equal-height paths) the
 // tile flood finishes from the current keys.
 int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_tiles, int64_t TT, bool packed,
-                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out, bool regrow = false,
-                 const uint32_t* ctrue = nullptr) {
+                 uint32_t* fst, int* iters_out, int* rounds_out, float* kms_out, bool regrow = false) {
     Workspace& w = h->ws;
     const int64_t nch = (TF >> kChunkShift) + 1;
     uint64_t* fb[2] = {w.front0, w.front1};  // changed bitmaps: iteration it reads fb[it & 1]
@@ -717,8 +714,7 @@ int run_frontier(ctws_handle* h, const Plan& pl, int nb, int64_t TF, int max_til
         k_frontier<ND, CW, CY, CZ><<<fg, 256, 0, h->stream>>>(                                                      \
             w.desc, w.stat, w.hm, w.key, w.fopen, fb[it & 1], fb[(it + 1) & 1], gen[(it + 1) & 1], gen[it & 1], it, \
             wl[it & 1], w.wlcnt + it, wl[(it + 1) & 1], w.wlcnt + it + 1, w.qgen, fst ? fst + nb : nullptr,         \
-            fst ? fst + 2 * nb : nullptr,                                                                             \
-            h->frontier_reps, h->frontier_dir, ctrue);                                                              \
+            h->frontier_reps, h->frontier_dir);                                                                     \
         break;
             switch (fkind) {
                 CTWS_FRONTIER_SHAPES(CTWS_FRONTIER)
@@ -1177,7 +1173,12 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         }
     } else {
         // y pass (final for a 2-D dt), then z pass (3-D dt)
-        const int Wy = h->edt_w ? h->edt_w : edt_col_width(maxY);
+        // (a forced width narrows until the column tile fits the LDS: the default already does)
+        auto fit = [](int W, int L) {
+            while (W > 8 && (size_t)L * W * 4 > kMaxLds) W /= 2;
+            return W;
+        };
+        const int Wy = fit(h->edt_w ? h->edt_w : edt_col_width(maxY), maxY);
         EdtColParams ep{1, pl.pitch[1] * pl.pitch[1], pl.dt_2d, pl.dt_2d, 0u};
         dim3 gy((unsigned)((int64_t)maxZ * ((maxX + Wy - 1) / Wy)), nb);
         const size_t ldsy = (size_t)maxY * Wy * 4;
@@ -1199,7 +1200,8 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 lds_optin(kern, lds);
                 kern<<<g, 256, lds, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list, cnt);
             };
-            if (W == 32) go(k_edt_col<32>);
+            if (W == 64) go(k_edt_col<64>);
+            else if (W == 32) go(k_edt_col<32>);
             else if (W == 16) go(k_edt_col<16>);
             else go(k_edt_col<8>);
             k_edt_col_fh<<<gfh, 256, 0, h->stream>>>(w.desc, w.stat, p, gin, gout, w.dt, w.smin, w.smax, fh_list, cnt);
@@ -1207,7 +1209,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
         launch_col(Wy, gy, ldsy, ep, (uint32_t*)w.A, (uint32_t*)w.Bf, fh_cnt);
         LAUNCHCHK();
         if (!pl.dt_2d) {
-            const int Wz = h->edt_wz ? h->edt_wz : h->edt_w ? h->edt_w : edt_col_width(maxZ);
+            const int Wz = fit(h->edt_wz ? h->edt_wz : h->edt_w ? h->edt_w : edt_col_width(maxZ), maxZ);
             dim3 gz((unsigned)((int64_t)maxY * ((maxX + Wz - 1) / Wz)), nb);
             const size_t ldsz = (size_t)maxZ * Wz * 4;
             EdtColParams ez{2, pl.pitch[0] * pl.pitch[0], 1, 0, 0u};
@@ -1390,7 +1392,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             LAUNCHCHK();
         }
         mark("descent_tile");
-        if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 3 * (size_t)nb, h->stream));
+        if (fst) HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 2 * (size_t)nb, h->stream));
         // masked blocks: their plateau leaves the open set until the rest is flooded (k_plateau.hip);
         // the plateau level comes out of the descent pass
         bool any_mask = false;
@@ -1427,69 +1429,30 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 return r;
         }
         mark("flood_relax");
-        if (fst && h->ctrue_exp && !plat_fill) {
-            // experiment: the frontier again from the descent, each write filtered by the final C
-            std::vector<uint32_t> hs(3 * (size_t)nb);
-            HIPCHK(hipMemcpyAsync(hs.data(), fst, sizeof(uint32_t) * 3 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
-            if ((r = grow(h, h->ctrue, sizeof(uint32_t) * (size_t)T)) != CTWS_OK) return r;
-            k_ctrue_copy<<<dim3(4096, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.key, (uint32_t*)h->ctrue.p);
-            HIPCHK(hipMemsetAsync(fst, 0, sizeof(uint32_t) * 3 * (size_t)nb, h->stream));
-            k_descent_init<8><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.P, w.key, w.cls, w.fopen,
-                                                         w.front0, fst, nullptr);
-            hipEvent_t e0, e1;
-            hipEventCreate(&e0);
-            hipEventCreate(&e1);
-            hipEventRecord(e0, h->stream);
-            int it2 = 0;
-            if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, fst, &it2, &rounds1, &fk1, false,
-                                  (const uint32_t*)h->ctrue.p)) != CTWS_OK)
-                return r;
-            hipEventRecord(e1, h->stream);
-            std::vector<uint32_t> hs2(3 * (size_t)nb);
-            HIPCHK(hipMemcpyAsync(hs2.data(), fst, sizeof(uint32_t) * 3 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
-            float ms = 0.f;
-            hipEventElapsedTime(&ms, e0, e1);
-            hipEventDestroy(e0);
-            hipEventDestroy(e1);
-            double v1 = 0, c1 = 0, v2 = 0, c2 = 0;
-            for (int i = 0; i < nb; ++i) {
-                v1 += hs[nb + i];
-                c1 += hs[2 * nb + i];
-                v2 += hs2[nb + i];
-                c2 += hs2[2 * nb + i];
-            }
-            add_timing(h, "exp_ctrue_ms", ms);
-            add_timing(h, "exp_ctrue_iters", (float)it2);
-            add_timing(h, "exp_ctrue_visits", (float)v2);
-            add_timing(h, "exp_ctrue_writes", (float)c2);
-            std::fprintf(stderr, "[ctws] ctrue exp: visits %.0f -> %.0f, writes %.0f -> %.0f, %d iters, %.3f ms\n", v1,
-                         v2, c1, c2, it2, ms);
-        }
         if (fst) {
-            std::vector<uint32_t> hs(3 * (size_t)nb);
-            HIPCHK(hipMemcpyAsync(hs.data(), fst, sizeof(uint32_t) * 3 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
+            std::vector<uint32_t> hs(2 * (size_t)nb);
+            HIPCHK(hipMemcpyAsync(hs.data(), fst, sizeof(uint32_t) * 2 * (size_t)nb, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
-            double no = 0, nv = 0, nc = 0;
+            double no = 0, nv = 0;
             for (int i = 0; i < nb; ++i) {
                 no += hs[i];
                 nv += hs[nb + i];
-                nc += hs[2 * nb + i];
             }
             add_timing(h, "open_voxels", (float)no);
             add_timing(h, "frontier_visits", (float)nv);
-            add_timing(h, "frontier_key_writes", (float)nc);
         }
-        // fixpoint check of every voxel (a guard: the descent argument and the frontier's
-        // convergence make a violation impossible); on a violation the batch is flooded again
-        // from the seeds alone.  On by default (CTWS_VERIFY=0 turns it off).
+        // fixpoint check of every voxel the relaxation solved (a guard: the descent argument and
+        // the frontier's convergence make a violation impossible; on a violation the batch is
+        // flooded again from the seeds alone) and the d-saturation detector (a solved key with d
+        // at kDMax sets BlockStat::dsat: the block runs again on the wide keys).  The kernel
+        // always runs; CTWS_VERIFY=0 drops only the violation handling.
+        HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
+        if (pl.nd_ws == 3)
+            k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+        else
+            k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+        LAUNCHCHK();
         if (h->verify) {
-            HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
-            if (pl.nd_ws == 3)
-                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
-            else
-                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
-            LAUNCHCHK();
             HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
             if (h->trace && h->h_counter[0]) {
@@ -1622,14 +1585,15 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             if ((r = run_frontier(h, pl, nb, TF, max_tiles, TT, packed, nullptr, &fiters2, &rounds2, &fk2, true)) !=
                 CTWS_OK)
                 return r;
+            // the regrow's fixpoint at the voxels it solved (the removed ones), and its d
+            // saturation (as after the first flood: the kernel always runs)
+            HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
+            if (pl.nd_ws == 3)
+                k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+            else
+                k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
+            LAUNCHCHK();
             if (h->verify) {
-                // the regrow's fixpoint at the voxels it solved (the removed ones)
-                HIPCHK(hipMemsetAsync(w.counter, 0, 40, h->stream));
-                if (pl.nd_ws == 3)
-                    k_flood_verify<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
-                else
-                    k_flood_verify<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.hm, w.key, w.fopen, w.counter);
-                LAUNCHCHK();
                 HIPCHK(hipMemcpyAsync(h->h_counter, w.counter, 40, hipMemcpyDeviceToHost, h->stream));
                 HIPCHK(hipStreamSynchronize(h->stream));
                 if (h->h_counter[0] && h->verify >= 2) {
@@ -1808,7 +1772,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
     add_timing(h, "flood_local_iters", (float)h->flood_iters);
     add_timing(h, "flood_lines_swept", (float)h->flood_lines);
     add_timing(h, "size_filter_kernel_ms", fk2);
-    // blocks whose packed flood wrote a key with d at kDMax (note_dsat): the 12-bit hop distance
+    // blocks whose packed flood ended with a key with d at kDMax (note_dsat): the 12-bit hop distance
     // may have saturated, so they are flooded again on the wide keys (32-bit d) below, never
     // returned with a possibly different fixpoint
     std::vector<int> wide;
@@ -2429,7 +2393,6 @@ int ctws_open(int device, ctws_handle** out) {
     if (const char* t = std::getenv("CTWS_NO_FALLBACK")) h->no_fallback = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FORCE_WIDE")) h->force_wide = std::atoi(t);
     if (const char* t = std::getenv("CTWS_SF_SPARSE")) h->sf_sparse = std::atoi(t);
-    if (const char* t = std::getenv("CTWS_CTRUE_EXP")) h->ctrue_exp = std::atoi(t);
     if (const char* t = std::getenv("CTWS_VERIFY")) h->verify = std::atoi(t);
     if (const char* t = std::getenv("CTWS_PREP_LDS")) h->prep_lds = std::atoi(t);
     if (const char* t = std::getenv("CTWS_FRONTIER_ITERS"))
@@ -2452,11 +2415,11 @@ int ctws_open(int device, ctws_handle** out) {
     }
     if (const char* t = std::getenv("CTWS_EDT_W")) {
         const int v = std::atoi(t);
-        h->edt_w = (v == 8 || v == 16 || v == 32) ? v : 0;
+        h->edt_w = (v == 8 || v == 16 || v == 32 || v == 64) ? v : 0;
     }
     if (const char* t = std::getenv("CTWS_EDT_WZ")) {
         const int v = std::atoi(t);
-        h->edt_wz = (v == 8 || v == 16 || v == 32) ? v : 0;
+        h->edt_wz = (v == 8 || v == 16 || v == 32 || v == 64) ? v : 0;
     }
     auto parse_chunk = [](const char* t, int* c, bool three_d) {
         int a = 0, b = 0, d = 0;

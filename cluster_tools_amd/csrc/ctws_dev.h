@@ -61,7 +61,7 @@ struct BlockStat {
     uint32_t n_auto;          // auto-seeded regrow: strict hmap minima of the seedless slices
     uint32_t _p[4];
     uint32_t dsat;            // packed flood: a key's hop distance d reached kDMax (note_dsat)
-    uint32_t unreached;       // 2-D size filter: voxels the flood did not reach (k_hist2d)
+    uint32_t _u;              // (unused)
     uint32_t sf_sparse;       // size filter: the removed segments are walked, not scanned (k_sf_plan)
     uint32_t _q;
 };
@@ -394,8 +394,8 @@ constexpr uint64_t kDMask = 0xFFFull << kLabelBits;
 // 12-bit field saturates at kDMax; INF has d = 0xFFF and stays INF).  d must grow along every
 // parent edge: then (C, d) strictly increases from a voxel's argmin neighbour to the voxel, the
 // fixpoint is unique, and any relaxation schedule reaches the sequential model's result.  A
-// saturated d breaks that, so a write of d = kDMax is reported (note_dsat below) and the block is
-// flooded again on the wide keys, whose 32-bit d never saturates (round 6).
+// saturated d breaks that, so a final key with d = kDMax is reported (note_dsat below) and the
+// block is flooded again on the wide keys, whose 32-bit d never saturates (round 6).
 // Orders with d capped at 1 or without d measured closer to vigra's heap order on tie-dominated
 // inputs (scripts/tie_order_experiment.py) but lose that: equal keys along a plateau path let a
 // cycle of voxels keep a stale label, and the GPU converged to such a fixpoint (round 4,
@@ -404,10 +404,11 @@ constexpr uint32_t kDMax = 4095;
 
 // A packed key whose d field is at kDMax: the hop distance may have saturated, so the packed
 // fixpoint may differ from the unbounded (C, d, label) one (a cycle of equal saturated keys can
-// keep a stale label).  Every kernel that writes a relaxed packed key reports such a write in
-// BlockStat::dsat; run_batch then floods those blocks again with the wide keys (k_flood: d is
-// 32 bits there and never saturates).  Writes with d < kDMax cannot differ from the unbounded
-// flood, so a batch without a report is exact.
+// keep a stale label).  k_flood_verify (after every frontier flood) and the tile flood's writes
+// report such a key in BlockStat::dsat; run_batch then floods those blocks again with the wide
+// keys (k_flood: d is 32 bits there and never saturates).  If every final d is below kDMax, each
+// final key is the exact f of its neighbours' minimum: a fixpoint of the unbounded order, which
+// is unique, so a batch without a report is exact.
 __device__ __forceinline__ bool key_dsat(uint64_t k) { return (k & kDMask) == kDMask && k != kPackInf; }
 __device__ __forceinline__ void note_dsat(const BlockStat* S, int b) {
     uint32_t* p = const_cast<uint32_t*>(&S[b].dsat);

@@ -179,9 +179,7 @@ __global__ void k_descent_init(const BlockDesc*, const BlockStat*, const float*,
 template <int ND, int CW, int CY, int CZ>
 __global__ void k_frontier(const BlockDesc*, const BlockStat*, const float*, uint64_t*, const uint64_t*,
                            const uint64_t*, uint64_t*, const uint32_t*, uint32_t*, int, const uint32_t*,
-                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int,
-                           const uint32_t*);
-__global__ void k_ctrue_copy(const BlockDesc*, const BlockStat*, const uint64_t*, uint32_t*);
+                           const uint32_t*, uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int);
 // k_eval.hip (VI / Rand contingency table)
 __global__ void k_eval_add(const uint64_t*, const uint64_t*, int64_t, int, uint64_t*, unsigned long long*, int64_t,
                            uint64_t*, unsigned long long*, int64_t, uint64_t*, unsigned long long*, int64_t,

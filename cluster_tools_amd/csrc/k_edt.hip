@@ -459,7 +459,7 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
                                                  uint32_t* fh_cnt) {
     extern __shared__ __attribute__((aligned(16))) int smem_i[];
     uint32_t* col = (uint32_t*)smem_i;
-    __shared__ uint32_t capped_cols;  // bit c: a voxel of column c hit kEdtSearchCap
+    __shared__ unsigned long long capped_cols;  // bit c: a voxel of column c hit kEdtSearchCap
     const BlockDesc& B = D[blockIdx.y];
     if (!S[blockIdx.y].active) return;
     const int nxc = (B.X + W - 1) / W;
@@ -481,7 +481,7 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
             r0, L, RS, [&](int p) { return colok ? gsrc[p * lstride] : kInfD2; },
             [&](int p, uint32_t v) { col[p * W + c] = v; });
     }
-    if (threadIdx.x == 0) capped_cols = 0u;
+    if (threadIdx.x == 0) capped_cols = 0ull;
     __syncthreads();
     uint32_t mn = 0xFFFFFFFFu, mx = 0u;
     const uint32_t maxd = ep.per_slice ? (uint32_t)(B.Y * B.Y + B.X * B.X) : B.maxd;
@@ -521,9 +521,9 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
             gout[gi] = best;
         }
     }
-    if (capped_any) atomicOr(&capped_cols, 1u << c);
+    if (capped_any) atomicOr(&capped_cols, 1ull << c);
     __syncthreads();
-    if (threadIdx.x < W && ((capped_cols >> threadIdx.x) & 1u)) {
+    if (threadIdx.x < W && ((capped_cols >> threadIdx.x) & 1ull)) {
         const uint32_t e = atomicAdd(fh_cnt, 1u);
         fh_list[e] = ((unsigned long long)blockIdx.y << 48) | ((unsigned long long)o << 24) |
                      (unsigned long long)(xb + threadIdx.x);
@@ -557,6 +557,7 @@ __global__ void __launch_bounds__(256) k_edt_col(const BlockDesc* __restrict__ D
 #define CTWS_EDT_COL(W)                                                                                          \
     template __global__ void k_edt_col<W>(const BlockDesc*, BlockStat*, EdtColParams, const uint32_t*, uint32_t*,   \
                                           float*, uint32_t*, uint32_t*, unsigned long long*, uint32_t*);
+CTWS_EDT_COL(64)
 CTWS_EDT_COL(32)
 CTWS_EDT_COL(16)
 CTWS_EDT_COL(8)

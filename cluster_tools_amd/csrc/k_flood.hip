@@ -972,8 +972,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                                                   uint32_t* __restrict__ gnext, int it, const uint32_t* __restrict__ list,
                                                   const uint32_t* __restrict__ cnt, uint32_t* __restrict__ list_next,
                                                   uint32_t* __restrict__ cnt_next, uint32_t* __restrict__ qgen,
-                                                  uint32_t* __restrict__ nvisit, uint32_t* __restrict__ nchange,
-                                                  int reps, int dirf, const uint32_t* __restrict__ ctrue) {
+                                                  uint32_t* __restrict__ nvisit, int reps, int dirf) {
     static_assert(ND == 3 || CZ == 1, "2-D ws: slices are independent, chunks are one slice deep");
     __shared__ uint64_t schg[kFrontierWaves][64];
     // dirf: the local sweeps queue only the neighbours a change of p can affect, by the (C, d)
@@ -1075,7 +1074,6 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
         uint64_t acc = 0ull;  // changed bits of this word over all local sweeps
         bool conv = true;     // the local sweeps ended without a pending change
         uint32_t vis = 0;     // statistics (CTWS_TRACE): voxels visited
-        uint32_t nch = 0;     // statistics (CTWS_TRACE): keys written
         for (int rep = 0;; ++rep) {
             // exclusive prefix of the per-word bit counts: entry e of the chunk's frontier list
             // is bit (e - pre[j]) of word j, the last j with pre[j] <= e
@@ -1158,10 +1156,10 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
                     if (m == kPackInf) continue;
                     const uint64_t k = f_packed(ordf(hv[u]), m);
                     if (k == own[u]) continue;
-                    if (ctrue && (uint32_t)(k >> 32) != ctrue[B.base + iv[u]]) continue;
+                    // (a saturated d is detected on the final keys, k_flood_verify; no statistics
+                    // either: each extra live value here costs a wave per SIMD, 3-D 125 -> 137
+                    // VGPRs with a write counter and the saturation test, config 4 relax +5 ms)
                     kb[iv[u]] = k;
-                    if (key_dsat(k)) note_dsat(S, bi);
-                    ++nch;
                     atomicOr((unsigned long long*)&schg[wv][jv[u]], 1ull << bv[u]);
                     if (dirf) {
                         // nb[] order: -z, +z, -y, +y, -x, +x (outside the block: INF, its bit is
@@ -1215,10 +1213,6 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
             f &= opw;
         }
         if (nvisit && lane == 0 && vis) atomicAdd(&nvisit[bi], vis);
-        if (nchange) {
-            for (int o = 32; o > 0; o >>= 1) nch += (uint32_t)__shfl_xor((int)nch, o);
-            if (lane == 0 && nch) atomicAdd(&nchange[bi], nch);
-        }
         if (__ballot(acc != 0ull) == 0ull) continue;
         // the chunk changed: publish its changed words and queue the chunks that hold a
         // neighbour of a change (faces), and itself unless its local sweeps converged
@@ -1253,8 +1247,7 @@ __global__ void __launch_bounds__(256) k_frontier(const BlockDesc* __restrict__ 
     template __global__ void k_frontier<ND, CW, CY, CZ>(const BlockDesc*, const BlockStat*, const float*, uint64_t*, \
                                                         const uint64_t*, const uint64_t*, uint64_t*, const uint32_t*,  \
                                                         uint32_t*, int, const uint32_t*, const uint32_t*, uint32_t*,   \
-                                                        uint32_t*, uint32_t*, uint32_t*, uint32_t*, int, int,         \
-                                                        const uint32_t*);
+                                                        uint32_t*, uint32_t*, uint32_t*, int, int);
 #define CTWS_LIST0_INST(CW, CY, CZ)                                                                             \
     template __global__ void k_frontier_list0<CW, CY, CZ>(const BlockDesc*, const BlockStat*, const uint64_t*, \
                                                           uint32_t*, uint32_t*);
@@ -1270,15 +1263,6 @@ CTWS_LIST0_INST(8, 8, 1)
 CTWS_LIST0_INST(1, 32, 2)
 #undef CTWS_FRONTIER_INST
 #undef CTWS_LIST0_INST
-
-// experiment (CTWS_CTRUE_EXP, trace): the C part of the final keys
-__global__ void __launch_bounds__(256) k_ctrue_copy(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                    const uint64_t* __restrict__ key, uint32_t* __restrict__ ct) {
-    const BlockDesc& B = D[blockIdx.y];
-    if (!S[blockIdx.y].active) return;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < B.N; i += (int64_t)gridDim.x * 256)
-        ct[B.base + i] = (uint32_t)(key[B.base + i] >> 32);
-}
 
 // tiles still holding open voxels -> full solve in the tile flood (when the frontier loop stops)
 __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restrict__ D, const BlockStat* S,
@@ -1330,7 +1314,7 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
     const int64_t per = (nunits + nwaves - 1) / nwaves;
     const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int64_t ubeg = wid * per, uend = min(nunits, ubeg + per);
-    bool bad = false;
+    bool bad = false, dsat = false;
     // 64 units at a time: lane l loads the open words of unit un0 + l, and only the units with an
     // open voxel are visited (the regrow's open set is a few removed segments: most units skip)
     for (int64_t un0 = ubeg; un0 < uend; un0 += 64) {
@@ -1405,6 +1389,9 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
             // survivors and auto seeds are taken out of the open set)
             const uint64_t e = (m == kPackInf) ? kPackInf : f_packed(ordf(hv[u]), m);
             const bool b1 = valid && ((ow[u] >> lane) & 1ull) && e != o;
+            // a solved key with d at kDMax: the 12-bit hop distance may have saturated (with every
+            // final d below kDMax the keys are a fixpoint of the exact f, which is unique)
+            dsat |= valid && ((ow[u] >> lane) & 1ull) && key_dsat(o);
             if (b1 && flag[1] < 8u) {  // diagnostics: the first few violations
                 const uint32_t slot = atomicAdd(&flag[1], 1u);
                 if (slot < 8u) flag[2 + slot] = (uint32_t)(B.base + zb + (int64_t)y * B.X + x);
@@ -1414,6 +1401,7 @@ __global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restric
       }
     }
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+    if (__ballot(dsat) && (threadIdx.x & 63) == 0) note_dsat(S, blockIdx.y);
 }
 template __global__ void k_flood_verify<3>(const BlockDesc*, const BlockStat*, const float*, const uint64_t*,
                                            const uint64_t*, uint32_t*);

@@ -185,7 +185,7 @@ __device__ __forceinline__ void gauss_run(const double (&k)[2 * R + 1], int L, i
 }
 
 template <int W, int R>
-__global__ void __launch_bounds__(256) k_gauss_col_r(const BlockDesc* __restrict__ D, const BlockStat* S,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_gauss_col_r(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                      GaussParams gp, HmapParams hp, const double* __restrict__ taps,
                                                      const float* __restrict__ in, const float* __restrict__ dt,
                                                      const uint32_t* smin, const uint32_t* smax,

@@ -27,8 +27,9 @@
 
 namespace ctws {
 
-// n more hops inside the plateau: d + n, saturating at kDMax as f_packed does (a saturated key
-// written is reported, note_dsat); INF stays INF
+// n more hops inside the plateau: d + n, saturating at kDMax as f_packed does (the plateau voxels
+// rejoin the open set, k_plat_restore, so a saturated final key is reported by k_flood_verify);
+// INF stays INF
 __device__ __forceinline__ uint64_t key_hops(uint64_t k, uint32_t n) {
     if (k == kPackInf) return k;
     const uint32_t d = (uint32_t)((k & kDMask) >> kLabelBits);
@@ -81,7 +82,6 @@ __global__ void __launch_bounds__(256) k_plat_entry(const BlockDesc* __restrict_
             if (m != kPackInf) {
                 const uint64_t k = f_packed(ordf(h[B.base + i]), m);
                 kb[i] = k;
-                if (key_dsat(k)) note_dsat(S, blockIdx.y);
             }
         }
     })
@@ -136,7 +136,6 @@ __global__ void __launch_bounds__(256) k_plat_scan_x(const BlockDesc* __restrict
                 if (!inp) v = kPackInf;
                 if (inp && v != v0) {
                     kb[i] = v;
-                    if (key_dsat(v)) note_dsat(S, blockIdx.y);
                 }
                 carry = shfl_u64(v, 63);  // kPackInf when the run does not reach the word's end
             }
@@ -193,7 +192,6 @@ __global__ void __launch_bounds__(256) k_plat_scan_col(const BlockDesc* __restri
                     const uint64_t nv = min(kv[u], key_hops(run, 1u));
                     if (nv != kv[u]) {
                         kb[vi[u]] = nv;
-                        if (key_dsat(nv)) note_dsat(S, blockIdx.y);
                     }
                     run = nv;
                 }

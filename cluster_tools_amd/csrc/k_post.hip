@@ -132,7 +132,6 @@ __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D,
     const int64_t i0 = (int64_t)z * YX + YX * s / splits, i1 = (int64_t)z * YX + YX * (s + 1) / splits;
     uint32_t* c = counts + B.base + b0 + 1;
     const int lane = threadIdx.x & 63;
-    uint32_t nzero = 0;
     constexpr int U = 8;
     for (int64_t ib = i0; ib < i1; ib += 256 * U) {
         uint32_t lv[U];
@@ -155,20 +154,14 @@ __global__ void __launch_bounds__(256) k_hist2d(const BlockDesc* __restrict__ D,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t l = lv[u];
-            // 0 (unreached) is not counted, only tallied for the size filter's plan (k_sf_plan)
+            // (0, unreached, is not counted: k_sf_plan derives it from the counts)
             count_label_runs(l, l != 0xFFFFFFFFu, lane, [&](uint32_t lb, uint32_t n) {
-                if (lb == 0) {
-                    nzero += n;
-                    return;
-                }
                 if (lb <= b0 || lb > b1) return;
                 if (use_lds) atomicAdd(&sh[lb - b0 - 1], n);
                 else atomicAdd(&c[lb - b0 - 1], n);
             });
         }
     }
-    nzero = wg_reduce_u32(nzero, OpAdd());
-    if (threadIdx.x == 0 && nzero) atomicAdd(const_cast<uint32_t*>(&S[blockIdx.y].unreached), nzero);
     if (!use_lds) return;
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += 256)
@@ -200,9 +193,15 @@ __global__ void __launch_bounds__(256) k_sf_plan(const BlockDesc* __restrict__ D
     const uint32_t ns = st.n_seeds;
     const uint32_t* c = counts + B.base;
     const uint8_t* ex = excl ? excl + B.base : nullptr;
-    uint32_t nsmall = 0;
-    for (uint32_t l = 1 + threadIdx.x; l <= ns; l += 256) nsmall += sf_keeps(c, ex, l, size_filter) ? 0u : 1u;
+    uint32_t nsmall = 0, tot = 0;
+    for (uint32_t l = 1 + threadIdx.x; l <= ns; l += 256) {
+        nsmall += sf_keeps(c, ex, l, size_filter) ? 0u : 1u;
+        tot += c[l];
+    }
     nsmall = wg_reduce_u32(nsmall, OpAdd());
+    // the voxels without a label (unreached by the flood): the block's voxels the labels' counts
+    // leave over (every labelled voxel is counted once, 2-D slices in their own label ranges)
+    tot = wg_reduce_u32(tot, OpAdd());
     // every slice (2-D) / the block (3-D) keeps a segment: no auto-seeded regrow
     uint32_t bare = 0;
     if (B.nd_ws == 2) {
@@ -216,7 +215,7 @@ __global__ void __launch_bounds__(256) k_sf_plan(const BlockDesc* __restrict__ D
         bare = threadIdx.x == 0 && nsmall == ns ? 1u : 0u;
     }
     bare = wg_reduce_u32(bare, OpAdd());
-    const uint32_t unreached = B.nd_ws == 2 ? st.unreached : c[0];
+    const uint32_t unreached = (uint32_t)B.N - tot;
     const bool sparse = size_filter <= kSfSparseMax && !unreached && !bare &&
                         (uint64_t)nsmall * size_filter <= (uint64_t)B.N / 8;
     if (threadIdx.x == 0) st.sf_sparse = sparse ? 1u : 0u;
