@@ -1297,7 +1297,7 @@ __global__ void __launch_bounds__(256) k_frontier_tiles(const BlockDesc* __restr
 // and lower rows; x-neighbours come from the neighbouring lanes, lane 0 / 63 fetch the key
 // left / right of the word.
 template <int ND>
-__global__ void __launch_bounds__(256) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_flood_verify(const BlockDesc* __restrict__ D, const BlockStat* S,
                                                       const float* __restrict__ h, const uint64_t* __restrict__ key,
                                                       const uint64_t* __restrict__ open, uint32_t* __restrict__ flag) {
     const BlockDesc& B = D[blockIdx.y];
