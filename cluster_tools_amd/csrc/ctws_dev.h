@@ -224,11 +224,14 @@ __device__ __forceinline__ void uf_union_scan(uint32_t* P, uint32_t a, uint32_t 
     }
 }
 
-// voxel i of block B (outer C index) in a per-row-word bitmap (the frontier layout at fbase)
+// voxel i of block B (outer C index) in a per-row-word bitmap (the frontier layout at fbase).
+// 32-bit division: a block holds fewer than 2^31 voxels (block_refusal), and the emulated 64-bit
+// one is a long instruction sequence per call (the pass-2 relabel calls this per voxel)
 __device__ __forceinline__ bool bit_of(const uint64_t* bits, const BlockDesc& B, int64_t i) {
-    const int64_t row = i / B.X;
-    const int x = (int)(i - row * B.X);
-    return (bits[B.fbase + row * ((B.X + 63) >> 6) + (x >> 6)] >> (x & 63)) & 1ull;
+    const uint32_t ii = (uint32_t)i;
+    const uint32_t row = ii / (uint32_t)B.X;
+    const int x = (int)(ii - row * (uint32_t)B.X);
+    return (bits[B.fbase + (int64_t)row * ((B.X + 63) >> 6) + (x >> 6)] >> (x & 63)) & 1ull;
 }
 
 // label of a CC member from its parent slot p = P[i] after k_root_label (0: background)

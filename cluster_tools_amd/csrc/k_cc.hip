@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(256) k_seed_members(const BlockDesc* __restric
     const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
     // one 64-voxel word per wave step (a lane per voxel): the member bits are one ballot
     for (int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < nw; w += nwaves) {
-        const int64_t row = w / wpr;
+        const int64_t row = (uint32_t)w / (uint32_t)wpr;  // (32-bit: fewer than 2^31 / 64 words)
         const int x = (int)(w - row * wpr) * 64 + lane;
         const bool in = x < B.X;
         const int64_t i = row * B.X + (in ? x : 0);

@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(256) k_p2_excl(const BlockDesc* __restrict__ D
         if (B.nd_ws == 3) {
             if (u <= nl) excl[B.base + u] = 1;
         } else {
-            const int z = (int)(i / YX);
+            const int z = (int)((uint32_t)i / (uint32_t)YX);
             const uint32_t b0 = sb[B.sbase + z];
             const uint32_t b1 = (z + 1 < B.Z) ? sb[B.sbase + z + 1] : nl;
             if (u <= (uint64_t)(b1 - b0)) excl[B.base + b0 + u] = 1;
@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(256) k_p2_check(const BlockDesc* __restrict__ 
     const int64_t YX = (int64_t)B.Y * B.X;
     BLOCK_LOOP(i, B) {
         const uint64_t u = gbl(B.init)[i];
-        const int z = (int)(i / YX);
+        const int z = (int)((uint32_t)i / (uint32_t)YX);
         if (i == (int64_t)z * YX) {
             // a shifted new seed that wraps to 0 would have become background
             const uint32_t t0 = 0u - (uint32_t)B.id_offset - soff[B.sbase + z];
@@ -305,15 +305,18 @@ __global__ void __launch_bounds__(256) k_p2_output(const BlockDesc* __restrict__
     const int64_t yx = (int64_t)B.IY * B.IX;
     uint32_t mx = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B.NI; i += (int64_t)gridDim.x * blockDim.x) {
-        const int z = (int)(i / yx);
-        const int rem = (int)(i - z * yx);
-        const int y = rem / B.IX, x = rem - (rem / B.IX) * B.IX;
+        // (32-bit divisions: a block holds fewer than 2^31 voxels)
+        const uint32_t ii = (uint32_t)i, yx32 = (uint32_t)yx;
+        const int z = (int)(ii / yx32);
+        const int rem = (int)(ii - (uint32_t)z * yx32);
+        const int y = rem / B.IX, x = rem - y * B.IX;
         const int64_t o = ((int64_t)(z + B.iz0) * B.Y + (y + B.iy0)) * B.X + (x + B.ix0);
         // the final label: from the packed keys (keys_final: no unpack pass over the outer
-        // block for the inner voxels read here) or from lab
+        // block for the inner voxels read here) or from lab; the mask loaded with it
         const uint32_t l = flood_label(lab, key, keys_final, B.base + o);
+        const bool inm = !B.mask || gbl(B.mask)[o];
         uint32_t v = 0;
-        if (l && (!B.mask || gbl(B.mask)[o])) {
+        if (l && inm) {
             v = oldv[B.base + l];
             if (B.nd_ws == 2 && !oldt[B.base + l]) v = v + (uint32_t)B.id_offset + soff[B.sbase + z + B.iz0];
         }
@@ -336,7 +339,7 @@ __global__ void __launch_bounds__(256) k_slice_inmask(const BlockDesc* __restric
     const int64_t YX = (int64_t)B.Y * B.X;
     BLOCK_LOOP(i, B) {
         if (B.mask && !gbl(B.mask)[i]) continue;
-        uint32_t* f = flag + B.sbase + (B.nd_ws == 2 ? (int)(i / YX) : 0);
+        uint32_t* f = flag + B.sbase + (B.nd_ws == 2 ? (int)((uint32_t)i / (uint32_t)YX) : 0);
         if (!*f) *f = 1;
     }
 }

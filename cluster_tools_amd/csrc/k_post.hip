@@ -258,9 +258,10 @@ __global__ void __launch_bounds__(256) k_sf_sparse(const BlockDesc* __restrict__
     claim((int64_t)rootpos[B.base + l]);
     while (qh < qt) {
         const int64_t v = q[qh++];
-        const int z = (int)(v / YX);
-        const int64_t r = v - (int64_t)z * YX;
-        const int y = (int)(r / B.X), x = (int)(r - (int64_t)y * B.X);
+        // (32-bit divisions: a block holds fewer than 2^31 voxels)
+        const int z = (int)((uint32_t)v / (uint32_t)YX);
+        const uint32_t r = (uint32_t)v - (uint32_t)z * (uint32_t)YX;
+        const int y = (int)(r / (uint32_t)B.X), x = (int)(r - (uint32_t)y * (uint32_t)B.X);
         int64_t nbr[6];
         int nn = 0;
         if (x > 0) nbr[nn++] = v - 1;
