@@ -197,48 +197,107 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
     if (threadIdx.x == 0 && nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
 }
 
-// 3-D seed components without a CC of their own.  Two adjacent local maxima have equal values
-// (else the smaller has a strictly greater neighbour), so they lie on one plateau, and every
-// voxel of a maximal plateau is a maximum: the seed components (direct 6-nbhd, as the plateau
-// CC's in 3-D) are the maximal plateau components and the isolated maxima.  The 3-D plateau CC
-// roots each component at its first voxel in scan order (k_tile_cc / k_tile_merge<3,
-// CC_PLATEAU>), so member i's parent is its plateau's root or i itself: the same seed forest
-// (members' parents at their roots) and member bitmap as k_tile_cc + k_tile_merge<3, CC_SEED>,
-// from one pass over the classes (the plateau voxels, rare, follow their plateau parents).
-// (2-D keeps the tile CC: its plateau CC is 8-connected in-plane and the seed CC 4-connected;
-// maxima as roots plus a union pass over the 4-adjacent plateau maxima measured config 3 seeds
-// 7.05 -> 7.35 ms.)
-__global__ void __launch_bounds__(256) k_seed_members(const BlockDesc* __restrict__ D, const BlockStat* S,
-                                                       const uint8_t* __restrict__ cls, const uint32_t* __restrict__ Pp,
-                                                       uint32_t* __restrict__ PFg, uint64_t* __restrict__ fseed) {
+// Seed components without a seed tile CC.  Two adjacent local maxima have equal values (else
+// the smaller has a strictly greater neighbour), so they lie on one plateau, and every voxel of
+// a maximal plateau is a maximum.  3-D: the seed components (direct 6-nbhd, as the plateau CC's)
+// are the maximal plateau components and the isolated maxima; the 3-D plateau CC roots each
+// component at its first voxel in scan order (k_tile_cc / k_tile_merge<3, CC_PLATEAU>), so
+// member i's parent is its plateau's root or i itself -- the same seed forest (members' parents
+// at their roots) and member bitmap as k_tile_cc + k_tile_merge<3, CC_SEED>.  2-D: the plateau
+// CC is 8-connected in-plane and the seed CC 4-connected, so every maximum starts as its own
+// root and the plateau maxima (rare) go to a list for k_seed_union2.  One pass over the classes,
+// 8 words in flight per wave (the plateau voxels follow their plateau parents).
+template <int ND>
+__global__ void __launch_bounds__(256) k_seed_members(const BlockDesc* __restrict__ D, BlockStat* S,
+                                                      const uint8_t* __restrict__ cls, const uint32_t* __restrict__ Pp,
+                                                      uint32_t* __restrict__ PFg, uint64_t* __restrict__ fseed,
+                                                      uint32_t* __restrict__ plist) {
     const BlockDesc& B = D[blockIdx.y];
-    const BlockStat& st = S[blockIdx.y];
+    BlockStat& st = S[blockIdx.y];
     if (!st.active) return;
     const bool plat = st.plateau != 0;
     const uint8_t* cl = cls + B.base;
     const uint32_t* PP = Pp + B.base;
     uint32_t* PF = PFg + B.base;
     const int wpr = (B.X + 63) >> 6;
-    const int64_t nw = (int64_t)B.Z * B.Y * wpr;
+    const int64_t nwords = (int64_t)B.Z * B.Y * wpr;
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    // one 64-voxel word per wave step (a lane per voxel): the member bits are one ballot
-    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < nw; w += nwaves) {
-        const int64_t row = (uint32_t)w / (uint32_t)wpr;  // (32-bit: fewer than 2^31 / 64 words)
-        const int x = (int)(w - row * wpr) * 64 + lane;
-        const bool in = x < B.X;
-        const int64_t i = row * B.X + (in ? x : 0);
-        const uint8_t c = gbl(cl)[i];
-        bool mx = in && !(c & 1);
-        uint32_t par = (uint32_t)i;
-        if (mx && (c & 2) && plat) {  // cc_is_max of a plateau voxel
-            const uint32_t r = uf_find(PP, (uint32_t)i);
-            if (cl[r] & 4) mx = false;
-            else par = r;
+    const int64_t per = (nwords + nwaves - 1) / nwaves;
+    const int64_t wid = (int64_t)xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t wbeg = wid * per, wend = min(nwords, wbeg + per);
+    // (row, word in the row) of the wave's next word, advanced word by word
+    int row_n = (int)((uint32_t)wbeg / (uint32_t)wpr), xw_n = (int)(wbeg - (int64_t)row_n * wpr);
+    constexpr int U = 8;
+    for (int64_t w0 = wbeg; w0 < wend; w0 += U) {
+        int64_t gi[U];
+        bool valid[U];
+        uint8_t c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = row_n;
+            const int x = xw_n * 64 + lane;
+            if (++xw_n == wpr) {
+                xw_n = 0;
+                ++row_n;
+            }
+            valid[u] = w0 + u < wend && x < B.X;
+            gi[u] = valid[u] ? row * B.X + x : 0;
+            c[u] = gbl(cl)[gi[u]];  // unconditional (clamped): all U loads in flight
         }
-        const uint64_t m = __ballot(mx);
-        if (lane == 0) fseed[B.fbase + w] = m;
-        if (mx) PF[i] = par;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            bool mx = valid[u] && !(c[u] & 1);
+            uint32_t par = (uint32_t)gi[u];
+            bool listed = false;
+            if (mx && (c[u] & 2) && plat) {  // cc_is_max of a plateau voxel
+                const uint32_t r = uf_find(PP, par);
+                if (cl[r] & 4) mx = false;
+                else if (ND == 3) par = r;
+                else listed = true;
+            }
+            const uint64_t m = __ballot(mx);
+            if (lane == 0 && w0 + u < wend) fseed[B.fbase + w0 + u] = m;
+            if (mx) PF[gi[u]] = par;
+            if (ND == 2) {
+                const uint64_t lm = __ballot(listed);
+                if (lm) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(&st._u, (uint32_t)__popcll(lm));
+                    base = (uint32_t)__shfl((int)base, 0);
+                    if (listed) plist[B.base + base + __popcll(lm & ((1ull << lane) - 1ull))] = par;
+                }
+            }
+        }
+    }
+}
+template __global__ void k_seed_members<2>(const BlockDesc*, BlockStat*, const uint8_t*, const uint32_t*, uint32_t*,
+                                           uint64_t*, uint32_t*);
+template __global__ void k_seed_members<3>(const BlockDesc*, BlockStat*, const uint8_t*, const uint32_t*, uint32_t*,
+                                           uint64_t*, uint32_t*);
+
+// 2-D: the listed plateau maxima united with their 4-adjacent backward maxima (x - 1, y - 1 in
+// the slice) by scan key, so each seed component is rooted at its first voxel in scan order as by
+// the tile CC
+__global__ void __launch_bounds__(256) k_seed_union2(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     const uint8_t* __restrict__ cls, const uint32_t* __restrict__ Pp,
+                                                     const uint32_t* __restrict__ plist, uint32_t* __restrict__ PFg) {
+    const BlockDesc& B = D[blockIdx.y];
+    const BlockStat& st = S[blockIdx.y];
+    if (!st.active) return;
+    const uint8_t* cl = cls + B.base;
+    const uint32_t* PP = Pp + B.base;
+    uint32_t* PF = PFg + B.base;
+    auto plat_max = [&](uint32_t i) {
+        const uint8_t c = cl[i];
+        return !(c & 1) && (c & 2) && !(cl[uf_find(PP, i)] & 4);
+    };
+    const uint32_t n = st._u;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        const uint32_t i = plist[B.base + e];
+        const uint32_t x = i % (uint32_t)B.X, y = (i / (uint32_t)B.X) % (uint32_t)B.Y;
+        if (x > 0 && plat_max(i - 1)) uf_union_scan(PF, i, i - 1, B, 0);
+        if (y > 0 && plat_max(i - (uint32_t)B.X)) uf_union_scan(PF, i, i - (uint32_t)B.X, B, 0);
     }
 }
 

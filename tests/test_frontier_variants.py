@@ -33,8 +33,9 @@ VARIANTS = {
     # the size filter's regrow initialised by the scan of every voxel instead of the walk over
     # the removed segments (k_sf_sparse, the default for size_filter <= 64)
     'sf_scan': {'CTWS_SF_SPARSE': '0'},
-    # the 3-D seed components by the tile CC (k_tile_cc / k_tile_merge<3, CC_SEED>) instead of
-    # from the plateau CC's maximal plateaus (k_seed_members, the default)
+    # the seed components by the tile CC (k_tile_cc / k_tile_merge<.., CC_SEED>) instead of from
+    # the classes (k_seed_members: 3-D the plateau CC's maximal plateaus, 2-D maxima as roots and
+    # the listed plateau maxima united, k_seed_union2; the default)
     'seed_tilecc': {'CTWS_SEED_TILECC': '1'},
 }
 
