@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6 final (1/2): the whole GPU suite as the driver runs it, smoke(), then the default bench line.
 cd "${GRAFT_REPO_ROOT:-.}"
-O=gpurun_out/r06_final
+O=gpurun_out/${FINAL_DIR:-r06_final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1

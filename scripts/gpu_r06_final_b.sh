@@ -2,7 +2,7 @@
 # Round 6 final (2/2): single-stream rocprofv3 kernel traces of configs 3 / 4 / 5 (stage table +
 # trace roofline), then FETCH_SIZE / WRITE_SIZE passes of configs 3 / 4 (HBM bytes per stage).
 cd "${GRAFT_REPO_ROOT:-.}"
-O=gpurun_out/r06_final
+O=gpurun_out/${FINAL_DIR:-r06_final}
 mkdir -p $O
 export TMPDIR=/tmp
 for c in ${TRACE_CONFIGS:-3 4 5}; do

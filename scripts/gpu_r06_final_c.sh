@@ -2,7 +2,7 @@
 # Round 6 final (3/3): rocprofv3 kernel stats of the default bench command (without the
 # end-to-end leg) and the SQ issue / stall counters of one single-stream config-3 step.
 cd "${GRAFT_REPO_ROOT:-.}"
-O=gpurun_out/r06_final
+O=gpurun_out/${FINAL_DIR:-r06_final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/prof_default -o run --output-format csv -- python3 -u bench.py --no-e2e > $O/bench_prof.json 2> $O/bench_prof.err || { tail -5 $O/bench_prof.err; exit 1; }
