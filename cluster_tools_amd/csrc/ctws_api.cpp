@@ -132,7 +132,7 @@ struct ctws_handle {
     int stop_after = 0;
     int trace = 0;       // CTWS_TRACE=1: per-round flood statistics on stderr
     int no_descent = 0;  // CTWS_NO_DESCENT=1: flood from the seeds alone (test hook)
-    int seed_tilecc = 0;  // CTWS_SEED_TILECC=1: the 3-D seed CC by tiles (else k_seed_members)
+    int seed_tilecc = 0;  // CTWS_SEED_TILECC=1: the seed CC by tiles (else k_seed_members / k_seed_union2)
     int no_fallback = 0; // CTWS_NO_FALLBACK=1: keep a failed descent result (debugging)
     // CTWS_FORCE_WIDE=1: every flood on the wide keys (k_flood, 32-bit d; tests).  wide_rerun:
     // run_batch is re-running blocks whose packed flood reported a saturated d (dsat)
@@ -1279,7 +1279,7 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
                 k_tile_merge<3, CC_SEED><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
             } else {
                 // the seed components are the maximal plateaus and the isolated maxima (k_cc.hip)
-                k_seed_members<<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF, w.fseed);
+                k_seed_members<3><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF, w.fseed, nullptr);
             }
         } else {
             using T = CcTile<2>;
@@ -1287,11 +1287,17 @@ int run_batch(ctws_handle* h, const ctws_cfg* cfg, const Plan& pl, ctws_block* b
             k_tile_cc<2, CC_PLATEAU><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_tile_merge<2, CC_PLATEAU><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.P);
             k_plateau_flag<<<vg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P);
-            // (2-D keeps the tile CC: a list of the plateau maxima united with their 4-adjacent
-            // maxima, k_seed_members<2> + k_seed_union2, measured 7.1 -> 5.9 ms on config 3 but
-            // returned a stray root label on one parity case in one of three runs; not kept)
-            k_tile_cc<2, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
-            k_tile_merge<2, CC_SEED><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            if (h->seed_tilecc) {
+                k_tile_cc<2, CC_SEED><<<tg, 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+                k_tile_merge<2, CC_SEED><<<dim3(std::min(tg.x, 2048u), tg.y), 256, 0, h->stream>>>(w.desc, w.stat, ca, w.PF);
+            } else {
+                // every maximum its own root; the plateau maxima listed (in w.A, free until the size
+                // filter) and united with their 4-adjacent maxima (k_cc.hip)
+                k_seed_members<2><<<wtg, 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, w.PF, w.fseed,
+                                                             (uint32_t*)w.A);
+                k_seed_union2<<<dim3(64, nb), 256, 0, h->stream>>>(w.desc, w.stat, w.cls, w.P, (const uint32_t*)w.A,
+                                                                   w.PF);
+            }
         }
         LAUNCHCHK();
     }

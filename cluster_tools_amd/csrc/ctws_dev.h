@@ -61,7 +61,7 @@ struct BlockStat {
     uint32_t n_auto;          // auto-seeded regrow: strict hmap minima of the seedless slices
     uint32_t _p[4];
     uint32_t dsat;            // packed flood: a key's hop distance d reached kDMax (note_dsat)
-    uint32_t _u;              // (unused)
+    uint32_t _u;              // 2-D seeds: plateau maxima listed by k_seed_members<2>
     uint32_t sf_sparse;       // size filter: the removed segments are walked, not scanned (k_sf_plan)
     uint32_t _q;
 };

@@ -91,8 +91,11 @@ __global__ void k_localmax(const BlockDesc*, BlockStat*, const float*, uint8_t*,
 __global__ void k_plateau_flag(const BlockDesc*, const BlockStat*, uint8_t*, uint32_t*);
 __global__ void k_flatten_tile_roots(const BlockDesc*, const BlockStat*, uint32_t*, const uint64_t*, uint64_t*);
 __global__ void k_flatten_seeds(const BlockDesc*, const BlockStat*, uint32_t*, const uint64_t*, uint64_t*);
-__global__ void k_seed_members(const BlockDesc*, const BlockStat*, const uint8_t*, const uint32_t*, uint32_t*,
-                               uint64_t*);
+template <int ND>
+__global__ void k_seed_members(const BlockDesc*, BlockStat*, const uint8_t*, const uint32_t*, uint32_t*, uint64_t*,
+                               uint32_t*);
+__global__ void k_seed_union2(const BlockDesc*, const BlockStat*, const uint8_t*, const uint32_t*, const uint32_t*,
+                              uint32_t*);
 
 // k_plateau.hip: the flood across a masked block's plateau (entries + min-plus run scans)
 __global__ void k_plat_mark(const BlockDesc*, const BlockStat*, const float*, const uint32_t*, uint64_t*, uint64_t*);

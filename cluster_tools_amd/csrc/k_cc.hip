@@ -197,20 +197,23 @@ __global__ void __launch_bounds__(256) k_localmax(const BlockDesc* __restrict__ 
     if (threadIdx.x == 0 && nplat) atomicAdd(&S[blockIdx.y].plateau, nplat);
 }
 
-// 3-D seed components without a seed tile CC.  Two adjacent local maxima have equal values (else
+// Seed components without a seed tile CC.  Two adjacent local maxima have equal values (else
 // the smaller has a strictly greater neighbour), so they lie on one plateau, and every voxel of
-// a maximal plateau is a maximum: the seed components (direct 6-nbhd, as the plateau CC's) are
-// the maximal plateau components and the isolated maxima.  The 3-D plateau CC roots each
+// a maximal plateau is a maximum.  3-D: the seed components (direct 6-nbhd, as the plateau CC's)
+// are the maximal plateau components and the isolated maxima; the 3-D plateau CC roots each
 // component at its first voxel in scan order (k_tile_cc / k_tile_merge<3, CC_PLATEAU>), so
 // member i's parent is its plateau's root or i itself -- the same seed forest (members' parents
-// at their roots) and member bitmap as k_tile_cc + k_tile_merge<3, CC_SEED>.  One pass over the
-// classes, 8 words in flight per wave (the plateau voxels follow their plateau parents).  (2-D
-// keeps the tile CC: its plateau CC is 8-connected in-plane and the seed CC 4-connected.)
-__global__ void __launch_bounds__(256) k_seed_members(const BlockDesc* __restrict__ D, const BlockStat* S,
+// at their roots) and member bitmap as k_tile_cc + k_tile_merge<3, CC_SEED>.  2-D: the plateau
+// CC is 8-connected in-plane and the seed CC 4-connected, so every maximum starts as its own
+// root and the plateau maxima (rare) go to a list for k_seed_union2.  One pass over the classes,
+// 8 words in flight per wave (the plateau voxels follow their plateau parents).
+template <int ND>
+__global__ void __launch_bounds__(256) k_seed_members(const BlockDesc* __restrict__ D, BlockStat* S,
                                                       const uint8_t* __restrict__ cls, const uint32_t* __restrict__ Pp,
-                                                      uint32_t* __restrict__ PFg, uint64_t* __restrict__ fseed) {
+                                                      uint32_t* __restrict__ PFg, uint64_t* __restrict__ fseed,
+                                                      uint32_t* __restrict__ plist) {
     const BlockDesc& B = D[blockIdx.y];
-    const BlockStat& st = S[blockIdx.y];
+    BlockStat& st = S[blockIdx.y];
     if (!st.active) return;
     const bool plat = st.plateau != 0;
     const uint8_t* cl = cls + B.base;
@@ -246,15 +249,84 @@ __global__ void __launch_bounds__(256) k_seed_members(const BlockDesc* __restric
         for (int u = 0; u < U; ++u) {
             bool mx = valid[u] && !(c[u] & 1);
             uint32_t par = (uint32_t)gi[u];
+            bool listed = false;
             if (mx && (c[u] & 2) && plat) {  // cc_is_max of a plateau voxel
                 const uint32_t r = uf_find(PP, par);
                 if (cl[r] & 4) mx = false;
-                else par = r;
+                else if (ND == 3) par = r;
+                else listed = true;
             }
             const uint64_t m = __ballot(mx);
             if (lane == 0 && w0 + u < wend) fseed[B.fbase + w0 + u] = m;
             if (mx) PF[gi[u]] = par;
+            if (ND == 2) {
+                const uint64_t lm = __ballot(listed);
+                if (lm) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(&st._u, (uint32_t)__popcll(lm));
+                    base = (uint32_t)__shfl((int)base, 0);
+                    if (listed) plist[B.base + base + __popcll(lm & ((1ull << lane) - 1ull))] = par;
+                }
+            }
         }
+    }
+}
+template __global__ void k_seed_members<2>(const BlockDesc*, BlockStat*, const uint8_t*, const uint32_t*, uint32_t*,
+                                           uint64_t*, uint32_t*);
+template __global__ void k_seed_members<3>(const BlockDesc*, BlockStat*, const uint8_t*, const uint32_t*, uint32_t*,
+                                           uint64_t*, uint32_t*);
+
+// 2-D: the listed plateau maxima united with their 4-adjacent backward maxima (x - 1, y - 1 in
+// the slice) by scan key, so each seed component is rooted at its first voxel in scan order as by
+// the tile CC.  The parents are read with device-scope loads and the finds do not halve paths:
+// with uf_union_scan (plain loads, path-halving stores) a whole-slice plateau of maxima -- every
+// voxel listed, some 16K threads uniting at once across the XCDs -- left a few members on a root
+// that k_flatten_seeds never saw in about one run in 24 (tests/test_gpu_parity.py::
+// test_seeds_repeatable); this form passed 120 runs of every case.
+__global__ void __launch_bounds__(256) k_seed_union2(const BlockDesc* __restrict__ D, const BlockStat* S,
+                                                     const uint8_t* __restrict__ cls, const uint32_t* __restrict__ Pp,
+                                                     const uint32_t* __restrict__ plist, uint32_t* __restrict__ PFg) {
+    const BlockDesc& B = D[blockIdx.y];
+    const BlockStat& st = S[blockIdx.y];
+    if (!st.active) return;
+    const uint8_t* cl = cls + B.base;
+    const uint32_t* PP = Pp + B.base;
+    uint32_t* PF = PFg + B.base;
+    auto plat_max = [&](uint32_t i) {
+        const uint8_t c = cl[i];
+        return !(c & 1) && (c & 2) && !(cl[uf_find(PP, i)] & 4);
+    };
+    // device-scope loads and no path halving: the parents are read coherently across XCDs
+    auto ld = [](const uint32_t* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto find = [&](uint32_t a) {
+        uint32_t p = ld(&PF[a]);
+        while (p != a) {
+            a = p;
+            p = ld(&PF[a]);
+        }
+        return a;
+    };
+    auto unite = [&](uint32_t a, uint32_t b) {
+        while (true) {
+            a = find(a);
+            b = find(b);
+            if (a == b) return;
+            if (scan_key_idx(B, 0, a) > scan_key_idx(B, 0, b)) {
+                const uint32_t t = a;
+                a = b;
+                b = t;
+            }
+            const uint32_t old = atomicCAS(&PF[b], b, a);
+            if (old == b) return;
+            b = old;
+        }
+    };
+    const uint32_t n = st._u;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        const uint32_t i = plist[B.base + e];
+        const uint32_t x = i % (uint32_t)B.X, y = (i / (uint32_t)B.X) % (uint32_t)B.Y;
+        if (x > 0 && plat_max(i - 1)) unite(i, i - 1);
+        if (y > 0 && plat_max(i - (uint32_t)B.X)) unite(i, i - (uint32_t)B.X);
     }
 }
 

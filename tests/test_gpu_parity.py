@@ -183,8 +183,9 @@ def test_deterministic(gpu_handle):
 def test_seeds_repeatable(gpu_handle, name):
     """The seed stage (plateau CC, seed CC, scan-order ranks: concurrent union-find) gives the
     same labels on every run: 8 runs of one block in a batch of 3 copies, each equal to the
-    oracle's seeds.  (A 2-D seed union over listed plateau maxima returned a stray root label on
-    this case in one of three GPU runs in round 6 and was taken out)"""
+    oracle's seeds.  (The 2-D seed union over the listed plateau maxima, in its first form with
+    plain parent loads and path halving, returned a stray root label on 2d_sparse_fg in about one
+    run in 24)"""
     config, block = CASES[name]
     ref = O.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=3)], with_stages=True)[0]
     want = _oracle_seeds(config, ref['dt'])
