@@ -201,6 +201,22 @@ def test_seeds_repeatable(gpu_handle, name):
         gpu_handle.debug_set_stop(0)
 
 
+@pytest.mark.parametrize('name', ['2d_sparse_fg', '3d_sparse_fg', '3d_plateaus', '2d_empty_slice', '3d_mask_halo',
+                                  '2d_sizefilter_noise_halo'])
+def test_pipeline_repeatable(gpu_handle, name):
+    """The whole block (plateau / seed / crop CCs: global union-find merges across workgroups,
+    the flood's fixpoint, the size filter) gives the same uint64 output on every run: 8 runs of a
+    batch of 3 copies of the block."""
+    config, block = CASES[name]
+    first = None
+    for _ in range(int(os.environ.get('CTWS_TEST_REPS', '8'))):
+        res = gpu_handle.ws_blocks(config, BLOCK_SHAPE, [dict(block, block_id=3) for _ in range(3)])
+        for r in res:
+            if first is None:
+                first = r['output'].copy()
+            np.testing.assert_array_equal(r['output'], first)
+
+
 def test_config2_block_full_size(gpu_handle):
     """One full 64x256x256 block of the bench workload against the oracle."""
     from cluster_tools_amd.synthetic import boundary_map
